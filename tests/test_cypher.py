@@ -1,0 +1,173 @@
+"""Cypher-subset semantics on small graphs, checked against brute-force oracles."""
+import itertools
+
+import networkx as nx
+import numpy as np
+import pytest
+
+from k8s_llm_rca_amd.graph import native
+from k8s_llm_rca_amd.graph.cypher import Executor, parse
+from k8s_llm_rca_amd.graph.model import CypherSyntaxError
+from k8s_llm_rca_amd.graph.schema import build_metagraph
+from k8s_llm_rca_amd.graph.store import PropertyGraph
+from k8s_llm_rca_amd.pipeline import find_metapath as FM
+
+
+def _toy():
+    g = PropertyGraph()
+    a = g.add_node("K", {"kind": "A"})
+    b = g.add_node("K", {"kind": "B"})
+    c = g.add_node("K", {"kind": "C"})
+    d = g.add_node("K", {"kind": "Namespace"})
+    g.add_edge(a, b, "R", {"key": "ab"})
+    g.add_edge(b, c, "R", {"key": "bc"})
+    g.add_edge(a, c, "R", {"key": "ac"})
+    g.add_edge(c, a, "S", {"key": "ca"})
+    g.add_edge(a, d, "R", {"key": "ns"})
+    g.add_edge(c, d, "R", {"key": "ns"})
+    return g.finalize()
+
+
+def kinds(path):
+    return [n["kind"] for n in path.nodes]
+
+
+def test_directed_and_min_len():
+    ex = Executor(_toy())
+    r = ex.run(FM.Q_DIRECTED, {"srcKind": "A", "destKind": "C", "intermediateKinds": []})
+    got = sorted(tuple(kinds(x["path"])) for x in r)
+    assert got == [("A", "B", "C"), ("A", "C")]
+
+
+def test_interior_predicate_excludes_one_hop():
+    ex = Executor(_toy())
+    r = ex.run(FM.Q_DIRECTED, {"srcKind": "A", "destKind": "C", "intermediateKinds": ["B"]})
+    assert [kinds(x["path"]) for x in r] == [["A", "B", "C"]]
+
+
+def test_undirected_and_namespace_excluded():
+    ex = Executor(_toy())
+    r = ex.run(FM.Q_UNDIRECTED, {"srcKind": "C", "destKind": "A", "intermediateKinds": []})
+    paths = sorted(tuple(kinds(x["path"])) for x in r)
+    # C-A via R(ac) and S(ca); C-B-A; never through Namespace
+    assert ("C", "A") in paths and ("C", "B", "A") in paths
+    assert all("Namespace" not in p for p in paths)
+    assert sum(1 for p in paths if p == ("C", "A")) == 2
+
+
+def test_namespace_cascade_query():
+    ex = Executor(_toy())
+    r = ex.run(FM.Q_NAMESPACE, {"srcKind": "A", "destKind": "C"})
+    assert [kinds(x["path"]) for x in r] == [["A", "Namespace", "C"]]
+
+
+def test_record_contract():
+    ex = Executor(_toy())
+    r = ex.run("MATCH (n:K) WHERE n.kind = 'A' RETURN n.kind, n AS node")
+    assert r[0]["n.kind"] == "A" and r[0][0] == "A" and len(r[0]) == 2
+    assert r[0]["node"]["missing"] is None
+    assert list(r[0].keys()) == ["n.kind", "node"]
+
+
+def test_three_valued_logic_and_in():
+    ex = Executor(_toy())
+    assert ex.run("MATCH (n) WHERE n.nope = 1 RETURN n") == []
+    assert ex.run("MATCH (n) WHERE NOT n.nope = 1 RETURN n") == []
+    r = ex.run("MATCH (n) WHERE n.nope IS NULL AND n.kind IN ['A','B'] RETURN n.kind ORDER BY n.kind DESC")
+    assert [x[0] for x in r] == ["B", "A"]
+    r = ex.run("RETURN [1,2,3][1..-1] AS s, size([1,2]) AS n, null IN [1] AS x, 2 IN [1, null] AS y")
+    assert r[0]["s"] == [2] and r[0]["n"] == 2 and r[0]["x"] is None and r[0]["y"] is None
+
+
+def test_rel_uniqueness_within_match():
+    ex = Executor(_toy())
+    r = ex.run("MATCH (a)-[r1]-(b)-[r2]-(c) WHERE a.kind = 'A' AND c.kind = 'A' RETURN r1, r2")
+    assert all(x["r1"] != x["r2"] for x in r)
+
+
+def test_aggregation_and_distinct():
+    ex = Executor(_toy())
+    r = ex.run("MATCH (a)-[r]->(b) RETURN a.kind AS k, count(*) AS c ORDER BY k")
+    assert [(x["k"], x["c"]) for x in r] == [("A", 3), ("B", 1), ("C", 2)]
+    r = ex.run("MATCH (a)-[r:R]->(b) RETURN DISTINCT r.key AS key ORDER BY key")
+    assert [x[0] for x in r] == ["ab", "ac", "bc", "ns"]
+
+
+def test_with_limit_and_case_insensitive_keywords():
+    ex = Executor(_toy())
+    r = ex.run("match (n:K) with n limit 1 match (n)-[r:R]->(m) where r.key = 'ab' return m.kind;")
+    assert [x[0] for x in r] == ["B"]
+
+
+@pytest.mark.parametrize("q", [
+    "MATCH (n RETURN n", "MATCH (n) RETURN", "MATCH (n)-[r]->(m)", "CREATE (n) RETURN n",
+    "MATCH (n) WHERE n.x = RETURN n", "RETURN 1 2",
+])
+def test_syntax_errors(q):
+    with pytest.raises(CypherSyntaxError):
+        parse(q)
+
+
+def test_metagraph_paths_vs_networkx():
+    mg = build_metagraph()
+    ex = Executor(mg)
+    G = nx.MultiDiGraph()
+    for e in range(mg.num_edges):
+        G.add_edge(int(mg.e_src[e]), int(mg.e_dst[e]), key=e)
+    kind = mg.node_column("kind")
+    for src, dst in [("Pod", "nfs"), ("Pod", "Secret"), ("StatefulSet", "ResourceQuota")]:
+        r = ex.run(FM.Q_DIRECTED, {"srcKind": src, "destKind": dst, "intermediateKinds": []})
+        got = sorted(tuple(n.id for n in x["path"].nodes) for x in r)
+        s = int(np.nonzero(kind == src)[0][0])
+        t = int(np.nonzero(kind == dst)[0][0])
+        exp = []
+        for p in nx.all_simple_paths(nx.DiGraph(G), s, t, cutoff=3):
+            if any(kind[n] in ("Event", "Namespace") for n in p):
+                continue
+            mult = 1
+            for u, v in zip(p[:-1], p[1:]):
+                mult *= G.number_of_edges(u, v)
+            exp += [tuple(p)] * mult
+        assert got == sorted(exp), (src, dst)
+
+
+def test_native_matches_numpy():
+    if not native.have_native():
+        pytest.skip("native _graphcore not built")
+    rng = np.random.default_rng(0)
+    n, e = 200, 1500
+    src = rng.integers(0, n, e)
+    dst = rng.integers(0, n, e)
+    a = native.build_csr(n, src, dst)
+    b = native.build_csr_np(n, src, dst)
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+    et = rng.integers(0, 3, e).astype(np.int32)
+    ek = rng.integers(-1, 4, e).astype(np.int32)
+    ids = rng.integers(0, n, 50)
+    for tids, kid in [(None, -2), (np.array([1], np.int32), -2), (np.array([0, 2], np.int32), 3)]:
+        r1 = native.expand(a[0], a[1], a[2], ids, et, ek, tids, kid)
+        r2 = native.expand_np(a[0], a[1], a[2], ids, et, ek, tids, kid)
+        for x, y in zip(r1, r2):
+            assert np.array_equal(x, y)
+    offs = np.array([0, 5, 5, 12], dtype=np.int64)
+    buf = np.frombuffer(b"helloabcdefg", dtype=np.uint8).copy()
+    ids = np.array([0, 1, 2, 2, 0])
+    for nd in [b"ll", b"", b"efg", b"x", b"abcdefg", b"abcdefgh"]:
+        assert np.array_equal(native.substr_mask(offs, buf, ids, nd), native.substr_mask_np(offs, buf, ids, nd))
+
+
+def test_native_var_length_matches_numpy():
+    if not native.have_native():
+        pytest.skip("native _graphcore not built")
+    g = _toy()
+    starts = np.arange(g.num_nodes)
+    for d in ("out", "in", "both"):
+        core = native._core
+        a = sorted((r, tuple(n), tuple(e)) for r, n, e in native.var_length(g, starts, 1, 3, d, None))
+        native._core = None
+        try:
+            b = sorted((r, tuple(n), tuple(e)) for r, n, e in native.var_length(g, starts, 1, 3, d, None))
+        finally:
+            native._core = core
+        assert a == b, d

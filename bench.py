@@ -1,0 +1,16 @@
+#!/usr/bin/env python
+"""Headline benchmark: RCA analyses/s + p50 latency (Llama-3-8B backend, 10k-node graph).
+
+Contract: ``python bench.py --gpus N --steps K --warmup W``; multi-GPU runs are
+launched by torchrun (one rank per GPU, data-parallel engine replicas) and
+rank 0 prints ONE JSON line.  See k8s_llm_rca_amd/bench/rca_bench.py.
+"""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from k8s_llm_rca_amd.bench.rca_bench import main  # noqa: E402
+
+if __name__ == "__main__":
+    sys.exit(main())

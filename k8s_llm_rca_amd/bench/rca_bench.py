@@ -1,0 +1,199 @@
+"""RCA benchmark: analyses/s and p50 end-to-end latency (BASELINE.json headline).
+
+One *step* = a batch of ``incidents`` RCA analyses (locate -> generate query
+-> analyze, the full reference pipeline) run concurrently on this rank's
+engine against this rank's synthetic k8s graph.  Ranks are independent engine
+replicas (data parallel, one process per GPU, TP=1): per-GPU work is fixed as
+N grows (weak scaling).  Timing brackets exactly ``steps`` batches with a
+barrier + device synchronize on both sides and takes the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import logging
+import os
+import statistics
+import sys
+import time
+from typing import Any, Dict, List, Optional
+
+import torch
+
+REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
+
+
+def _dist_init():
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world > 1 and not dist.is_initialized():
+        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        if backend == "nccl":
+            torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
+        dist.init_process_group(backend)
+    rank = dist.get_rank() if world > 1 else 0
+    return world, rank
+
+
+def _barrier(world: int, device):
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize(device)
+
+
+def _allreduce_max(x: float, world: int, device) -> float:
+    if world == 1:
+        return x
+    import torch.distributed as dist
+    t = torch.tensor([x], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def _allgather_list(xs: List[float], world: int, device) -> List[float]:
+    if world == 1:
+        return xs
+    import torch.distributed as dist
+    out: List[Any] = [None] * world
+    dist.all_gather_object(out, xs)
+    return [v for part in out for v in part]
+
+
+def run(args) -> Optional[Dict[str, Any]]:
+    logging.basicConfig(level=logging.WARNING)
+    world, rank = _dist_init()
+    if args.gpus and world > 1 and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    cuda = torch.cuda.is_available() and args.device != "cpu"
+    device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}" if cuda else "cpu")
+    if cuda:
+        torch.cuda.set_device(device)
+
+    from ..api.graph import GraphQueryExecutor
+    from ..api.service import AssistantService
+    from ..engine.backend import EngineBackend
+    from ..engine.engine import EngineConfig, LLMEngine
+    from ..graph.synth import generate_cluster
+    from ..pipeline.formats import GenerationBudget
+    from ..pipeline.rca import RCAConfig, RCAPipeline, run_batch
+    from ..utils import tracing
+
+    n_steps, n_warm, per_step = args.steps, args.warmup, args.incidents
+    t_setup = time.perf_counter()
+    cluster = generate_cluster(args.graph_nodes, per_step * (n_steps + n_warm), seed=args.seed + 7919 * rank)
+    if cuda and args.graph_device:
+        from ..graph.device import to_device
+        to_device(cluster.stategraph, device)
+    eng = LLMEngine(EngineConfig(model=args.model, device=str(device),
+                                 dtype=torch.bfloat16 if cuda else torch.float32,
+                                 kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,
+                                 use_graphs=cuda and not args.no_graphs, seed=args.seed + rank,
+                                 num_blocks=None if cuda else 512))
+    eng.start()
+    svc = AssistantService(EngineBackend(eng, temperature=args.temperature))
+    budget = GenerationBudget(semantic_tokens=args.semantic_tokens, explanation_tokens=args.explanation_tokens,
+                              conclusion_tokens=args.conclusion_tokens, resolution_tokens=args.resolution_tokens)
+    cfg = RCAConfig(model=args.model, hints=not args.no_hints, budget=budget)
+    meta_qe = GraphQueryExecutor(cluster.metagraph)
+    state_qe = GraphQueryExecutor(cluster.stategraph)
+    pipelines = [RCAPipeline(svc, meta_qe, state_qe, cfg) for _ in range(per_step)]
+    setup_s = time.perf_counter() - t_setup
+
+    incidents = cluster.incidents
+    lat: List[float] = []
+    errors: List[str] = []
+    n_done = 0
+    for w in range(n_warm):
+        chunk = incidents[w * per_step:(w + 1) * per_step]
+        st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
+        errors += st.errors
+    tracing.reset()
+    stats0 = dict(eng.stats)
+    _barrier(world, device)
+    t0 = time.perf_counter()
+    for s in range(n_steps):
+        chunk = incidents[(n_warm + s) * per_step:(n_warm + s + 1) * per_step]
+        st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
+        lat += st.latencies
+        errors += st.errors
+        n_done += len(st.results)
+    _barrier(world, device)
+    elapsed = time.perf_counter() - t0
+    eng.stop()
+    if eng.error is not None:
+        raise eng.error
+    max_elapsed = _allreduce_max(elapsed, world, device)
+    all_lat = _allgather_list(lat, world, device)
+    total = n_done * world
+    value = total / max_elapsed
+    d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    p50 = statistics.median(all_lat) if all_lat else 0.0
+    p90 = sorted(all_lat)[int(0.9 * (len(all_lat) - 1))] if all_lat else 0.0
+    res = {
+        "metric": "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-node graph",
+        "value": round(value, 4),
+        "unit": "analyses/s",
+        "n_gpus": world,
+        "steps": n_steps,
+        "warmup": n_warm,
+        "ms_per_step": round(1000.0 * max_elapsed / n_steps, 2),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": round(value / REF_MAX_ANALYSES_PER_S, 2),
+        "dtype": "bf16" if cuda else "fp32",
+        "data": "synthetic k8s stategraph (seeded generator, fault injection) + random-init weights",
+        "config": {"model": "Llama-3-8B" if args.model == "llama3-8b" else args.model,
+                   "global_batch": per_step * world, "seq_len": eng.max_context,
+                   "parallelism": f"dp{world}", "graph_nodes": cluster.stategraph.num_nodes,
+                   "incidents_per_gpu_per_step": per_step, "grammar_hints": not args.no_hints},
+        "p50_latency_s": round(p50, 3),
+        "p90_latency_s": round(p90, 3),
+        "errors": len(errors),
+        "engine": {"steps": d["steps"], "graph_steps": d["graph_steps"], "prefill_tokens": d["prefill_tokens"],
+                   "decode_tokens": d["decode_tokens"], "sampled_tokens": d["sampled_tokens"],
+                   "forced_tokens": d["forced_tokens"], "forward_s": round(d["forward_s"], 3),
+                   "sample_s": round(d["sample_s"], 3), "host_s": round(d["host_s"], 3),
+                   "evictions": d["evictions"], "requests": d["requests"]},
+        "setup_s": round(setup_s, 1),
+        "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
+    }
+    if world > 1:
+        import torch.distributed as dist
+        dist.barrier()
+    return res if rank == 0 else None
+
+
+def parser() -> argparse.ArgumentParser:
+    p = argparse.ArgumentParser(description=__doc__)
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=2)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--model", default="llama3-8b")
+    p.add_argument("--device", default="cuda")
+    p.add_argument("--incidents", type=int, default=64, help="concurrent RCA analyses per GPU per step")
+    p.add_argument("--graph-nodes", type=int, default=10_000)
+    p.add_argument("--graph-device", action="store_true", help="mirror the stategraph to HBM (HIP graph kernels)")
+    p.add_argument("--seed", type=int, default=0)
+    p.add_argument("--kv-gb", type=float, default=96.0)
+    p.add_argument("--max-batch-tokens", type=int, default=8192)
+    p.add_argument("--temperature", type=float, default=0.7)
+    p.add_argument("--semantic-tokens", type=int, default=192)
+    p.add_argument("--explanation-tokens", type=int, default=40)
+    p.add_argument("--conclusion-tokens", type=int, default=80)
+    p.add_argument("--resolution-tokens", type=int, default=80)
+    p.add_argument("--no-hints", action="store_true")
+    p.add_argument("--no-graphs", action="store_true")
+    return p
+
+
+def main(argv=None) -> int:
+    args = parser().parse_args(argv)
+    res = run(args)
+    if res is not None:
+        print(json.dumps(res), flush=True)
+    return 0

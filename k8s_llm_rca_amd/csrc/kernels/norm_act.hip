@@ -1,0 +1,170 @@
+// Memory-bound fused elementwise kernels (B2 RMSNorm, B8 SwiGLU, B3+B5 RoPE/KV write).
+// All loads/stores are 16-byte vectors (8 bf16); math in fp32.
+#include "common.h"
+
+namespace k8s {
+
+// ------------------------------------------------------------ RMSNorm (+add)
+// y = rmsnorm(x [+ res]) * w ; when res != nullptr, res <- x + res (bf16).
+// One workgroup per row; each thread keeps NC 8-element chunks in registers.
+template <int NC>
+__global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res,
+                                                      const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                      int H, int x_stride, int y_stride, float eps) {
+  __shared__ float scratch[16];
+  const int row = blockIdx.x;
+  const int nv = H >> 3;
+  const uint16_t* xr = x + (size_t)row * x_stride;
+  uint16_t* rr = res ? res + (size_t)row * H : nullptr;
+  float v[NC][8];
+  float ss = 0.f;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = threadIdx.x + c * 256;
+    if (i < nv) {
+      u16x8 a = *reinterpret_cast<const u16x8*>(xr + i * 8);
+      if (rr) {
+        u16x8 b = *reinterpret_cast<const u16x8*>(rr + i * 8);
+        u16x8 s;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = bf2f(a[j]) + bf2f(b[j]);
+          s[j] = f2bf(t);
+          v[c][j] = bf2f(s[j]);
+        }
+        *reinterpret_cast<u16x8*>(rr + i * 8) = s;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) v[c][j] = bf2f(a[j]);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j) ss += v[c][j] * v[c][j];
+    }
+  }
+  const float tot = block_sum(ss, scratch);
+  const float inv = rsqrtf(tot / (float)H + eps);
+  uint16_t* yr = y + (size_t)row * y_stride;
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = threadIdx.x + c * 256;
+    if (i < nv) {
+      u16x8 wv = *reinterpret_cast<const u16x8*>(w + i * 8);
+      u16x8 o;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[j]));
+      *reinterpret_cast<u16x8*>(yr + i * 8) = o;
+    }
+  }
+}
+
+// -------------------------------------------------------------- SiLU * up
+// gu: [T][2I] (gate | up)  ->  out: [T][I]
+__global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restrict__ gu, uint16_t* __restrict__ out,
+                                                       int T, int I) {
+  const int nv = I >> 3;
+  const size_t total = (size_t)T * nv;
+  for (size_t idx = blockIdx.x * (size_t)blockDim.x + threadIdx.x; idx < total; idx += (size_t)gridDim.x * blockDim.x) {
+    const size_t t = idx / nv, i = idx % nv;
+    u16x8 g = *reinterpret_cast<const u16x8*>(gu + t * 2 * I + i * 8);
+    u16x8 u = *reinterpret_cast<const u16x8*>(gu + t * 2 * I + I + i * 8);
+    u16x8 o;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float gv = bf2f(g[j]);
+      o[j] = f2bf(gv / (1.f + __expf(-gv)) * bf2f(u[j]));
+    }
+    *reinterpret_cast<u16x8*>(out + t * I + i * 8) = o;
+  }
+}
+
+// ------------------------------------------------------ RoPE + paged KV write
+// qkv: [T][ld] with q heads, then k heads, then v heads (128 dims each).
+// Rotates q and k in place (rotate-half / NeoX pairing i <-> i+64), writes
+// k -> K page [blk][h][off][:], v -> transposed V page [blk][h][:][off].
+// cos_sin: [max_pos][128] fp32 = cos[0..63] | sin[0..63].
+__global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv, int ld, const int* __restrict__ pos,
+                                                      const float* __restrict__ cos_sin,
+                                                      const int* __restrict__ slots, uint16_t* __restrict__ kc,
+                                                      uint16_t* __restrict__ vc, int nq, int nkv, int BS) {
+  const int t = blockIdx.x;
+  uint16_t* row = qkv + (size_t)t * ld;
+  const int p = pos[t];
+  const float* cs = cos_sin + (size_t)p * 128;
+  const int slot = slots ? slots[t] : -1;
+  const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
+  const int nrot = (nq + nkv) * 8;  // 8 threads per head, 8 pairs each
+  for (int i = threadIdx.x; i < nrot; i += blockDim.x) {
+    const int hd = i >> 3, c = (i & 7) * 8;
+    uint16_t* xp = row + hd * 128;
+    u16x8 lo = *reinterpret_cast<u16x8*>(xp + c);
+    u16x8 hi = *reinterpret_cast<u16x8*>(xp + 64 + c);
+    u16x8 olo, ohi;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float co = cs[c + j], si = cs[64 + c + j];
+      const float a = bf2f(lo[j]), b = bf2f(hi[j]);
+      olo[j] = f2bf(a * co - b * si);
+      ohi[j] = f2bf(b * co + a * si);
+    }
+    *reinterpret_cast<u16x8*>(xp + c) = olo;
+    *reinterpret_cast<u16x8*>(xp + 64 + c) = ohi;
+    if (hd >= nq && slot >= 0) {
+      const int kh = hd - nq;
+      uint16_t* kp = kc + (((size_t)blk * nkv + kh) * BS + off) * 128;
+      *reinterpret_cast<u16x8*>(kp + c) = olo;
+      *reinterpret_cast<u16x8*>(kp + 64 + c) = ohi;
+    }
+  }
+  if (slot < 0) return;
+  // V: nkv*128 values, transposed scatter into the page
+  const uint16_t* vrow = row + (nq + nkv) * 128;
+  for (int i = threadIdx.x; i < nkv * 16; i += blockDim.x) {
+    const int kh = i >> 4, d0 = (i & 15) * 8;
+    u16x8 v = *reinterpret_cast<const u16x8*>(vrow + kh * 128 + d0);
+    uint16_t* vp = vc + ((size_t)blk * nkv + kh) * 128 * BS + off;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) vp[(size_t)(d0 + j) * BS] = v[j];
+  }
+}
+
+}  // namespace k8s
+
+using namespace k8s;
+
+K8S_API int k8s_rmsnorm(const void* x, void* res, const void* w, void* y, int T, int H, int x_stride, int y_stride,
+                        float eps, hipStream_t s) {
+  if (H % 8) return (int)hipErrorInvalidValue;
+  const int nc = (H / 8 + 255) / 256;
+  const uint16_t* xx = (const uint16_t*)x;
+  uint16_t* rr = (uint16_t*)res;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  if (T <= 0) return 0;
+  switch (nc) {
+    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
+    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
+    case 3:
+    case 4: hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
+    default:
+      if (nc > 8) return (int)hipErrorInvalidValue;
+      hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps);
+  }
+  return (int)hipGetLastError();
+}
+
+K8S_API int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s) {
+  if (I % 8) return (int)hipErrorInvalidValue;
+  if (T <= 0) return 0;
+  const size_t total = (size_t)T * (I / 8);
+  const int grid = (int)std::min<size_t>((total + 255) / 256, 4096);
+  hipLaunchKernelGGL(silu_mul_kernel, dim3(grid), dim3(256), 0, s, (const uint16_t*)gu, (uint16_t*)out, T, I);
+  return (int)hipGetLastError();
+}
+
+K8S_API int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc,
+                        int T, int nq, int nkv, int BS, hipStream_t s) {
+  if (T <= 0) return 0;
+  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
+                     (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS);
+  return (int)hipGetLastError();
+}

@@ -1,0 +1,626 @@
+"""LLM engine: continuous batching over every active assistant run.
+
+Scheduling model (one step = one forward over a flattened token batch):
+
+* each conversation *thread* owns a :class:`Sequence` whose token list and KV
+  pages persist across runs -> a new run only prefills the newly appended
+  messages (per-thread prefix reuse; the reference re-sent the whole thread
+  to GPT-4 on every run, ``openai_generic_assistant.py:45-51``);
+* decode rows (one pending token) go first and use the split-KV decode kernel;
+  prefill rows (new prompt text, or literal text forced by the grammar --
+  "jump-forward") are chunked under ``max_batch_tokens`` and use the varlen
+  prefill kernel in the same step;
+* pure-decode steps replay a captured HIP graph per (batch bucket, KV
+  partition bucket), so Python/launch overhead is paid once per step;
+* sampling is one masked kernel over the logits rows (grammar allow-lists /
+  bitmaps), then each row's grammar state advances on the host;
+* when the KV pool runs dry, idle threads are evicted LRU (their tokens are
+  kept and re-prefilled on their next run).
+
+The engine runs in a background thread (:meth:`start`) or is stepped
+explicitly (:meth:`step`); :meth:`submit` is thread-safe.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, List, Optional, Sequence as Seq, Tuple
+
+import numpy as np
+import torch
+
+from ..models.config import ModelConfig, get_config
+from ..ops import attention as A
+from ..ops import sampling as SMP
+from ..parallel.groups import ParallelContext, single
+from ..utils import tracing
+from .kv_cache import KVPool
+from .structured import GrammarRuntime, GrammarState
+from .tokenizer import get_tokenizer
+
+log = logging.getLogger(__name__)
+
+PART_SIZE = 256
+
+
+@dataclass
+class EngineConfig:
+    model: str = "llama3-8b"
+    device: str = "cuda"
+    dtype: torch.dtype = torch.bfloat16
+    block_size: int = 64
+    num_blocks: Optional[int] = None
+    kv_mem_fraction: float = 0.85
+    kv_max_gb: Optional[float] = None
+    max_batch_tokens: int = 8192
+    max_decode_seqs: int = 256
+    max_context: Optional[int] = None
+    use_graphs: bool = True
+    graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
+    seed: int = 0
+    temperature: float = 0.7
+    use_hints: bool = True
+    model_overrides: dict = field(default_factory=dict)
+
+
+class Request:
+    __slots__ = ("seq", "gs", "max_new", "temperature", "seed", "on_done", "n_prompt", "generated", "mask",
+                 "t_submit", "t_first", "n_forced", "n_sampled", "cancelled")
+
+    def __init__(self, seq, gs, max_new, temperature, seed, on_done, n_prompt):
+        self.seq = seq
+        self.gs: GrammarState = gs
+        self.max_new = max_new
+        self.temperature = temperature
+        self.seed = seed
+        self.on_done = on_done
+        self.n_prompt = n_prompt
+        self.generated: List[int] = []
+        self.mask = None
+        self.t_submit = time.perf_counter()
+        self.t_first = None
+        self.n_forced = 0
+        self.n_sampled = 0
+        self.cancelled = False
+
+
+class Sequence:
+    __slots__ = ("id", "tokens", "n_cached", "blocks", "req", "last_used")
+
+    def __init__(self, sid: int):
+        self.id = sid
+        self.tokens: List[int] = []
+        self.n_cached = 0
+        self.blocks: List[int] = []
+        self.req: Optional[Request] = None
+        self.last_used = 0.0
+
+    @property
+    def pending(self) -> int:
+        return len(self.tokens) - self.n_cached
+
+
+def _build_model(mc: ModelConfig, device, dtype, pc, seed):
+    if mc.arch == "opt":
+        from ..models.opt import OPTModel
+        return OPTModel(mc, device, dtype, seed=seed)
+    from ..models.llama import LlamaModel
+    return LlamaModel(mc, device, dtype, pc, seed=seed)
+
+
+class LLMEngine:
+    def __init__(self, cfg: EngineConfig, pc: Optional[ParallelContext] = None, model=None):
+        self.cfg = cfg
+        self.pc = pc or single()
+        self.device = torch.device(cfg.device)
+        self.mc = get_config(cfg.model, **cfg.model_overrides)
+        self.max_context = cfg.max_context or self.mc.max_position
+        t0 = time.perf_counter()
+        self.model = model or _build_model(self.mc, self.device, cfg.dtype, self.pc, cfg.seed)
+        self.t_model_init = time.perf_counter() - t0
+        self.tok = get_tokenizer()
+        self.vocab = min(self.mc.vocab_size, max(self.tok.vocab_size, 1))
+        self.grt = GrammarRuntime(self.tok, self.mc.vocab_size)
+        self.eos_ids = [self.tok.eot_id, self.tok.eos_id]
+        BS = cfg.block_size
+        nkv, D = self.model.nkv, self.model.D
+        nb = cfg.num_blocks
+        if nb is None:
+            per = KVPool.bytes_per_block(self.mc.n_layers, nkv, D, BS)
+            if self.device.type == "cuda":
+                free, _ = torch.cuda.mem_get_info(self.device)
+                budget = free * cfg.kv_mem_fraction - self._workspace_bytes()
+            else:
+                budget = 2 << 30
+            if cfg.kv_max_gb is not None:
+                budget = min(budget, cfg.kv_max_gb * (1 << 30))
+            nb = max(16, int(budget // per))
+        self.kv = KVPool(self.mc.n_layers, nkv, D, nb, BS, self.device, cfg.dtype)
+        self.max_blocks_per_seq = (self.max_context + BS - 1) // BS + 1
+        self.seqs: Dict[int, Sequence] = {}
+        self._next_sid = 0
+        self._incoming: List[tuple] = []
+        self._lock = threading.Lock()
+        self._cv = threading.Condition(self._lock)
+        self._thread: Optional[threading.Thread] = None
+        self._stop = False
+        self._mask_dev: Optional[torch.Tensor] = None
+        self._mask_ver = -1
+        self._graphs: Dict[tuple, tuple] = {}
+        self._graph_pool = None
+        self._static = None
+        self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
+                      "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
+                      "evictions": 0, "requests": 0}
+        self.error: Optional[BaseException] = None
+
+    def _workspace_bytes(self) -> int:
+        mc = self.mc
+        t = self.cfg.max_batch_tokens
+        act = t * (mc.hidden * 8 + (mc.q_size + 2 * mc.kv_size) * 2 + mc.intermediate * 6)
+        if mc.n_experts:
+            act += t * mc.top_k * (mc.hidden * 4 + mc.intermediate * 6)
+        logits = self.cfg.max_decode_seqs * mc.vocab_size * 4
+        return int(act + logits + (4 << 30))
+
+    # ------------------------------------------------------------------ API
+    def new_sequence(self) -> int:
+        with self._lock:
+            sid = self._next_sid
+            self._next_sid += 1
+            self.seqs[sid] = Sequence(sid)
+        return sid
+
+    def release_sequence(self, sid: int) -> None:
+        with self._lock:
+            s = self.seqs.pop(sid, None)
+        if s is not None:
+            self.kv.release(s.blocks)
+
+    def submit(self, sid: int, tokens: List[int], grammar=None, max_new: int = 256,
+               temperature: Optional[float] = None, seed: int = 0,
+               on_done: Optional[Callable[[List[int], Dict[str, float]], None]] = None) -> None:
+        """Set sequence ``sid``'s desired token list (prompt) and generate a reply."""
+        with self._cv:
+            self._incoming.append((sid, list(tokens), grammar, max_new,
+                                   self.cfg.temperature if temperature is None else temperature, seed, on_done))
+            self._cv.notify()
+
+    def start(self) -> None:
+        if self._thread is not None:
+            return
+        self._stop = False
+        self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
+        self._thread.start()
+
+    def stop(self) -> None:
+        with self._cv:
+            self._stop = True
+            self._cv.notify()
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    def _loop(self) -> None:
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
+        while True:
+            with self._cv:
+                while not self._stop and not self._incoming and not self._has_work():
+                    self._cv.wait(0.05)
+                if self._stop:
+                    return
+            try:
+                self.step()
+            except BaseException as e:  # surface engine faults as failed runs, never a hang
+                log.exception("engine step failed")
+                self.error = e
+                self._fail_all(repr(e))
+
+    def _fail_all(self, err: str) -> None:
+        for s in list(self.seqs.values()):
+            r = s.req
+            if r is not None:
+                s.req = None
+                s.n_cached = 0
+                self.kv.release(s.blocks)
+                s.blocks = []
+                if r.on_done:
+                    r.on_done(None, {"error": err})
+
+    def _has_work(self) -> bool:
+        return any(s.req is not None for s in self.seqs.values())
+
+    def run_until_idle(self, max_steps: int = 1_000_000) -> None:
+        for _ in range(max_steps):
+            if not self.step():
+                return
+
+    # ---------------------------------------------------------------- steps
+    def _admit(self) -> None:
+        with self._lock:
+            inc, self._incoming = self._incoming, []
+        for sid, toks, grammar, max_new, temp, seed, on_done in inc:
+            s = self.seqs[sid]
+            if s.req is not None:
+                raise RuntimeError(f"sequence {sid} already has an active request")
+            # longest common prefix with what is cached -> keep that KV
+            lcp = 0
+            n = min(s.n_cached, len(toks))
+            cur = s.tokens
+            while lcp < n and cur[lcp] == toks[lcp]:
+                lcp += 1
+            s.tokens = toks
+            s.n_cached = lcp
+            keep = (lcp + self.kv.block_size - 1) // self.kv.block_size
+            if len(s.blocks) > keep:
+                self.kv.release(s.blocks[keep:])
+                s.blocks = s.blocks[:keep]
+            gs = GrammarState(self.grt, grammar, self.eos_ids, max_tokens=max_new, use_hints=self.cfg.use_hints)
+            r = Request(s, gs, max_new, temp, seed, on_done, len(toks))
+            s.req = r
+            self.stats["requests"] += 1
+            self._drive(r)
+
+    def _drive(self, r: Request) -> None:
+        """Run grammar actions until a sample is needed (forced text is appended)."""
+        s = r.seq
+        while True:
+            act, arg = r.gs.action()
+            if act == "force":
+                s.tokens.extend(arg)
+                r.generated.extend(arg)
+                r.n_forced += len(arg)
+                self.stats["forced_tokens"] += len(arg)
+                continue
+            if act == "sample":
+                if len(r.generated) >= r.max_new * 4 + 64:
+                    self._finish(r)
+                    return
+                r.mask = arg
+                return
+            self._finish(r)
+            return
+
+    def _finish(self, r: Request) -> None:
+        s = r.seq
+        s.req = None
+        s.tokens.append(self.tok.eot_id)  # end of the assistant message; prefilled with the next run
+        s.last_used = time.perf_counter()
+        st = {"prompt_tokens": r.n_prompt, "completion_tokens": len(r.generated), "forced_tokens": r.n_forced,
+              "sampled_tokens": r.n_sampled, "latency_s": time.perf_counter() - r.t_submit,
+              "ttft_s": (r.t_first - r.t_submit) if r.t_first else 0.0}
+        if r.on_done:
+            r.on_done(list(r.generated), st)
+
+    def _ensure_blocks(self, s: Sequence, upto: int, protect: set) -> bool:
+        need = (upto + self.kv.block_size - 1) // self.kv.block_size - len(s.blocks)
+        if need <= 0:
+            return True
+        if need > self.kv.free_blocks:
+            self._evict(need - self.kv.free_blocks, protect)
+        if need > self.kv.free_blocks:
+            return False
+        s.blocks.extend(self.kv.alloc(need))
+        return True
+
+    def _evict(self, n_blocks: int, protect: set) -> None:
+        idle = sorted((s for s in self.seqs.values() if s.req is None and s.blocks and s.id not in protect),
+                      key=lambda s: s.last_used)
+        freed = 0
+        for s in idle:
+            freed += len(s.blocks)
+            self.kv.release(s.blocks)
+            s.blocks = []
+            s.n_cached = 0
+            self.stats["evictions"] += 1
+            if freed >= n_blocks:
+                return
+
+    def step(self) -> bool:
+        t_host0 = time.perf_counter()
+        self._admit()
+        active = [s for s in self.seqs.values() if s.req is not None and s.pending > 0]
+        if not active:
+            return False
+        BS = self.kv.block_size
+        decode, prefill = [], []
+        budget = self.cfg.max_batch_tokens
+        protect = set(s.id for s in active)
+        for s in active:
+            if s.pending == 1 and len(decode) < self.cfg.max_decode_seqs:
+                if self._ensure_blocks(s, s.n_cached + 1, protect):
+                    decode.append(s)
+        budget -= len(decode)
+        chunks: List[Tuple[Sequence, int]] = []
+        for s in sorted((s for s in active if s.pending > 1 or (s.pending == 1 and s not in decode)),
+                        key=lambda s: s.req.t_submit):
+            if budget <= 0:
+                break
+            q = min(s.pending, budget)
+            if s.n_cached + q > self.kv.num_blocks * BS:
+                raise MemoryError("sequence longer than the whole KV pool")
+            if not self._ensure_blocks(s, s.n_cached + q, protect):
+                continue
+            chunks.append((s, q))
+            budget -= q
+        if not decode and not chunks:
+            raise MemoryError("KV pool exhausted with no evictable sequence")
+        rows = [(s, 1) for s in decode] + chunks
+        sample_rows = []  # (row index in batch, seq)
+        off = 0
+        for s, q in rows:
+            off += q
+            if s.n_cached + q == len(s.tokens):
+                sample_rows.append((off - 1, s))
+        self.stats["host_s"] += time.perf_counter() - t_host0
+        logits = self._forward(decode, chunks, [i for i, _ in sample_rows])
+        for s, q in rows:
+            s.n_cached += q
+            s.last_used = time.perf_counter()
+        self.stats["steps"] += 1
+        self.stats["prefill_tokens"] += sum(q for _, q in chunks)
+        self.stats["decode_tokens"] += len(decode)
+        if sample_rows:
+            self._sample_and_advance(logits, [s for _, s in sample_rows])
+        return True
+
+    # ------------------------------------------------------------- forward
+    def _meta_arrays(self, seqs_q: List[Tuple[Sequence, int]]):
+        BS = self.kv.block_size
+        n = len(seqs_q)
+        maxb = max(len(s.blocks) for s, _ in seqs_q)
+        bt = np.zeros((n, maxb), dtype=np.int32)
+        ctx = np.zeros(n, dtype=np.int32)
+        qs = np.zeros(n + 1, dtype=np.int32)
+        for i, (s, q) in enumerate(seqs_q):
+            bt[i, : len(s.blocks)] = s.blocks
+            ctx[i] = s.n_cached + q
+            qs[i + 1] = qs[i] + q
+        return bt, ctx, qs
+
+    def _token_arrays(self, rows: List[Tuple[Sequence, int]]):
+        BS = self.kv.block_size
+        ids, pos, slots = [], [], []
+        for s, q in rows:
+            a = s.n_cached
+            ids.extend(s.tokens[a:a + q])
+            p = np.arange(a, a + q, dtype=np.int64)
+            pos.append(p)
+            blk = np.asarray(s.blocks, dtype=np.int64)[p // BS]
+            slots.append(blk * BS + p % BS)
+        return (np.asarray(ids, dtype=np.int32), np.concatenate(pos).astype(np.int32),
+                np.concatenate(slots).astype(np.int32))
+
+    def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int]):
+        t0 = time.perf_counter()
+        if not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode:
+            out = self._forward_graph(decode)
+            self.stats["graph_steps"] += 1
+            self.stats["decode_steps"] += 1
+        else:
+            out = self._forward_eager(decode, chunks, sample_idx)
+            if not chunks:
+                self.stats["decode_steps"] += 1
+        self.stats["forward_s"] += time.perf_counter() - t0
+        return out
+
+    def _to_dev(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
+        """One H2D copy for all int32 metadata arrays."""
+        sizes = [a.size for a in arrays]
+        flat = np.concatenate([a.reshape(-1).astype(np.int32, copy=False) for a in arrays]) if arrays else \
+            np.zeros(0, np.int32)
+        host = torch.from_numpy(flat)
+        if self.device.type == "cuda":
+            host = host.pin_memory()
+            dev = host.to(self.device, non_blocking=True)
+        else:
+            dev = host
+        out, o = [], 0
+        for a, n in zip(arrays, sizes):
+            out.append(dev[o:o + n].view(*a.shape))
+            o += n
+        return out
+
+    def _forward_eager(self, decode, chunks, sample_idx):
+        from ..models.llama import StepInputs
+
+        rows = [(s, 1) for s in decode] + list(chunks)
+        ids, pos, slots = self._token_arrays(rows)
+        arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
+        dmeta = pmeta = None
+        if decode:
+            bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
+            arrays += [bt_d, ctx_d, qs_d]
+        if chunks:
+            bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
+            ts, t0, tl = A.build_prefill_tiles(qs_p.tolist(), self.model.nq // self.model.nkv)
+            arrays += [bt_p, ctx_p, qs_p, np.asarray(ts, np.int32), np.asarray(t0, np.int32),
+                       np.asarray(tl, np.int32)]
+        dev = self._to_dev(arrays)
+        d_ids, d_pos, d_slots, d_sidx = dev[:4]
+        k = 4
+        if decode:
+            bt, ctx, qs = dev[k:k + 3]
+            k += 3
+            n_parts = self._n_parts(int(ctx_d.max()))
+            dmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=len(decode), decode=True,
+                               n_parts=n_parts, part_size=PART_SIZE, ctx_lens_host=ctx_d.tolist(),
+                               q_start_host=qs_d.tolist())
+            if n_parts > 1:
+                dmeta.part_o = torch.empty(len(decode) * self.model.nq * n_parts * self.model.D,
+                                           dtype=torch.float32, device=self.device)
+                dmeta.part_ml = torch.empty(len(decode) * self.model.nq * n_parts * 2, dtype=torch.float32,
+                                            device=self.device)
+        if chunks:
+            bt, ctx, qs, tsd, t0d, tld = dev[k:k + 6]
+            pmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=len(chunks), decode=False,
+                               tile_seq=tsd, tile_tok0=t0d, tile_len=tld, n_tiles=len(ts),
+                               ctx_lens_host=ctx_p.tolist(), q_start_host=qs_p.tolist())
+        inp = StepInputs(d_ids, d_pos, d_slots, len(decode), dmeta, pmeta, d_sidx.long())
+        return self.model.forward(inp, self.kv.k, self.kv.v)
+
+    @staticmethod
+    def _n_parts(max_ctx: int) -> int:
+        n = max(1, (max_ctx + PART_SIZE - 1) // PART_SIZE)
+        return 1 << (n - 1).bit_length()
+
+    # ---------------------------------------------------------- HIP graphs
+    def _bucket(self, n: int) -> int:
+        for b in self.cfg.graph_batch_sizes:
+            if b >= n:
+                return b
+        return n
+
+    def _ensure_static(self):
+        if self._static is not None:
+            return self._static
+        Bmax = max(self.cfg.graph_batch_sizes)
+        mb = self.max_blocks_per_seq
+        npmax = self._n_parts(self.max_context)
+        dev = self.device
+        st = {
+            "ids": torch.zeros(Bmax, dtype=torch.int32, device=dev),
+            "pos": torch.zeros(Bmax, dtype=torch.int32, device=dev),
+            "slots": torch.full((Bmax,), -1, dtype=torch.int32, device=dev),
+            "bt": torch.zeros(Bmax, mb, dtype=torch.int32, device=dev),
+            "ctx": torch.ones(Bmax, dtype=torch.int32, device=dev),
+            "qs": torch.arange(Bmax + 1, dtype=torch.int32, device=dev),
+            "sidx": torch.arange(Bmax, dtype=torch.int64, device=dev),
+            "part_o": torch.empty(Bmax * self.model.nq * npmax * self.model.D, dtype=torch.float32, device=dev),
+            "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
+            "host": torch.zeros(Bmax * (3 + mb + 1), dtype=torch.int32).pin_memory(),
+        }
+        self._static = st
+        return st
+
+    def _graph_inputs(self, B: int, n_parts: int):
+        from ..models.llama import StepInputs
+
+        st = self._static
+        meta = A.AttnMeta(block_tables=st["bt"][:B], ctx_lens=st["ctx"][:B], q_start=st["qs"][:B + 1], num_seqs=B,
+                          decode=True, n_parts=n_parts, part_size=PART_SIZE, part_o=st["part_o"],
+                          part_ml=st["part_ml"])
+        return StepInputs(st["ids"][:B], st["pos"][:B], st["slots"][:B], B, meta, None, st["sidx"][:B])
+
+    def _capture(self, B: int, n_parts: int):
+        key = (B, n_parts)
+        g = self._graphs.get(key)
+        if g is not None:
+            return g
+        inp = self._graph_inputs(B, n_parts)
+        s = torch.cuda.Stream(self.device)
+        s.wait_stream(torch.cuda.current_stream(self.device))
+        with torch.cuda.stream(s):
+            for _ in range(2):
+                self.model.forward(inp, self.kv.k, self.kv.v)
+        torch.cuda.current_stream(self.device).wait_stream(s)
+        graph = torch.cuda.CUDAGraph()
+        if self._graph_pool is None:
+            self._graph_pool = torch.cuda.graph_pool_handle()
+        with torch.cuda.graph(graph, pool=self._graph_pool):
+            out = self.model.forward(inp, self.kv.k, self.kv.v)
+        self._graphs[key] = (graph, out)
+        return self._graphs[key]
+
+    def _forward_graph(self, decode: List[Sequence]):
+        st = self._ensure_static()
+        B = len(decode)
+        Bb = self._bucket(B)
+        if Bb > max(self.cfg.graph_batch_sizes):
+            return self._forward_eager(decode, [], list(range(B)))
+        BS = self.kv.block_size
+        mb = self.max_blocks_per_seq
+        ctx = np.ones(Bb, dtype=np.int32)
+        ids = np.zeros(Bb, dtype=np.int32)
+        pos = np.zeros(Bb, dtype=np.int32)
+        slots = np.full(Bb, -1, dtype=np.int32)
+        bt = np.zeros((Bb, mb), dtype=np.int32)
+        for i, s in enumerate(decode):
+            p = s.n_cached
+            ids[i] = s.tokens[p]
+            pos[i] = p
+            slots[i] = s.blocks[p // BS] * BS + p % BS
+            ctx[i] = p + 1
+            bt[i, : len(s.blocks)] = s.blocks
+        n_parts = self._n_parts(int(ctx.max()))
+        host = st["host"]
+        hv = host.numpy()
+        o = 0
+        for arr in (ids, pos, slots, ctx):
+            hv[o:o + Bb] = arr
+            o += Bb
+        hv[o:o + Bb * mb] = bt.reshape(-1)
+        stream = torch.cuda.current_stream(self.device)
+        dev_flat = torch.empty(o + Bb * mb, dtype=torch.int32, device=self.device)
+        dev_flat.copy_(host[: o + Bb * mb], non_blocking=True)
+        st["ids"][:Bb].copy_(dev_flat[0:Bb])
+        st["pos"][:Bb].copy_(dev_flat[Bb:2 * Bb])
+        st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
+        st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
+        st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
+        graph, out = self._capture(Bb, n_parts)
+        graph.replay()
+        return out[:B]
+
+    # ------------------------------------------------------------ sampling
+    def _mask_table(self) -> Optional[torch.Tensor]:
+        if self._mask_ver != self.grt.masks.version:
+            arr = self.grt.masks.array()
+            self._mask_dev = torch.from_numpy(arr).to(self.device)
+            self._mask_ver = self.grt.masks.version
+        return self._mask_dev
+
+    def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> None:
+        t0 = time.perf_counter()
+        B = len(seqs)
+        mask_id = np.full(B, -1, dtype=np.int32)
+        list_off = np.zeros(B, dtype=np.int32)
+        list_len = np.zeros(B, dtype=np.int32)
+        lists: List[int] = []
+        temps = np.zeros(B, dtype=np.float32)
+        seeds = np.zeros(B, dtype=np.int32)
+        steps = np.zeros(B, dtype=np.int32)
+        for i, s in enumerate(seqs):
+            r = s.req
+            kind, m = r.mask
+            if kind == "list":
+                list_off[i] = len(lists)
+                list_len[i] = len(m)
+                lists.extend(m)
+            else:
+                mask_id[i] = m
+            temps[i] = r.temperature
+            seeds[i] = (r.seed * 2654435761 + s.id) & 0x7FFFFFFF
+            steps[i] = len(r.generated)
+        table = self._mask_table()
+        if not lists:
+            lists = [0]
+        ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps])
+        d_temps = torch.from_numpy(temps).to(self.device)
+        tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
+                         vocab=self.vocab)
+        toks = tok.tolist()
+        self.stats["sample_s"] += time.perf_counter() - t0
+        now = time.perf_counter()
+        for s, t in zip(seqs, toks):
+            r = s.req
+            if r.t_first is None:
+                r.t_first = now
+            if t < 0:
+                self._finish(r)
+                continue
+            r.n_sampled += 1
+            self.stats["sampled_tokens"] += 1
+            r.generated.append(t)
+            if t in self.eos_ids:
+                r.generated.pop()
+                r.gs.advance(t)
+                self._finish(r)
+                continue
+            s.tokens.append(t)
+            r.gs.advance(t)
+            self._drive(r)

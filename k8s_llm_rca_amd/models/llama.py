@@ -1,0 +1,143 @@
+"""Llama-3 / Mixtral decoder (the in-process replacement for GPT-4).
+
+Per layer (bf16, fp32 accumulation inside every kernel)::
+
+    y      = rmsnorm(prev + residual)            # HIP fused add+norm, residual updated in place
+    qkv    = y @ Wqkv^T                          # hipBLASLt (column-parallel under TP)
+    rope_kv_write(qkv)                           # HIP: rotate q,k in place, scatter k,v to pages
+    a      = paged_attention(qkv)                # HIP MFMA kernels (decode split-KV / varlen prefill)
+    o      = a @ Wo^T ; all_reduce(o)            # row-parallel + RCCL
+    y      = rmsnorm(o + residual)
+    d      = silu_mul(y @ Wgu^T) @ Wdown^T ; all_reduce(d)     (dense)
+           = moe(y)                                             (Mixtral: router + grouped experts)
+
+Logits are computed only for the rows that sample (last token of each
+sequence); the lm_head is vocab-parallel under TP and all-gathered.
+Weights are random-init (seeded, std ``init_std``) in the real shapes;
+``load_safetensors`` accepts real checkpoints when present.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import attention as A
+from ..ops import norm as N
+from ..parallel.groups import ParallelContext, single
+from .config import ModelConfig
+from . import moe as MOE
+
+
+@dataclass
+class StepInputs:
+    input_ids: torch.Tensor        # [T] int32
+    positions: torch.Tensor        # [T] int32
+    slots: torch.Tensor            # [T] int32 (-1: no KV write)
+    n_decode: int                  # rows [0, n_decode) are single-token decode rows
+    meta_decode: Optional[A.AttnMeta]
+    meta_prefill: Optional[A.AttnMeta]
+    logits_idx: torch.Tensor       # [n] int64 rows whose logits are needed
+
+
+class LlamaModel:
+    def __init__(self, cfg: ModelConfig, device, dtype=torch.bfloat16, pc: Optional[ParallelContext] = None,
+                 seed: int = 0, init: bool = True):
+        self.cfg = cfg
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.pc = pc or single()
+        tp = self.pc.tp_size
+        if cfg.n_heads % tp:
+            raise ValueError(f"{cfg.n_heads} heads not divisible by tp={tp}")
+        self.nq = cfg.n_heads // tp
+        self.nkv = max(1, cfg.n_kv_heads // tp)   # kv heads replicated when n_kv < tp
+        self.D = cfg.head_dim
+        self.inter = cfg.intermediate // tp if cfg.n_experts == 0 else cfg.intermediate
+        self.vocab_local = (cfg.vocab_size + tp - 1) // tp
+        self.scale = 1.0 / math.sqrt(self.D)
+        self.cos_sin = A.rope_cos_sin(cfg.max_position, cfg.rope_theta, self.D, cfg.scaling_dict(), device=self.device)
+        self.layers: List[Dict[str, torch.Tensor]] = []
+        self.moe: Optional[MOE.MoELayerSet] = None
+        if init:
+            self._random_init(seed)
+
+    # --------------------------------------------------------------- weights
+    def _randn(self, g, *shape, std=None):
+        std = self.cfg.init_std if std is None else std
+        t = torch.empty(*shape, dtype=self.dtype, device=self.device)
+        t.normal_(0.0, std, generator=g)
+        return t
+
+    def _random_init(self, seed: int) -> None:
+        cfg = self.cfg
+        g = torch.Generator(device=self.device)
+        g.manual_seed(seed * 1000 + self.pc.tp_rank)
+        H = cfg.hidden
+        qkv_out = (self.nq + 2 * self.nkv) * self.D
+        out_std = cfg.init_std / math.sqrt(2 * cfg.n_layers)
+        for _ in range(cfg.n_layers):
+            L = {
+                "in_norm": torch.ones(H, dtype=self.dtype, device=self.device),
+                "post_norm": torch.ones(H, dtype=self.dtype, device=self.device),
+                "wqkv": self._randn(g, qkv_out, H),
+                "wo": self._randn(g, H, self.nq * self.D, std=out_std),
+            }
+            if cfg.n_experts == 0:
+                L["w_gu"] = self._randn(g, 2 * self.inter, H)
+                L["w_down"] = self._randn(g, H, self.inter, std=out_std)
+            self.layers.append(L)
+        if cfg.n_experts:
+            self.moe = MOE.MoELayerSet(cfg, self.device, self.dtype, self.pc, g, out_std)
+        self.embed = self._randn(g, cfg.vocab_size, H)
+        self.final_norm = torch.ones(H, dtype=self.dtype, device=self.device)
+        self.lm_head = self._randn(g, self.vocab_local, H)
+
+    def weight_bytes(self) -> int:
+        n = sum(t.numel() * t.element_size() for L in self.layers for t in L.values())
+        n += self.embed.numel() * 2 + self.lm_head.numel() * 2
+        if self.moe is not None:
+            n += self.moe.weight_bytes()
+        return n
+
+    # -------------------------------------------------------------- forward
+    def forward(self, inp: StepInputs, k_cache: torch.Tensor, v_cache: torch.Tensor) -> torch.Tensor:
+        """k_cache/v_cache: [n_layers, NB, nkv, BS, D] / [n_layers, NB, nkv, D, BS]."""
+        cfg = self.cfg
+        T = inp.input_ids.shape[0]
+        H = cfg.hidden
+        residual = F.embedding(inp.input_ids.long(), self.embed)     # [T, H]
+        prev: Optional[torch.Tensor] = None
+        y = torch.empty_like(residual)
+        attn = torch.empty((T, self.nq * self.D), dtype=self.dtype, device=self.device)
+        nd = inp.n_decode
+        for li, L in enumerate(self.layers):
+            if prev is None:
+                N.rmsnorm(residual, L["in_norm"], cfg.rms_eps, out=y)
+            else:
+                N.rmsnorm(prev, L["in_norm"], cfg.rms_eps, residual=residual, out=y)
+            qkv = F.linear(y, L["wqkv"])
+            A.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, k_cache[li], v_cache[li], self.nq, self.nkv)
+            if inp.meta_decode is not None and nd > 0:
+                A.paged_attention(qkv[:nd], k_cache[li], v_cache[li], inp.meta_decode, self.nq, self.nkv, self.scale,
+                                  out=attn[:nd])
+            if inp.meta_prefill is not None and nd < T:
+                A.paged_attention(qkv[nd:], k_cache[li], v_cache[li], inp.meta_prefill, self.nq, self.nkv,
+                                  self.scale, out=attn[nd:])
+            o = F.linear(attn, L["wo"])
+            self.pc.all_reduce(o)
+            N.rmsnorm(o, L["post_norm"], cfg.rms_eps, residual=residual, out=y)
+            if self.moe is not None:
+                prev = self.moe.forward(li, y)
+            else:
+                gu = F.linear(y, L["w_gu"])
+                act = N.silu_mul(gu)
+                prev = F.linear(act, L["w_down"])
+                self.pc.all_reduce(prev)
+        N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
+        sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
+        logits = F.linear(sel, self.lm_head)
+        return self.pc.all_gather_last(logits)

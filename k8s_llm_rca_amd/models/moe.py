@@ -1,0 +1,73 @@
+"""Mixtral sparse MoE block (B11-B13, B15).
+
+``router -> top-k -> permute -> per-expert SwiGLU -> weighted combine``.
+Routing (softmax + top-2 + renormalise), the token permutation (expert
+histogram + prefix scan) and the weighted combine are HIP kernels
+(``csrc/kernels/moe.hip``); expert GEMMs run on hipBLASLt over each expert's
+contiguous token slice.  Under expert parallelism (EP) the whole experts live
+on ``E / ep`` ranks and tokens travel by all-to-all (:mod:`..parallel.ep`).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.nn.functional as F
+
+from ..ops import moe as M
+from ..ops import norm as N
+from ..parallel.groups import ParallelContext
+from .config import ModelConfig
+
+
+class MoELayerSet:
+    def __init__(self, cfg: ModelConfig, device, dtype, pc: ParallelContext, g: torch.Generator, out_std: float):
+        self.cfg = cfg
+        self.pc = pc
+        self.E = cfg.n_experts
+        self.k = cfg.top_k
+        ep = pc.ep_size
+        if self.E % ep:
+            raise ValueError(f"{self.E} experts not divisible by ep={ep}")
+        self.E_local = self.E // ep
+        self.e0 = pc.ep_rank * self.E_local
+        H, I = cfg.hidden, cfg.intermediate
+        self.router: List[torch.Tensor] = []
+        self.w13: List[torch.Tensor] = []
+        self.w2: List[torch.Tensor] = []
+        for _ in range(cfg.n_layers):
+            r = torch.empty(self.E, H, dtype=dtype, device=device)
+            r.normal_(0.0, cfg.init_std, generator=g)
+            self.router.append(r)
+            w13 = torch.empty(self.E_local, 2 * I, H, dtype=dtype, device=device)
+            w13.normal_(0.0, cfg.init_std, generator=g)
+            w2 = torch.empty(self.E_local, H, I, dtype=dtype, device=device)
+            w2.normal_(0.0, out_std, generator=g)
+            self.w13.append(w13)
+            self.w2.append(w2)
+
+    def weight_bytes(self) -> int:
+        return sum(t.numel() * t.element_size() for lst in (self.router, self.w13, self.w2) for t in lst)
+
+    def forward(self, li: int, y: torch.Tensor) -> torch.Tensor:
+        T, H = y.shape
+        logits = F.linear(y, self.router[li])                          # [T, E]
+        topk_w, topk_ids = M.route_topk(logits, self.k)                # [T,k] fp32, int32
+        if self.pc.ep_size > 1:
+            from ..parallel.ep import ep_moe_forward
+            return ep_moe_forward(self, li, y, topk_w, topk_ids)
+        order, inv, offsets = M.align(topk_ids, self.E)                # (token,k) slots sorted by expert
+        x_perm = y.index_select(0, (order // self.k).long())           # [T*k, H]
+        out_perm = self.experts(li, x_perm, offsets.tolist())
+        return M.combine(out_perm, inv, topk_w, T, self.k)
+
+    def experts(self, li: int, x_perm: torch.Tensor, offsets: List[int]) -> torch.Tensor:
+        """Grouped SwiGLU over contiguous expert slices: offsets[e]..offsets[e+1]."""
+        out = torch.empty_like(x_perm)
+        for e in range(self.E_local):
+            a, b = offsets[e], offsets[e + 1]
+            if b <= a:
+                continue
+            gu = F.linear(x_perm[a:b], self.w13[li][e])
+            out[a:b] = F.linear(N.silu_mul(gu), self.w2[li][e])
+        return out

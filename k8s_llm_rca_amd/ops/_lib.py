@@ -1,0 +1,94 @@
+"""Loader for ``libk8srca_hip.so`` (all hand-written gfx950 kernels, C ABI).
+
+The library is loaded with ctypes *after* ``import torch`` so it binds to the
+HIP runtime torch already mapped (same SONAME ``libamdhip64.so.7``) and shares
+torch's device context and streams.  On a GPU box a missing or broken library
+is a hard error (ops never silently fall back to eager PyTorch on device
+tensors); CPU tensors use the fp32 PyTorch references in the op modules.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+import torch
+
+from .. import _build
+
+_lib = None
+_lock = threading.Lock()
+_err = None
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+F = ctypes.c_float
+
+_SIGS = {
+    "k8s_rmsnorm": [P, P, P, P, I, I, I, I, F, P],
+    "k8s_silu_mul": [P, P, I, I, P],
+    "k8s_rope_kv": [P, I, P, P, P, P, P, I, I, I, I, P],
+    "k8s_attn_decode": [P, I, P, P, P, I, P, P, I, I, I, I, F, P, I, P, P, I, I, P],
+    "k8s_attn_prefill": [P, I, P, P, P, I, P, P, P, P, P, I, I, I, I, F, P, I, P],
+    "k8s_sample": [P, I, I, I, P, P, P, P, P, I, P, P, P, P, P],
+    "k8s_moe_route": [P, I, I, I, P, P, P],
+    "k8s_moe_align": [P, I, I, I, P, P, P, P],
+    "k8s_moe_combine": [P, P, P, I, I, I, P, P],
+    "k8s_substr_search": [P, P, P, I, P, I, P, P],
+    "k8s_graph_expand": [P, P, P, P, I, P, P, I, I, P, P, P, P, I, P, P],
+    "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P],
+    "k8s_metapath_count": [P, P, P, P, P, P, P, I, I, I, I, P, I, P, P, P],
+}
+
+
+def lib():
+    """The loaded library; raises if unavailable."""
+    global _lib, _err
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            path = _build.hip_lib_path()
+            if not os.path.exists(path):
+                if os.environ.get("K8SRCA_AUTOBUILD", "1") == "1":
+                    _build.build_hip()
+                else:
+                    raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
+            L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            for name, args in _SIGS.items():
+                fn = getattr(L, name, None)
+                if fn is None:
+                    continue
+                fn.argtypes = args
+                fn.restype = ctypes.c_int
+            _lib = L
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:  # noqa: BLE001
+        return False
+
+
+def stream_ptr(t: torch.Tensor = None) -> int:
+    return torch.cuda.current_stream(t.device if t is not None else None).cuda_stream
+
+
+def ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
+
+
+def check(rc: int, name: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{name} failed with hipError {rc}")
+
+
+def use_hip(*tensors) -> bool:
+    """True when the op must run on the HIP kernels (device tensors)."""
+    dev = any(t is not None and t.is_cuda for t in tensors)
+    if dev:
+        lib()  # fail loudly when the native library is missing
+    return dev

@@ -1,0 +1,178 @@
+"""RoPE + paged-KV write (B3+B5) and paged GQA attention (B6/B7).
+
+KV cache layout per layer (page = ``block_size`` tokens):
+``k_cache[num_blocks, n_kv, block_size, 128]`` and
+``v_cache[num_blocks, n_kv, 128, block_size]`` (V pages transposed so the PV
+MFMA operand is a contiguous load; see ``csrc/kernels/attention.hip``).
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Optional
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr, use_hip
+
+HEAD_DIM = 128
+
+
+def rope_cos_sin(max_pos: int, theta: float = 500000.0, head_dim: int = HEAD_DIM, scaling: Optional[dict] = None,
+                 device=None) -> torch.Tensor:
+    """[max_pos, head_dim] fp32 table: cos(f_i p) for i < d/2, then sin(f_i p)."""
+    half = head_dim // 2
+    inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) / half))
+    if scaling and scaling.get("type") == "llama3":
+        factor = scaling.get("factor", 8.0)
+        lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
+        old = scaling.get("original_max_position_embeddings", 8192)
+        wavelen = 2 * math.pi / inv
+        lo_w, hi_w = old / lo, old / hi
+        smooth = (old / wavelen - lo) / (hi - lo)
+        scaled = torch.where(wavelen > lo_w, inv / factor, inv)
+        mid = (wavelen <= lo_w) & (wavelen >= hi_w)
+        inv = torch.where(mid, (1 - smooth) * inv / factor + smooth * inv, scaled)
+    p = torch.arange(max_pos, dtype=torch.float64)[:, None] * inv[None, :]
+    return torch.cat([p.cos(), p.sin()], dim=1).to(torch.float32).to(device)
+
+
+def kv_write(k: torch.Tensor, v: torch.Tensor, slots: torch.Tensor, k_cache: torch.Tensor,
+             v_cache: torch.Tensor) -> None:
+    """Scatter un-rotated k,v [T, nkv, D] into pages (learned-position models, e.g. OPT)."""
+    BS = k_cache.shape[2]
+    s = slots.long()
+    ok = s >= 0
+    blk, off = (s // BS)[ok], (s % BS)[ok]
+    k_cache[blk, :, off, :] = k[ok].to(k_cache.dtype)
+    v_cache[blk, :, :, off] = v[ok].to(v_cache.dtype)
+
+
+def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor, slots: Optional[torch.Tensor],
+                  k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int, nkv: int) -> None:
+    """Rotate q,k in place inside ``qkv`` and scatter k,v into their pages."""
+    T, ld = qkv.shape
+    BS = k_cache.shape[2]
+    assert ld >= (nq + 2 * nkv) * HEAD_DIM
+    if use_hip(qkv):
+        assert qkv.stride(1) == 1 and positions.dtype == torch.int32 and cos_sin.dtype == torch.float32
+        assert slots is None or slots.dtype == torch.int32
+        assert k_cache.shape[1] == nkv and v_cache.shape[2] == HEAD_DIM and v_cache.shape[3] == BS
+        check(lib().k8s_rope_kv(ptr(qkv), qkv.stride(0), ptr(positions), ptr(cos_sin), ptr(slots), ptr(k_cache),
+                                ptr(v_cache), T, nq, nkv, BS, stream_ptr(qkv)), "rope_kv")
+        return
+    half = HEAD_DIM // 2
+    cs = cos_sin[positions.long()]
+    cos, sin = cs[:, None, :half], cs[:, None, half:]
+    nh = nq + nkv
+    x = qkv[:, : nh * HEAD_DIM].float().view(T, nh, HEAD_DIM)
+    a, b = x[..., :half], x[..., half:]
+    rot = torch.cat([a * cos - b * sin, b * cos + a * sin], dim=-1)
+    qkv[:, : nh * HEAD_DIM] = rot.reshape(T, -1).to(qkv.dtype)
+    if slots is None:
+        return
+    k = qkv[:, nq * HEAD_DIM: nh * HEAD_DIM].view(T, nkv, HEAD_DIM)
+    v = qkv[:, nh * HEAD_DIM: (nh + nkv) * HEAD_DIM].view(T, nkv, HEAD_DIM)
+    s = slots.long()
+    ok = s >= 0
+    blk, off = (s // BS)[ok], (s % BS)[ok]
+    k_cache[blk, :, off, :] = k[ok]
+    v_cache[blk, :, :, off] = v[ok]
+
+
+@dataclass
+class AttnMeta:
+    """Per-step attention metadata (device tensors, int32)."""
+    block_tables: torch.Tensor   # [S, max_blocks]
+    ctx_lens: torch.Tensor       # [S]
+    q_start: torch.Tensor        # [S+1]
+    num_seqs: int
+    decode: bool                 # every sequence has exactly one query token
+    # prefill tiling
+    tile_seq: Optional[torch.Tensor] = None
+    tile_tok0: Optional[torch.Tensor] = None
+    tile_len: Optional[torch.Tensor] = None
+    n_tiles: int = 0
+    # decode split-KV
+    n_parts: int = 1
+    part_size: int = 512
+    part_o: Optional[torch.Tensor] = None
+    part_ml: Optional[torch.Tensor] = None
+    # host copies for the reference path
+    ctx_lens_host: Optional[list] = None
+    q_start_host: Optional[list] = None
+
+
+def plan_decode_split(max_ctx: int, num_seqs: int, nkv: int, target_wgs: int = 1024) -> tuple:
+    """Pick a key-partition size (multiple of 64) so the grid fills the chip."""
+    part = 512
+    while part > 64 and num_seqs * nkv * max(1, (max_ctx + part - 1) // part) < target_wgs:
+        part //= 2
+    n_parts = max(1, (max_ctx + part - 1) // part)
+    return n_parts, part
+
+
+def build_prefill_tiles(q_start_host: list, G: int) -> tuple:
+    per = max(1, 64 // G)
+    seq, tok0, ln = [], [], []
+    for s in range(len(q_start_host) - 1):
+        a, b = q_start_host[s], q_start_host[s + 1]
+        for t in range(a, b, per):
+            seq.append(s)
+            tok0.append(t)
+            ln.append(min(per, b - t))
+    return seq, tok0, ln
+
+
+def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta, nq: int,
+                    nkv: int, scale: float, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """q: [T, >= nq*D] (row stride free) -> out [T, nq*D]."""
+    T = q.shape[0]
+    BS = k_cache.shape[2]
+    D = k_cache.shape[3]
+    if out is None:
+        out = torch.empty((T, nq * D), dtype=q.dtype, device=q.device)
+    if use_hip(q) and D == HEAD_DIM:
+        assert q.stride(1) == 1 and out.stride(1) == 1 and q.dtype == torch.bfloat16
+        assert meta.block_tables.dtype == torch.int32 and meta.block_tables.is_contiguous()
+        L = lib()
+        if meta.decode:
+            assert T == meta.num_seqs
+            check(L.k8s_attn_decode(ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(meta.block_tables),
+                                    meta.block_tables.stride(0), ptr(meta.ctx_lens), ptr(meta.q_start),
+                                    meta.num_seqs, nq, nkv, BS, float(scale), ptr(out), out.stride(0),
+                                    ptr(meta.part_o), ptr(meta.part_ml), meta.n_parts, meta.part_size,
+                                    stream_ptr(q)), "attn_decode")
+        else:
+            check(L.k8s_attn_prefill(ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(meta.block_tables),
+                                     meta.block_tables.stride(0), ptr(meta.ctx_lens), ptr(meta.q_start),
+                                     ptr(meta.tile_seq), ptr(meta.tile_tok0), ptr(meta.tile_len), meta.n_tiles,
+                                     nq, nkv, BS, float(scale), ptr(out), out.stride(0), stream_ptr(q)),
+                  "attn_prefill")
+        return out
+    return _attention_ref(q, k_cache, v_cache, meta, nq, nkv, scale, out)
+
+
+def _attention_ref(q, k_cache, v_cache, meta: AttnMeta, nq, nkv, scale, out):
+    BS = k_cache.shape[2]
+    HEAD_DIM = k_cache.shape[3]
+    G = nq // nkv
+    qs = meta.q_start_host if meta.q_start_host is not None else meta.q_start.tolist()
+    cl = meta.ctx_lens_host if meta.ctx_lens_host is not None else meta.ctx_lens.tolist()
+    bt = meta.block_tables
+    for s in range(meta.num_seqs):
+        a, b = qs[s], qs[s + 1]
+        qlen, ctx = b - a, cl[s]
+        nb = (ctx + BS - 1) // BS
+        blocks = bt[s, :nb].long()
+        K = k_cache[blocks].permute(1, 0, 2, 3).reshape(nkv, nb * BS, HEAD_DIM)[:, :ctx].float()
+        V = v_cache[blocks].permute(1, 0, 3, 2).reshape(nkv, nb * BS, HEAD_DIM)[:, :ctx].float()
+        Q = q[a:b, : nq * HEAD_DIM].float().view(qlen, nkv, G, HEAD_DIM)
+        S = torch.einsum("tkgd,knd->kgtn", Q, K) * scale
+        pos = torch.arange(ctx - qlen, ctx)[:, None]
+        mask = torch.arange(ctx)[None, :] <= pos
+        S = S.masked_fill(~mask, float("-inf"))
+        P = torch.softmax(S, dim=-1)
+        O = torch.einsum("kgtn,knd->tkgd", P, V)
+        out[a:b] = O.reshape(qlen, nq * HEAD_DIM).to(out.dtype)
+    return out

@@ -1,0 +1,56 @@
+"""MoE routing ops (B11/B12): top-k router, expert permutation, weighted combine."""
+from __future__ import annotations
+
+from typing import Tuple
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr, use_hip
+
+
+def route_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
+    """softmax -> top-k -> renormalise.  Returns (weights fp32 [T,k], ids int32 [T,k])."""
+    T, E = logits.shape
+    if use_hip(logits):
+        assert logits.dtype == torch.bfloat16 and logits.is_contiguous()
+        w = torch.empty(T, k, dtype=torch.float32, device=logits.device)
+        ids = torch.empty(T, k, dtype=torch.int32, device=logits.device)
+        check(lib().k8s_moe_route(ptr(logits), T, E, k, ptr(w), ptr(ids), stream_ptr(logits)), "moe_route")
+        return w, ids
+    p = torch.softmax(logits.float(), dim=-1)
+    w, ids = torch.topk(p, k, dim=-1)
+    return w / w.sum(-1, keepdim=True), ids.int()
+
+
+def align(ids: torch.Tensor, E: int) -> Tuple[torch.Tensor, torch.Tensor, torch.Tensor]:
+    """Sort the T*k (token, slot) pairs by expert.  Returns (order, inv, offsets[E+1]) int32."""
+    flat = ids.reshape(-1).contiguous()
+    n = flat.numel()
+    if use_hip(flat):
+        order = torch.empty(n, dtype=torch.int32, device=flat.device)
+        inv = torch.empty(n, dtype=torch.int32, device=flat.device)
+        offsets = torch.empty(E + 1, dtype=torch.int32, device=flat.device)
+        check(lib().k8s_moe_align(ptr(flat), n, E, 0, ptr(order), ptr(inv), ptr(offsets), stream_ptr(flat)),
+              "moe_align")
+        return order, inv, offsets
+    order = torch.argsort(flat.long(), stable=True).int()
+    inv = torch.empty_like(order)
+    inv[order.long()] = torch.arange(n, dtype=torch.int32)
+    counts = torch.bincount(flat.long(), minlength=E)
+    offsets = torch.zeros(E + 1, dtype=torch.int32)
+    offsets[1:] = torch.cumsum(counts, 0).int()
+    return order, inv, offsets
+
+
+def combine(y_perm: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k: int) -> torch.Tensor:
+    """out[t] = sum_j w[t,j] * y_perm[inv[t*k+j]]."""
+    H = y_perm.shape[1]
+    out = torch.empty(T, H, dtype=y_perm.dtype, device=y_perm.device)
+    if use_hip(y_perm):
+        assert y_perm.is_contiguous() and w.dtype == torch.float32
+        check(lib().k8s_moe_combine(ptr(y_perm), ptr(inv), ptr(w), T, k, H, ptr(out), stream_ptr(y_perm)),
+              "moe_combine")
+        return out
+    g = y_perm.float()[inv.long()].view(T, k, H)
+    out.copy_((g * w.view(T, k, 1)).sum(1).to(out.dtype))
+    return out

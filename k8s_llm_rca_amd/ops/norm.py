@@ -1,0 +1,46 @@
+"""Fused residual-add + RMSNorm (B2) and SwiGLU (B8)."""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._lib import check, lib, ptr, stream_ptr, use_hip
+
+
+def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Optional[torch.Tensor] = None,
+            out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``y = rmsnorm(x + residual) * w``; when ``residual`` is given it is updated in place to ``x + residual``."""
+    T, H = x.shape
+    if out is None:
+        out = torch.empty((T, H), dtype=x.dtype, device=x.device)
+    if use_hip(x):
+        assert x.dtype == torch.bfloat16 and weight.dtype == torch.bfloat16 and H % 8 == 0
+        assert x.stride(1) == 1 and out.is_contiguous() and weight.is_contiguous() and H <= 16384
+        if residual is not None:
+            assert residual.is_contiguous() and residual.shape == (T, H)
+        check(lib().k8s_rmsnorm(ptr(x), ptr(residual), ptr(weight), ptr(out), T, H, x.stride(0), out.stride(0),
+                                float(eps), stream_ptr(x)), "rmsnorm")
+        return out
+    xf = x.float()
+    if residual is not None:
+        xf = xf + residual.float()
+        residual.copy_(xf.to(residual.dtype))
+        xf = residual.float()
+    var = xf.pow(2).mean(-1, keepdim=True)
+    out.copy_((xf * torch.rsqrt(var + eps) * weight.float()).to(out.dtype))
+    return out
+
+
+def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    T, I2 = gu.shape
+    inter = I2 // 2
+    if out is None:
+        out = torch.empty((T, inter), dtype=gu.dtype, device=gu.device)
+    if use_hip(gu):
+        assert gu.is_contiguous() and out.is_contiguous() and inter % 8 == 0 and gu.dtype == torch.bfloat16
+        check(lib().k8s_silu_mul(ptr(gu), ptr(out), T, inter, stream_ptr(gu)), "silu_mul")
+        return out
+    g, u = gu.float().split(inter, dim=-1)
+    out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
+    return out

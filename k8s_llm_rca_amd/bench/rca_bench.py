@@ -158,7 +158,9 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "decode_tokens": d["decode_tokens"], "sampled_tokens": d["sampled_tokens"],
                    "forced_tokens": d["forced_tokens"], "forward_s": round(d["forward_s"], 3),
                    "sample_s": round(d["sample_s"], 3), "host_s": round(d["host_s"], 3),
-                   "evictions": d["evictions"], "requests": d["requests"]},
+                   "evictions": d["evictions"], "requests": d["requests"],
+                   "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
+                   "kv_blocks": eng.kv.num_blocks},
         "setup_s": round(setup_s, 1),
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }
@@ -179,7 +181,7 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--graph-nodes", type=int, default=10_000)
     p.add_argument("--graph-device", action="store_true", help="mirror the stategraph to HBM (HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--kv-gb", type=float, default=96.0)
+    p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
     p.add_argument("--max-batch-tokens", type=int, default=8192)
     p.add_argument("--temperature", type=float, default=0.7)
     p.add_argument("--semantic-tokens", type=int, default=192)

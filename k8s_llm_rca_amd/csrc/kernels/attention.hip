@@ -17,9 +17,10 @@
 //     with one bf16 pack and no lane movement.
 //   * the 128-wide head dim is split over the 4 MFMA k-steps as dims
 //     32h+8c+j, so every Q/K fragment is a contiguous 16-byte load.
-// Decode (one token / seq): workgroup = (seq, kv head, key partition); its 4
-// waves split the partition's keys and merge through LDS; partitions are merged
-// by attn_reduce (flash-decoding split-KV).  Prefill / extend (varlen, causal,
+// Decode (one token / seq): each WAVE owns one (seq, kv head, key partition)
+// and streams its pages 64 keys at a time (32 x 16-byte loads in flight per
+// lane group before the first MFMA); partitions are merged by attn_reduce
+// (flash-decoding split-KV).  No LDS, no barriers.  Prefill / extend (varlen, causal,
 // cached prefix): workgroup = (tile of 64/G tokens, kv head); each wave owns 16
 // rows and walks the keys its rows can see.
 #include "common.h"
@@ -70,8 +71,11 @@ __device__ __forceinline__ bf16x8 zero8() {
   return z;
 }
 
-// Process one 32-key chunk starting at absolute key `kb` (kb % 32 == 0).
-// `limit` = number of keys this lane's row may see (keys < limit are valid).
+// Process NSUB consecutive 32-key sub-chunks starting at absolute key `kb`
+// (kb % 32 == 0, all inside one page) with ONE online-softmax update.
+// All K/V loads of the group are issued before the first MFMA so a wave keeps
+// NSUB*16 KB in flight.  `limit` = keys < limit are visible to this lane's row.
+template <int NSUB>
 __device__ __forceinline__ void chunk(RowState& st, const AttnArgs& a, const int* bt, int kvh, int kb, int limit,
                                       int lane) {
   const int r = lane & 15, h = lane >> 4;
@@ -80,50 +84,54 @@ __device__ __forceinline__ void chunk(RowState& st, const AttnArgs& a, const int
   const size_t page = ((size_t)blk * a.nkv + kvh);
   const uint16_t* kp = a.kc + page * (size_t)a.BS * D;
   const uint16_t* vp = a.vc + page * (size_t)D * a.BS;
-  // K fragments: tile t row r -> key 8*(r>>2)+4t+(r&3); dims 32h+8c..+8
-  bf16x8 kf[2][4];
+  // K fragments: sub-chunk u, tile t, row r -> key 32u + 8*(r>>2) + 4t + (r&3); dims 32h+8c..+8
+  bf16x8 kf[NSUB][2][4];
 #pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int key = off + 8 * (r >> 2) + 4 * t + (r & 3);
+  for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-    for (int c = 0; c < 4; ++c) kf[t][c] = load16(kp + (size_t)key * D + 32 * h + 8 * c);
-  }
-  // V fragments: column d = 16*dt + r, keys off+8h..+8 (transposed page)
-  bf16x8 vf[8];
+    for (int t = 0; t < 2; ++t) {
+      const int key = off + 32 * u + 8 * (r >> 2) + 4 * t + (r & 3);
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt) vf[dt] = load16(vp + (size_t)(16 * dt + r) * a.BS + off + 8 * h);
+      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16(kp + (size_t)key * D + 32 * h + 8 * c);
+    }
+  // V fragments: column d = 16*dt + r, keys off + 32u + 8h .. +8 (transposed page)
+  bf16x8 vf[NSUB][8];
+#pragma unroll
+  for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vf[u][dt] = load16(vp + (size_t)(16 * dt + r) * a.BS + off + 32 * u + 8 * h);
 
-  f32x4 s[2];
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    s[t] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-    for (int c = 0; c < 4; ++c) s[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[t][c], st.qf[c], s[t], 0, 0, 0);
-  }
-  // lane owns row r, keys kb + 8h + j, j = 4t + i
-  float p[8];
+  float p[NSUB][8];
   float cmax = -INFINITY;
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int u = 0; u < NSUB; ++u)
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int key = kb + 8 * h + 4 * t + i;
-      const float v = (key < limit) ? s[t][i] * a.scale_log2 : -INFINITY;
-      p[4 * t + i] = v;
-      cmax = fmaxf(cmax, v);
+    for (int t = 0; t < 2; ++t) {
+      f32x4 s = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int c = 0; c < 4; ++c) s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][t][c], st.qf[c], s, 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int key = kb + 32 * u + 8 * h + 4 * t + i;
+        const float v = (key < limit) ? s[i] * a.scale_log2 : -INFINITY;
+        p[u][4 * t + i] = v;
+        cmax = fmaxf(cmax, v);
+      }
     }
   cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
   cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
   const float mnew = fmaxf(st.m, cmax);
   const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(st.m - mnew);
   float psum = 0.f;
-  bf16x8 pf;
+  bf16x8 pf[NSUB];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const float e = (mnew == -INFINITY) ? 0.f : exp2f(p[j] - mnew);
-    psum += e;
-    pf[j] = (__bf16)e;
-  }
+  for (int u = 0; u < NSUB; ++u)
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float e = (mnew == -INFINITY) ? 0.f : exp2f(p[u][j] - mnew);
+      psum += e;
+      pf[u][j] = (__bf16)e;
+    }
   st.l = st.l * alpha + psum;
   st.m = mnew;
   // O rows 4h+i need the alpha of row 4h+i (owned by lane 4h+i)
@@ -134,7 +142,9 @@ __device__ __forceinline__ void chunk(RowState& st, const AttnArgs& a, const int
   for (int dt = 0; dt < 8; ++dt) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) st.o[dt][i] *= ar[i];
-    st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf, vf[dt], st.o[dt], 0, 0, 0);
+#pragma unroll
+    for (int u = 0; u < NSUB; ++u)
+      st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[u], vf[u][dt], st.o[dt], 0, 0, 0);
   }
 }
 
@@ -150,76 +160,57 @@ __device__ __forceinline__ void init_state(RowState& st, const AttnArgs& a, int 
 }
 
 // ---------------------------------------------------------------- decode
-// grid: (n_parts, nkv, S); block 256 (4 waves)
+// grid: (n_parts / 4, nkv, S); block 256.  Each WAVE owns one key partition of
+// `part_size` keys (a multiple of the page size): no LDS, no barriers; it
+// writes an unnormalised partial (O, m, l) merged by attn_reduce, or the final
+// bf16 row when n_parts == 1.
 __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
-  const int part = blockIdx.x, kvh = blockIdx.y, seq = blockIdx.z;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int part = blockIdx.x * 4 + w, kvh = blockIdx.y, seq = blockIdx.z;
   const int r = lane & 15, h = lane >> 4;
   const int ctx = a.ctx_lens[seq];
   const int k0 = part * a.part_size;
+  if (part >= a.n_parts || k0 >= ctx) return;  // wave-uniform exit
   const int k1 = min(ctx, k0 + a.part_size);
   const int qrow = a.q_start[seq];
   const bool valid = r < a.G;
   const int head = kvh * a.G + (valid ? r : 0);
   const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
 
-  __shared__ float sm_o[4][ROWS][D + 1];
-  __shared__ float sm_m[4][ROWS];
-  __shared__ float sm_l[4][ROWS];
-
   RowState st;
   init_state(st, a, qrow, head, valid, lane);
-  if (k0 < k1) {
-    for (int kb = k0 + CH * w; kb < k1; kb += CH * 4) chunk(st, a, bt, kvh, kb, k1, lane);
-  }
-  // lane-partial sums -> row sums
+  int kb = k0;
+  for (; kb + 64 <= k1 && ((kb % a.BS) + 64 <= a.BS); kb += 64) chunk<2>(st, a, bt, kvh, kb, k1, lane);
+  for (; kb < k1; kb += 32) chunk<1>(st, a, bt, kvh, kb, k1, lane);
+
   float l = st.l + __shfl_xor(st.l, 16, 64);
   l += __shfl_xor(l, 32, 64);
-  if (h == 0) {
-    sm_m[w][r] = st.m;
-    sm_l[w][r] = l;
+  // rows 4h+i of O belong to lanes 4h+i for m / l
+  float mr[4], lr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    mr[i] = __shfl(st.m, 4 * h + i, 64);
+    lr[i] = __shfl(l, 4 * h + i, 64);
   }
 #pragma unroll
-  for (int dt = 0; dt < 8; ++dt)
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * h + i;
+    if (row >= a.G) continue;
+    const int qh = kvh * a.G + row;
+    if (a.n_parts == 1) {
+      const float inv = lr[i] > 0.f ? 1.f / lr[i] : 0.f;
+      uint16_t* dst = a.out + (size_t)qrow * a.out_stride + qh * D;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) sm_o[w][4 * h + i][16 * dt + r] = st.o[dt][i];
-  __syncthreads();
-  // merge the 4 waves: thread -> (row, 8 columns)
-  const int row = threadIdx.x >> 4;        // 0..15
-  const int col0 = (threadIdx.x & 15) * 8; // 0..120
-  float M = -INFINITY;
+      for (int dt = 0; dt < 8; ++dt) dst[16 * dt + r] = f2bf(st.o[dt][i] * inv);
+    } else {
+      const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts + part;
+      float* po = a.part_o + base * D;
 #pragma unroll
-  for (int ww = 0; ww < 4; ++ww) M = fmaxf(M, sm_m[ww][row]);
-  float L = 0.f, f[4];
-#pragma unroll
-  for (int ww = 0; ww < 4; ++ww) {
-    f[ww] = (sm_m[ww][row] == -INFINITY) ? 0.f : exp2f(sm_m[ww][row] - M);
-    L += sm_l[ww][row] * f[ww];
-  }
-  float acc[8];
-#pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    float v = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < 4; ++ww) v += sm_o[ww][row][col0 + j] * f[ww];
-    acc[j] = v;
-  }
-  if (row >= a.G) return;
-  const int qh = kvh * a.G + row;
-  if (a.n_parts == 1) {
-    const float inv = (L > 0.f) ? 1.f / L : 0.f;
-    u16x8 o;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) o[j] = f2bf(acc[j] * inv);
-    *reinterpret_cast<u16x8*>(a.out + (size_t)qrow * a.out_stride + qh * D + col0) = o;
-  } else {
-    const size_t base = (((size_t)seq * a.nq + qh) * a.n_parts + part);
-    float4* po = reinterpret_cast<float4*>(a.part_o + base * D + col0);
-    po[0] = make_float4(acc[0], acc[1], acc[2], acc[3]);
-    po[1] = make_float4(acc[4], acc[5], acc[6], acc[7]);
-    if ((threadIdx.x & 15) == 0) {
-      a.part_ml[base * 2 + 0] = M;
-      a.part_ml[base * 2 + 1] = L;
+      for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
+      if (r == 0) {
+        a.part_ml[base * 2 + 0] = mr[i];
+        a.part_ml[base * 2 + 1] = lr[i];
+      }
     }
   }
 }
@@ -272,7 +263,9 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnArgs a) {
 
   RowState st;
   init_state(st, a, qrow, head, valid, lane);
-  for (int kb = 0; kb < wave_limit; kb += CH) chunk(st, a, bt, kvh, kb, limit, lane);
+  int kb = 0;
+  for (; kb + 64 <= wave_limit && ((kb % a.BS) + 64 <= a.BS); kb += 64) chunk<2>(st, a, bt, kvh, kb, limit, lane);
+  for (; kb < wave_limit; kb += CH) chunk<1>(st, a, bt, kvh, kb, limit, lane);
 
   float l = st.l + __shfl_xor(st.l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -321,7 +314,7 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   a.part_ml = part_ml;
   a.n_parts = n_parts;
   a.part_size = part_size;
-  hipLaunchKernelGGL(attn_decode_kernel, dim3(n_parts, nkv, S), dim3(256), 0, stream, a);
+  hipLaunchKernelGGL(attn_decode_kernel, dim3((n_parts + 3) / 4, nkv, S), dim3(256), 0, stream, a);
   if (n_parts > 1) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -154,7 +154,7 @@ class LLMEngine:
         self._static = None
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
-                      "evictions": 0, "requests": 0}
+                      "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0}
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -364,6 +364,8 @@ class LLMEngine:
         self.stats["steps"] += 1
         self.stats["prefill_tokens"] += sum(q for _, q in chunks)
         self.stats["decode_tokens"] += len(decode)
+        self.stats["decode_ctx_tokens"] += sum(s.n_cached for s in decode)
+        self.stats["prefill_ctx_tokens"] += sum(s.n_cached * q for s, q in chunks)
         if sample_rows:
             self._sample_and_advance(logits, [s for _, s in sample_rows])
         return True

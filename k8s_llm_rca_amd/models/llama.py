@@ -27,6 +27,7 @@ import torch.nn.functional as F
 
 from ..ops import attention as A
 from ..ops import norm as N
+from ..ops.linear import linear
 from ..parallel.groups import ParallelContext, single
 from .config import ModelConfig
 from . import moe as MOE
@@ -119,7 +120,7 @@ class LlamaModel:
                 N.rmsnorm(residual, L["in_norm"], cfg.rms_eps, out=y)
             else:
                 N.rmsnorm(prev, L["in_norm"], cfg.rms_eps, residual=residual, out=y)
-            qkv = F.linear(y, L["wqkv"])
+            qkv = linear(y, L["wqkv"])
             A.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, k_cache[li], v_cache[li], self.nq, self.nkv)
             if inp.meta_decode is not None and nd > 0:
                 A.paged_attention(qkv[:nd], k_cache[li], v_cache[li], inp.meta_decode, self.nq, self.nkv, self.scale,
@@ -127,17 +128,17 @@ class LlamaModel:
             if inp.meta_prefill is not None and nd < T:
                 A.paged_attention(qkv[nd:], k_cache[li], v_cache[li], inp.meta_prefill, self.nq, self.nkv,
                                   self.scale, out=attn[nd:])
-            o = F.linear(attn, L["wo"])
+            o = linear(attn, L["wo"])
             self.pc.all_reduce(o)
             N.rmsnorm(o, L["post_norm"], cfg.rms_eps, residual=residual, out=y)
             if self.moe is not None:
                 prev = self.moe.forward(li, y)
             else:
-                gu = F.linear(y, L["w_gu"])
+                gu = linear(y, L["w_gu"])
                 act = N.silu_mul(gu)
-                prev = F.linear(act, L["w_down"])
+                prev = linear(act, L["w_down"])
                 self.pc.all_reduce(prev)
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
-        logits = F.linear(sel, self.lm_head)
+        logits = linear(sel, self.lm_head)
         return self.pc.all_gather_last(logits)

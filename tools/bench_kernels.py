@@ -1,0 +1,124 @@
+"""Microbenchmarks of the hot kernels at the RCA workload's shapes (Llama-3-8B).
+
+Prints achieved HBM bandwidth / TFLOP/s per kernel so kernel work can be
+prioritised from measurements (run on the GPU box).
+"""
+import argparse
+import json
+import math
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, ".")
+from k8s_llm_rca_amd.ops import attention as A  # noqa: E402
+from k8s_llm_rca_amd.ops import norm as N  # noqa: E402
+
+
+def timeit(fn, iters=50, warm=5):
+    for _ in range(warm):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e3  # us
+
+
+def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
+    S = len(ctx)
+    nbs = [(c + BS - 1) // BS for c in ctx]
+    maxb = max(nbs)
+    perm = torch.randperm(sum(nbs))
+    bt = torch.zeros(S, maxb, dtype=torch.int32)
+    u = 0
+    for s, nb in enumerate(nbs):
+        bt[s, :nb] = perm[u:u + nb].int()
+        u += nb
+    qs = [0]
+    for l in qlen:
+        qs.append(qs[-1] + l)
+    meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
+                      q_start=torch.tensor(qs, dtype=torch.int32, device=dev), num_seqs=S, decode=decode)
+    if decode:
+        n = max(1, (max(ctx) + part_size - 1) // part_size)
+        meta.n_parts = 1 << (n - 1).bit_length()
+        meta.part_size = part_size
+        meta.part_o = torch.empty(S * nq * meta.n_parts * 128, dtype=torch.float32, device=dev)
+        meta.part_ml = torch.empty(S * nq * meta.n_parts * 2, dtype=torch.float32, device=dev)
+    else:
+        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv)
+        meta.tile_seq = torch.tensor(ts, dtype=torch.int32, device=dev)
+        meta.tile_tok0 = torch.tensor(t0, dtype=torch.int32, device=dev)
+        meta.tile_len = torch.tensor(tl, dtype=torch.int32, device=dev)
+        meta.n_tiles = len(ts)
+    return meta, sum(nbs)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--what", default="all")
+    args = ap.parse_args()
+    dev = "cuda"
+    torch.manual_seed(0)
+    nq, nkv, BS, H, I = 32, 8, 64, 4096, 14336
+    res = {}
+    if args.what in ("all", "attn"):
+        for B, ctxv, ps in [(64, 3400, 256), (64, 3400, 512), (16, 3400, 256), (128, 2000, 256), (64, 800, 256)]:
+            ctx = [ctxv] * B
+            meta, nb = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True, ps)
+            kc = torch.randn(nb, nkv, BS, 128, device=dev).bfloat16()
+            vc = torch.randn(nb, nkv, 128, BS, device=dev).bfloat16()
+            q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+            out = torch.empty(B, nq * 128, device=dev).bfloat16()
+            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out))
+            byts = B * ctxv * nkv * 128 * 2 * 2
+            res[f"decode B{B} ctx{ctxv} part{ps}"] = f"{us:.1f}us {byts / us / 1e6:.2f} TB/s"
+        for T, ctxv in [(512, 3000), (2048, 2048), (64, 3000)]:
+            S = max(1, 4096 // T)
+            ctx = [ctxv] * S
+            meta, nb = make_meta(ctx, [T] * S, nq, nkv, BS, dev, False)
+            kc = torch.randn(nb, nkv, BS, 128, device=dev).bfloat16()
+            vc = torch.randn(nb, nkv, 128, BS, device=dev).bfloat16()
+            q = torch.randn(T * S, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+            out = torch.empty(T * S, nq * 128, device=dev).bfloat16()
+            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out), iters=10)
+            # causal-ish flops: each query attends to (ctx - T + i) keys
+            pairs = S * sum(ctxv - T + i + 1 for i in range(T))
+            fl = pairs * nq * 128 * 4
+            res[f"prefill S{S} q{T} ctx{ctxv}"] = f"{us:.1f}us {fl / us / 1e6:.1f} TFLOP/s"
+    if args.what in ("all", "gemm"):
+        for M in (1, 16, 64, 128):
+            for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:
+                x = torch.randn(M, k, device=dev).bfloat16()
+                w = torch.randn(n, k, device=dev).bfloat16()
+                us = timeit(lambda: torch.nn.functional.linear(x, w), iters=20)
+                res[f"gemm M{M} N{n} K{k}"] = f"{us:.1f}us {n * k * 2 / us / 1e6:.2f} TB/s"
+                if M <= 128:
+                    from k8s_llm_rca_amd.ops import linear as LIN
+                    LIN.SKINNY_MAX_M = 128
+                    us2 = timeit(lambda: LIN.linear(x, w), iters=20)
+                    res[f"skinny M{M} N{n} K{k}"] = f"{us2:.1f}us {n * k * 2 / us2 / 1e6:.2f} TB/s"
+                    us3 = timeit(lambda: torch.matmul(w, x.t()).t(), iters=20)
+                    res[f"swapT M{M} N{n} K{k}"] = f"{us3:.1f}us {n * k * 2 / us3 / 1e6:.2f} TB/s"
+    if args.what in ("all", "misc"):
+        for T in (64, 4096):
+            x = torch.randn(T, H, device=dev).bfloat16()
+            r = torch.randn(T, H, device=dev).bfloat16()
+            w = torch.ones(H, device=dev).bfloat16()
+            us = timeit(lambda: N.rmsnorm(x, w, 1e-5, residual=r))
+            res[f"rmsnorm T{T}"] = f"{us:.1f}us {T * H * 2 * 4 / us / 1e6:.2f} TB/s"
+            gu = torch.randn(T, 2 * I, device=dev).bfloat16()
+            us = timeit(lambda: N.silu_mul(gu))
+            res[f"silu_mul T{T}"] = f"{us:.1f}us {T * I * 2 * 3 / us / 1e6:.2f} TB/s"
+    for k, v in res.items():
+        print(f"{k:40s} {v}")
+    json.dump(res, open("gpurun_out/bench_kernels.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()

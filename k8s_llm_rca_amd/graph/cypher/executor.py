@@ -363,7 +363,8 @@ class Executor:
         cur_ids = table.cols[cur]
         valid = np.nonzero(cur_ids >= 0)[0]
         uniq, inv = np.unique(cur_ids[valid], return_inverse=True)
-        walks = self.g.var_length(uniq, r.min_hops, r.max_hops, direction, r.types or None)
+        end_label = npat.labels[0] if (len(npat.labels) == 1 and nxt not in table.cols) else None
+        walks = self.g.var_length(uniq, r.min_hops, r.max_hops, direction, r.types or None, end_label)
         by_start: Dict[int, List[Tuple[List[int], List[int]]]] = {}
         for srow, nodes, edges in walks:
             by_start.setdefault(srow, []).append((nodes, edges))

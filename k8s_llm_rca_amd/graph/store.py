@@ -273,6 +273,8 @@ class PropertyGraph:
         ``direction`` is 'out', 'in' or 'both'.  ``rel_types`` / ``key`` filter
         edges by type / interned key equality.
         """
+        if self.device is not None and len(ids) >= self.device.min_gpu_rows:
+            return self.device.expand(np.asarray(ids), direction, rel_types, key)
         tids = None
         if rel_types:
             tids = np.asarray([self.rel_types.lookup(t) for t in rel_types], dtype=np.int32)
@@ -307,16 +309,30 @@ class PropertyGraph:
         return row[order], eid[order], nbr[order]
 
     def var_length(self, starts: np.ndarray, min_hops: int, max_hops: int, direction: str,
-                   rel_types: Optional[Sequence[str]] = None) -> List[Tuple[int, List[int], List[int]]]:
+                   rel_types: Optional[Sequence[str]] = None,
+                   end_label: Optional[str] = None) -> List[Tuple[int, List[int], List[int]]]:
         """Enumerate relationship-unique walks of ``min_hops..max_hops`` hops from each start.
 
         Returns a list of ``(start_row, node_ids, edge_ids)`` (Cypher
         var-length semantics: a relationship appears at most once per path).
+        ``end_label`` keeps only walks ending on that label (planner pushdown).
         """
+        if (self.device is not None and len(starts) >= self.device.min_gpu_rows and 1 <= min_hops
+                and max_hops <= 3):
+            rec = self.device.walks(np.asarray(starts), min_hops, max_hops, direction, rel_types, end_label)
+            out = []
+            for r in rec.tolist():
+                h = r[1]
+                out.append((r[0], r[2:3 + h], r[6:6 + h]))
+            return out
         tids = None
         if rel_types:
             tids = np.asarray([self.rel_types.lookup(t) for t in rel_types], dtype=np.int32)
-        return _native.var_length(self, starts, min_hops, max_hops, direction, tids)
+        walks = _native.var_length(self, starts, min_hops, max_hops, direction, tids)
+        if end_label is not None:
+            lid = self.labels.lookup(end_label)
+            walks = [w for w in walks if self.node_label[w[1][-1]] == lid]
+        return walks
 
     def state_lookup(self, entity_ids: np.ndarray, ts_ms: np.ndarray, state_label: Optional[str] = None,
                      mode: str = "strict", tmax_ms: Optional[np.ndarray] = None,

@@ -198,6 +198,33 @@ class AssistantService:
             msgs = msgs[::-1]
         return MessageList(msgs[:limit], has_more=len(msgs) > limit)
 
+    # --------------------------------------------------------- persistence
+    def export_state(self) -> dict:
+        """Assistants + threads + messages as plain JSON (resume across processes,
+        the reference's retrieve_assistant / retrieve_thread, openai_generic_assistant.py:25-35)."""
+        with self._lock:
+            asst = [vars(a).copy() for a in self.assistants.values()]
+            threads = []
+            for ts in self.threads.values():
+                with ts.lock:
+                    threads.append({"id": ts.thread.id, "created_at": ts.thread.created_at,
+                                    "messages": [{"id": m.id, "role": m.role, "text": m.text,
+                                                  "created_at": m.created_at, "assistant_id": m.assistant_id,
+                                                  "run_id": m.run_id} for m in ts.messages]})
+        return {"assistants": asst, "threads": threads}
+
+    def import_state(self, state: dict) -> None:
+        with self._lock:
+            for a in state.get("assistants", []):
+                self.assistants[a["id"]] = Assistant(**a)
+            for t in state.get("threads", []):
+                ts = ThreadState(Thread(t["id"], t["created_at"]))
+                for m in t["messages"]:
+                    ts.messages.append(Message(m["id"], t["id"], m["role"], [TextContent(Text(m["text"]))],
+                                               m["created_at"], m.get("assistant_id"), m.get("run_id")))
+                self.threads[t["id"]] = ts
+                self._runs_by_thread.setdefault(t["id"], [])
+
     # ------------------------------------------------------------------ runs
     def create_run(self, thread_id: str, assistant_id: str, instructions: Optional[str] = None,
                    response_format: Any = None, max_tokens: Optional[int] = None,

@@ -399,7 +399,7 @@ class LLMEngine:
 
     def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int]):
         t0 = time.perf_counter()
-        if not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode:
+        if not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1:
             out = self._forward_graph(decode)
             self.stats["graph_steps"] += 1
             self.stats["decode_steps"] += 1
@@ -427,43 +427,118 @@ class LLMEngine:
             o += n
         return out
 
-    def _forward_eager(self, decode, chunks, sample_idx):
-        from ..models.llama import StepInputs
+    # Step wire format (also the TP broadcast): header int64[12] + one int32 payload
+    # = ids[T] pos[T] slots[T] sidx[ns] | bt_d ctx_d qs_d | bt_p ctx_p qs_p tseq ttok0 tlen
+    HDR = 12
 
+    def _pack_step(self, decode, chunks, sample_idx):
         rows = [(s, 1) for s in decode] + list(chunks)
         ids, pos, slots = self._token_arrays(rows)
         arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
-        dmeta = pmeta = None
+        nd = len(decode)
+        maxb_d = maxb_p = n_tiles = 0
+        n_parts = 1
         if decode:
             bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
+            maxb_d = bt_d.shape[1]
+            n_parts = self._n_parts(int(ctx_d.max()))
             arrays += [bt_d, ctx_d, qs_d]
         if chunks:
             bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
+            maxb_p = bt_p.shape[1]
             ts, t0, tl = A.build_prefill_tiles(qs_p.tolist(), self.model.nq // self.model.nkv)
+            n_tiles = len(ts)
             arrays += [bt_p, ctx_p, qs_p, np.asarray(ts, np.int32), np.asarray(t0, np.int32),
                        np.asarray(tl, np.int32)]
-        dev = self._to_dev(arrays)
-        d_ids, d_pos, d_slots, d_sidx = dev[:4]
-        k = 4
-        if decode:
-            bt, ctx, qs = dev[k:k + 3]
-            k += 3
-            n_parts = self._n_parts(int(ctx_d.max()))
-            dmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=len(decode), decode=True,
-                               n_parts=n_parts, part_size=PART_SIZE, ctx_lens_host=ctx_d.tolist(),
-                               q_start_host=qs_d.tolist())
+        flat = np.concatenate([x.reshape(-1).astype(np.int32, copy=False) for x in arrays])
+        header = np.array([1, flat.size, len(ids), nd, nd, maxb_d, len(chunks), maxb_p, n_tiles,
+                           len(sample_idx), n_parts, 0], dtype=np.int64)
+        return header, flat
+
+    def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor):
+        """Build StepInputs from the wire format and run the forward (every TP rank)."""
+        from ..models.llama import StepInputs
+
+        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, _ = [int(v) for v in header]
+        o = 0
+
+        def take(n, shape=None):
+            nonlocal o
+            d = flat_dev[o:o + n]
+            h = flat_host[o:o + n] if flat_host is not None else None
+            o += n
+            if shape is not None:
+                d = d.view(*shape)
+            return d, h
+
+        d_ids, _ = take(T)
+        d_pos, _ = take(T)
+        d_slots, _ = take(T)
+        d_sidx, _ = take(ns)
+        dmeta = pmeta = None
+        if n_dec:
+            bt, _ = take(n_dec * maxb_d, (n_dec, maxb_d))
+            ctx, ctx_h = take(n_dec)
+            qs, qs_h = take(n_dec + 1)
+            dmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=n_dec, decode=True,
+                               n_parts=n_parts, part_size=PART_SIZE,
+                               ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
+                               q_start_host=None if qs_h is None else qs_h.tolist())
             if n_parts > 1:
-                dmeta.part_o = torch.empty(len(decode) * self.model.nq * n_parts * self.model.D,
-                                           dtype=torch.float32, device=self.device)
-                dmeta.part_ml = torch.empty(len(decode) * self.model.nq * n_parts * 2, dtype=torch.float32,
+                dmeta.part_o = torch.empty(n_dec * self.model.nq * n_parts * self.model.D, dtype=torch.float32,
+                                           device=self.device)
+                dmeta.part_ml = torch.empty(n_dec * self.model.nq * n_parts * 2, dtype=torch.float32,
                                             device=self.device)
-        if chunks:
-            bt, ctx, qs, tsd, t0d, tld = dev[k:k + 6]
-            pmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=len(chunks), decode=False,
-                               tile_seq=tsd, tile_tok0=t0d, tile_len=tld, n_tiles=len(ts),
-                               ctx_lens_host=ctx_p.tolist(), q_start_host=qs_p.tolist())
-        inp = StepInputs(d_ids, d_pos, d_slots, len(decode), dmeta, pmeta, d_sidx.long())
+        if n_pre:
+            bt, _ = take(n_pre * maxb_p, (n_pre, maxb_p))
+            ctx, ctx_h = take(n_pre)
+            qs, qs_h = take(n_pre + 1)
+            tsd, _ = take(n_tiles)
+            t0d, _ = take(n_tiles)
+            tld, _ = take(n_tiles)
+            pmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=n_pre, decode=False,
+                               tile_seq=tsd, tile_tok0=t0d, tile_len=tld, n_tiles=n_tiles,
+                               ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
+                               q_start_host=None if qs_h is None else qs_h.tolist())
+        inp = StepInputs(d_ids, d_pos, d_slots, nd, dmeta, pmeta, d_sidx.long())
         return self.model.forward(inp, self.kv.k, self.kv.v)
+
+    def _bcast(self, t: torch.Tensor) -> None:
+        import torch.distributed as dist
+        dist.broadcast(t, src=0, group=self.pc.tp_group)
+
+    def _comm_device(self):
+        return self.device if self.device.type == "cuda" else torch.device("cpu")
+
+    def _forward_eager(self, decode, chunks, sample_idx):
+        header, flat = self._pack_step(decode, chunks, sample_idx)
+        if self.pc.tp_size > 1:
+            h = torch.from_numpy(header).to(self._comm_device())
+            self._bcast(h)
+        dev = self._to_dev([flat])[0]
+        if self.pc.tp_size > 1:
+            self._bcast(dev)
+        return self._exec_step(header, flat, dev)
+
+    def serve_worker(self) -> None:
+        """TP ranks > 0: replay every step rank 0 schedules until it sends STOP."""
+        assert self.pc.tp_rank > 0
+        cd = self._comm_device()
+        while True:
+            h = torch.empty(self.HDR, dtype=torch.int64, device=cd)
+            self._bcast(h)
+            header = h.cpu().numpy()
+            if header[0] == 0:
+                return
+            dev = torch.empty(int(header[1]), dtype=torch.int32, device=self.device)
+            self._bcast(dev)
+            host = dev.numpy() if self.device.type == "cpu" else None
+            self._exec_step(header, host, dev)
+
+    def stop_workers(self) -> None:
+        if self.pc.tp_size > 1 and self.pc.tp_rank == 0:
+            h = torch.zeros(self.HDR, dtype=torch.int64, device=self._comm_device())
+            self._bcast(h)
 
     @staticmethod
     def _n_parts(max_ctx: int) -> int:

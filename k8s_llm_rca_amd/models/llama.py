@@ -46,7 +46,7 @@ class StepInputs:
 
 class LlamaModel:
     def __init__(self, cfg: ModelConfig, device, dtype=torch.bfloat16, pc: Optional[ParallelContext] = None,
-                 seed: int = 0, init: bool = True):
+                 seed: int = 0, init: bool = True, init_mode: str = "shard"):
         self.cfg = cfg
         self.device = torch.device(device)
         self.dtype = dtype
@@ -63,6 +63,7 @@ class LlamaModel:
         self.cos_sin = A.rope_cos_sin(cfg.max_position, cfg.rope_theta, self.D, cfg.scaling_dict(), device=self.device)
         self.layers: List[Dict[str, torch.Tensor]] = []
         self.moe: Optional[MOE.MoELayerSet] = None
+        self.init_mode = init_mode
         if init:
             self._random_init(seed)
 
@@ -74,28 +75,66 @@ class LlamaModel:
         return t
 
     def _random_init(self, seed: int) -> None:
+        """Seeded random weights in the real shapes.
+
+        ``init_mode='shard'``: each TP rank draws only its own shard (fast: a
+        70B/TP8 rank never materialises the full model).  ``'full_slice'``:
+        every rank draws the FULL tensors from the same seed and keeps its slice,
+        so a TP=k model equals the TP=1 model exactly (used by the parity tests).
+        """
         cfg = self.cfg
+        tp, r = self.pc.tp_size, self.pc.tp_rank
+        full = self.init_mode == "full_slice"
         g = torch.Generator(device=self.device)
-        g.manual_seed(seed * 1000 + self.pc.tp_rank)
-        H = cfg.hidden
-        qkv_out = (self.nq + 2 * self.nkv) * self.D
+        g.manual_seed(seed * 1000 + (0 if full else r))
+        H, D = cfg.hidden, self.D
         out_std = cfg.init_std / math.sqrt(2 * cfg.n_layers)
+        nq, nkv = self.nq, self.nkv
+        kv_rep = cfg.n_kv_heads < tp  # kv heads replicated across ranks
+
+        def qkv_shard():
+            if not full:
+                return self._randn(g, (nq + 2 * nkv) * D, H)
+            w = self._randn(g, (cfg.n_heads + 2 * cfg.n_kv_heads) * D, H)
+            q = w[: cfg.n_heads * D].view(cfg.n_heads, D, H)[r * nq:(r + 1) * nq]
+            kh = (r * cfg.n_kv_heads) // tp if kv_rep else r * nkv
+            k = w[cfg.n_heads * D:(cfg.n_heads + cfg.n_kv_heads) * D].view(cfg.n_kv_heads, D, H)[kh:kh + nkv]
+            v = w[(cfg.n_heads + cfg.n_kv_heads) * D:].view(cfg.n_kv_heads, D, H)[kh:kh + nkv]
+            return torch.cat([q.reshape(-1, H), k.reshape(-1, H), v.reshape(-1, H)]).contiguous()
+
+        def cols(n_out, n_in_full, lo, hi, std):
+            if not full:
+                return self._randn(g, n_out, hi - lo, std=std)
+            return self._randn(g, n_out, n_in_full, std=std)[:, lo:hi].contiguous()
+
         for _ in range(cfg.n_layers):
             L = {
                 "in_norm": torch.ones(H, dtype=self.dtype, device=self.device),
                 "post_norm": torch.ones(H, dtype=self.dtype, device=self.device),
-                "wqkv": self._randn(g, qkv_out, H),
-                "wo": self._randn(g, H, self.nq * self.D, std=out_std),
+                "wqkv": qkv_shard(),
+                "wo": cols(H, cfg.n_heads * D, r * nq * D, (r + 1) * nq * D, out_std),
             }
             if cfg.n_experts == 0:
-                L["w_gu"] = self._randn(g, 2 * self.inter, H)
-                L["w_down"] = self._randn(g, H, self.inter, std=out_std)
+                I, Il = cfg.intermediate, self.inter
+                if full:
+                    gu = self._randn(g, 2 * I, H)
+                    L["w_gu"] = torch.cat([gu[r * Il:(r + 1) * Il], gu[I + r * Il: I + (r + 1) * Il]]).contiguous()
+                else:
+                    L["w_gu"] = self._randn(g, 2 * Il, H)
+                L["w_down"] = cols(H, I, r * Il, (r + 1) * Il, out_std)
             self.layers.append(L)
         if cfg.n_experts:
-            self.moe = MOE.MoELayerSet(cfg, self.device, self.dtype, self.pc, g, out_std)
+            self.moe = MOE.MoELayerSet(cfg, self.device, self.dtype, self.pc, g, out_std, full_slice=full)
         self.embed = self._randn(g, cfg.vocab_size, H)
         self.final_norm = torch.ones(H, dtype=self.dtype, device=self.device)
-        self.lm_head = self._randn(g, self.vocab_local, H)
+        if full:
+            lm = self._randn(g, cfg.vocab_size, H)
+            pad = self.vocab_local * tp - cfg.vocab_size
+            if pad:
+                lm = torch.cat([lm, torch.zeros(pad, H, dtype=self.dtype, device=self.device)])
+            self.lm_head = lm[r * self.vocab_local:(r + 1) * self.vocab_local].contiguous()
+        else:
+            self.lm_head = self._randn(g, self.vocab_local, H)
 
     def weight_bytes(self) -> int:
         n = sum(t.numel() * t.element_size() for L in self.layers for t in L.values())

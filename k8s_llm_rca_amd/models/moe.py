@@ -21,7 +21,8 @@ from .config import ModelConfig
 
 
 class MoELayerSet:
-    def __init__(self, cfg: ModelConfig, device, dtype, pc: ParallelContext, g: torch.Generator, out_std: float):
+    def __init__(self, cfg: ModelConfig, device, dtype, pc: ParallelContext, g: torch.Generator, out_std: float,
+                 full_slice: bool = False):
         self.cfg = cfg
         self.pc = pc
         self.E = cfg.n_experts
@@ -35,16 +36,18 @@ class MoELayerSet:
         self.router: List[torch.Tensor] = []
         self.w13: List[torch.Tensor] = []
         self.w2: List[torch.Tensor] = []
+        ne = self.E if full_slice else self.E_local
+        sl = slice(self.e0, self.e0 + self.E_local) if full_slice else slice(0, self.E_local)
         for _ in range(cfg.n_layers):
             r = torch.empty(self.E, H, dtype=dtype, device=device)
             r.normal_(0.0, cfg.init_std, generator=g)
             self.router.append(r)
-            w13 = torch.empty(self.E_local, 2 * I, H, dtype=dtype, device=device)
+            w13 = torch.empty(ne, 2 * I, H, dtype=dtype, device=device)
             w13.normal_(0.0, cfg.init_std, generator=g)
-            w2 = torch.empty(self.E_local, H, I, dtype=dtype, device=device)
+            w2 = torch.empty(ne, H, I, dtype=dtype, device=device)
             w2.normal_(0.0, out_std, generator=g)
-            self.w13.append(w13)
-            self.w2.append(w2)
+            self.w13.append(w13[sl].contiguous())
+            self.w2.append(w2[sl].contiguous())
 
     def weight_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for lst in (self.router, self.w13, self.w2) for t in lst)

@@ -1,0 +1,153 @@
+"""Engine, scheduler and constrained-decoding semantics on CPU (tiny models)."""
+import json
+import random
+
+import numpy as np
+import pytest
+import torch
+
+from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+from k8s_llm_rca_amd.engine.grammar import Choice, Free, Grammar, Lit, Repeat
+from k8s_llm_rca_amd.engine.structured import GrammarRuntime, GrammarState
+from k8s_llm_rca_amd.engine.tokenizer import get_tokenizer
+from k8s_llm_rca_amd.graph.schema import EXTERNAL_KINDS, NATIVE_KINDS
+from k8s_llm_rca_amd.pipeline import formats as F
+from k8s_llm_rca_amd.pipeline.find_metapath import extract_json
+from k8s_llm_rca_amd.pipeline.generate_query import extract_cypher
+
+
+def _engine(model="tiny-llama", **kw):
+    cfg = dict(model=model, device="cpu", dtype=torch.float32, num_blocks=64, block_size=32, max_batch_tokens=128,
+               temperature=0.8)
+    cfg.update(kw)
+    return LLMEngine(EngineConfig(**cfg))
+
+
+def _walk(rt, tok, g, seed, hints=True):
+    rnd = random.Random(seed)
+    st = GrammarState(rt, g, [tok.eot_id], 64, use_hints=hints)
+    ids = []
+    while True:
+        a, arg = st.action()
+        if a == "done":
+            break
+        if a == "force":
+            ids += arg
+            continue
+        kind, m = arg
+        if kind == "list":
+            t = rnd.choice(m)
+        else:
+            bits = np.unpackbits(rt.masks.rows[m].view(np.uint8), bitorder="little")
+            t = int(rnd.choice(np.nonzero(bits)[0]))
+        ids.append(t)
+        st.advance(t)
+    return tok.decode(ids)
+
+
+@pytest.mark.parametrize("hints", [True, False])
+def test_locator_grammar_always_parses(hints):
+    tok = get_tokenizer()
+    rt = GrammarRuntime(tok, 128256)
+    kinds = NATIVE_KINDS + EXTERNAL_KINDS
+    b = F.GenerationBudget()
+    for seed in range(6):
+        g = F.locator_grammar(kinds, "Pod", b, ("Pod", "nfs", ["Pod", "PersistentVolumeClaim", "nfs"]))
+        j = extract_json(_walk(rt, tok, g, seed, hints))
+        assert j["DestinationKind"] in kinds and all(k in kinds for k in j["RelevantResources"])
+        if hints:
+            assert j["DestinationKind"] == "nfs" and j["RelevantResources"] == ["Pod", "PersistentVolumeClaim", "nfs"]
+
+
+def test_cypher_grammar_parses_and_hints_match_template():
+    from k8s_llm_rca_amd.graph.cypher import parse
+    from k8s_llm_rca_amd.pipeline.generate_query import human_generate_cypher_query
+    tok = get_tokenizer()
+    rt = GrammarRuntime(tok, 128256)
+    mp = ("\n    HasEvent, Event, EVENT, metadata_uid;\n    ReferInternal, Event, Pod, involvedObject_uid;\n"
+          "    ReferInternal, Pod, Secret, spec_volumes_secret_secretName;\n")
+    msg = 'secret "x" not found'
+    for seed in range(4):
+        q = extract_cypher(_walk(rt, tok, F.cypher_grammar(mp, msg, hint=seed % 2 == 0), seed))
+        parse(q)  # every constrained generation is valid Cypher
+    q = extract_cypher(_walk(rt, tok, F.cypher_grammar(mp, msg, hint=True), 0))
+    assert q.replace("\n\n", "\n") == human_generate_cypher_query(mp, msg).replace("\n\n", "\n")
+
+
+def test_summary_grammar_is_json():
+    tok = get_tokenizer()
+    rt = GrammarRuntime(tok, 128256)
+    b = F.GenerationBudget(explanation_tokens=6, conclusion_tokens=6, resolution_tokens=6)
+    for seed in range(4):
+        j = json.loads(_walk(rt, tok, F.summary_grammar(["Pod", "Secret"], b, "Secret"), seed))
+        assert {e["kind"] for e in j["summary"]} == {"Pod", "Secret"}
+
+
+def test_prefix_reuse_and_generation_lengths():
+    eng = _engine()
+    sid = eng.new_sequence()
+    p1 = eng.tok.system_prefix("sys") + eng.tok.message("user", "hello " * 40) + eng.tok.header("assistant")
+    out = {}
+    eng.submit(sid, p1, None, 10, on_done=lambda g, st: out.setdefault("a", (g, st)))
+    eng.run_until_idle()
+    g1, st1 = out["a"]
+    assert len(g1) <= 10 and st1["prompt_tokens"] == len(p1)
+    pre = eng.stats["prefill_tokens"]
+    p2 = eng.seqs[sid].tokens + eng.tok.message("user", "again") + eng.tok.header("assistant")
+    eng.submit(sid, p2, None, 5, on_done=lambda g, st: out.setdefault("b", (g, st)))
+    eng.run_until_idle()
+    new = len(eng.tok.message("user", "again") + eng.tok.header("assistant")) + 1  # + the pending eot
+    assert eng.stats["prefill_tokens"] - pre <= new + 1
+
+
+def test_eviction_and_recompute_under_kv_pressure():
+    eng = _engine(num_blocks=12)
+    outs = {}
+    sids = [eng.new_sequence() for _ in range(4)]
+    for i, sid in enumerate(sids):
+        p = eng.tok.system_prefix("s") + eng.tok.message("user", ("x%d " % i) * 60) + eng.tok.header("assistant")
+        eng.submit(sid, p, None, 6, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+        eng.run_until_idle()
+    assert len(outs) == 4
+    assert eng.stats["evictions"] > 0
+    # the first thread was evicted: its next run re-prefills and still completes
+    p = eng.seqs[sids[0]].tokens + eng.tok.message("user", "more") + eng.tok.header("assistant")
+    eng.submit(sids[0], p, None, 4, on_done=lambda g, st: outs.__setitem__("again", g))
+    eng.run_until_idle()
+    assert "again" in outs
+
+
+def test_backend_truncates_long_threads():
+    from k8s_llm_rca_amd.api.assistant import GenericAssistant
+    from k8s_llm_rca_amd.api.service import AssistantService
+    from k8s_llm_rca_amd.engine.backend import EngineBackend
+    eng = _engine(max_context=600, num_blocks=128)
+    svc = AssistantService(EngineBackend(eng, default_max_tokens=8, keep_seed=1))
+    a = GenericAssistant(svc)
+    a.create_assistant("You are terse.", "t", "tiny-llama")
+    a.create_thread()
+    a.add_message("seed message that must survive")
+    eng.start()
+    try:
+        for i in range(12):
+            a.add_message(f"incident {i} " + "detail " * 30)
+            a.run_assistant(max_tokens=8)
+            m = a.wait_get_last_k_message(1, timeout=120)
+            assert m is not None
+        assert len(eng.seqs[a.service.threads[a.thread.id].backend_state.sid].tokens) <= 600
+        usage = a.get_token_usage(0, 1e12, 50)
+        assert usage["completion_tokens"] > 0
+    finally:
+        eng.stop()
+
+
+def test_mixtral_and_opt_engines_generate():
+    for model in ("tiny-mixtral", "tiny-opt"):
+        eng = _engine(model)
+        sid = eng.new_sequence()
+        out = {}
+        g = Grammar([Lit('{"a": '), Choice(['"x"', '"yy"'], "c"), Lit("}")])
+        eng.submit(sid, eng.tok.system_prefix("s") + eng.tok.header("assistant"), g, 8,
+                   on_done=lambda gen, st: out.setdefault("t", eng.tok.decode(gen)))
+        eng.run_until_idle()
+        assert json.loads(out["t"])["a"] in ("x", "yy")

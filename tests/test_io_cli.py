@@ -1,0 +1,51 @@
+"""Graph persistence, CLI drivers and assistant-service state round trips."""
+import json
+import os
+
+from k8s_llm_rca_amd.api.service import AssistantService, ScriptedBackend
+from k8s_llm_rca_amd.graph import io as GIO
+from k8s_llm_rca_amd.graph.cypher import Executor
+from k8s_llm_rca_amd.graph.synth import generate_cluster
+
+
+def test_graph_roundtrip(tmp_path):
+    c = generate_cluster(1500, 5, seed=3)
+    p = str(tmp_path / "g.jsonl.gz")
+    GIO.save_graph(c.stategraph, p)
+    g2 = GIO.load_graph(p)
+    assert g2.num_nodes == c.stategraph.num_nodes and g2.num_edges == c.stategraph.num_edges
+    q = "MATCH (e:EVENT) WHERE e.message CONTAINS $m RETURN e.timestamp AS t"
+    for inc in c.incidents:
+        a = Executor(c.stategraph).run(q, {"m": inc.message})
+        b = Executor(g2).run(q, {"m": inc.message})
+        assert [r["t"] for r in a] == [r["t"] for r in b]
+    GIO.save_incidents_csv(c.incidents, str(tmp_path / "i.csv"))
+    back = GIO.load_incidents_csv(str(tmp_path / "i.csv"))
+    assert [i.message for i in back] == c.messages and back[0].path_kinds == c.incidents[0].path_kinds
+
+
+def test_cli_run_and_resume(tmp_path, capsys):
+    from k8s_llm_rca_amd.cli import main
+    d = str(tmp_path / "c")
+    assert main(["gen-graph", "--graph-nodes", "1500", "--incidents", "4", "--out", d]) == 0
+    out = str(tmp_path / "res.json")
+    assert main(["run", "--graph-dir", d, "--backend", "oracle", "--output", out, "--limit", "2"]) == 0
+    assert main(["run", "--graph-dir", d, "--backend", "oracle", "--output", out, "--resume"]) == 0
+    from k8s_llm_rca_amd.pipeline.rca import read_results
+    res = read_results(out)
+    assert len(res) == 4 and len({r["error_message"] for r in res}) == 4
+
+
+def test_service_state_roundtrip():
+    svc = AssistantService(ScriptedBackend(lambda rs: "reply"))
+    a = svc.create_assistant("ins", "n", "m")
+    t = svc.create_thread()
+    svc.add_message(t.id, "hi")
+    r = svc.create_run(t.id, a.id)
+    svc.wait_run(r.id, 5)
+    st = json.loads(json.dumps(svc.export_state()))
+    svc2 = AssistantService(ScriptedBackend(lambda rs: "x"))
+    svc2.import_state(st)
+    assert svc2.retrieve_assistant(a.id).instructions == "ins"
+    msgs = svc2.list_messages(t.id, order="asc").data
+    assert [m.role for m in msgs] == ["user", "assistant"] and msgs[1].text == "reply"

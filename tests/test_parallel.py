@@ -1,0 +1,129 @@
+"""Tensor / expert parallelism on CPU with gloo (world_size 2), checked against the unsharded model."""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inputs(cfg, device="cpu"):
+    """A mixed step: 2 decode rows + a 7-token prefill chunk over a paged cache."""
+    from k8s_llm_rca_amd.models.llama import StepInputs
+    from k8s_llm_rca_amd.ops import attention as A
+    torch.manual_seed(0)
+    BS = 32
+    ids = torch.randint(0, 500, (9,), dtype=torch.int32)
+    # seq0: ctx 40 (decode), seq1: ctx 3 (decode), seq2: 7 new tokens at positions 5..11
+    pos = torch.tensor([39, 2, 5, 6, 7, 8, 9, 10, 11], dtype=torch.int32)
+    bt_d = torch.tensor([[0, 1], [2, 0]], dtype=torch.int32)
+    slots = torch.tensor([1 * BS + 7, 2 * BS + 2, 3 * BS + 5, 3 * BS + 6, 3 * BS + 7, 3 * BS + 8, 3 * BS + 9,
+                          3 * BS + 10, 3 * BS + 11], dtype=torch.int32)
+    md = A.AttnMeta(block_tables=bt_d, ctx_lens=torch.tensor([40, 3], dtype=torch.int32),
+                    q_start=torch.tensor([0, 1, 2], dtype=torch.int32), num_seqs=2, decode=True,
+                    ctx_lens_host=[40, 3], q_start_host=[0, 1, 2])
+    mp_ = A.AttnMeta(block_tables=torch.tensor([[3]], dtype=torch.int32), ctx_lens=torch.tensor([12], dtype=torch.int32),
+                     q_start=torch.tensor([0, 7], dtype=torch.int32), num_seqs=1, decode=False,
+                     ctx_lens_host=[12], q_start_host=[0, 7])
+    return StepInputs(ids, pos, slots, 2, md, mp_, torch.tensor([0, 1, 8])), BS
+
+
+def _run_model(rank, world, port, name, out_path):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, ep_size=world, ep_rank=rank,
+                         ep_group=dist.group.WORLD)
+    cfg = get_config(name)
+    m = LlamaModel(cfg, "cpu", torch.float32, pc, seed=3, init_mode="full_slice")
+    inp, BS = _inputs(cfg)
+    torch.manual_seed(1)
+    k = torch.randn(cfg.n_layers, 6, m.nkv, BS, 128) * 0.5
+    v = torch.randn(cfg.n_layers, 6, m.nkv, 128, BS)
+    # each rank holds its own kv heads: slice the shared random cache consistently
+    kf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, BS, 128, generator=torch.Generator().manual_seed(7)) * 0.5
+    vf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, 128, BS, generator=torch.Generator().manual_seed(8))
+    h0 = (rank * cfg.n_kv_heads) // world if cfg.n_kv_heads < world else rank * m.nkv
+    k.copy_(kf[:, :, h0:h0 + m.nkv])
+    v.copy_(vf[:, :, h0:h0 + m.nkv])
+    logits = m.forward(inp, k, v)
+    if rank == 0:
+        torch.save(logits[:, : cfg.vocab_size], out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _reference(name):
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    cfg = get_config(name)
+    m = LlamaModel(cfg, "cpu", torch.float32, None, seed=3, init_mode="full_slice")
+    inp, BS = _inputs(cfg)
+    kf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, BS, 128, generator=torch.Generator().manual_seed(7)) * 0.5
+    vf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, 128, BS, generator=torch.Generator().manual_seed(8))
+    return m.forward(inp, kf, vf)[:, : cfg.vocab_size]
+
+
+@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
+def test_tp2_matches_tp1(name):
+    port = _free_port()
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "logits.pt")
+        mp.spawn(_run_model, args=(2, port, name, out), nprocs=2, join=True)
+        got = torch.load(out, weights_only=True)
+    ref = _reference(name)
+    torch.testing.assert_close(got, ref, atol=2e-4, rtol=2e-4)
+
+
+def _run_engine(rank, world, port, out_path):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    if world > 1:
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
+    else:
+        pc = None
+    cfg = EngineConfig(model="tiny-llama", device="cpu", dtype=torch.float32, num_blocks=32, block_size=32,
+                       max_batch_tokens=64, temperature=0.0)
+    model = LlamaModel(get_config("tiny-llama"), "cpu", torch.float32, pc, seed=5, init_mode="full_slice")
+    eng = LLMEngine(cfg, pc, model=model)
+    if rank > 0:
+        eng.serve_worker()
+    else:
+        outs = {}
+        for i in range(3):
+            sid = eng.new_sequence()
+            toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "message %d " % i * (5 + 9 * i)) + \
+                eng.tok.header("assistant")
+            eng.submit(sid, toks, None, 12, temperature=0.0, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+        eng.run_until_idle()
+        eng.stop_workers()
+        torch.save(outs, out_path)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def test_tp2_engine_generation_matches_tp1():
+    with tempfile.TemporaryDirectory() as d:
+        o2, o1 = os.path.join(d, "tp2.pt"), os.path.join(d, "tp1.pt")
+        mp.spawn(_run_engine, args=(2, _free_port(), o2), nprocs=2, join=True)
+        _run_engine(0, 1, _free_port(), o1)
+        a = torch.load(o2, weights_only=True)
+        b = torch.load(o1, weights_only=True)
+    assert a == b and all(len(v) == 12 for v in a.values())

@@ -16,7 +16,9 @@
 //     the PV MFMA's A operand: P goes from the S accumulator to the PV operand
 //     with one bf16 pack and no lane movement.
 //   * the 128-wide head dim is split over the 4 MFMA k-steps as dims
-//     32h+8c+j, so every Q/K fragment is a contiguous 16-byte load.
+//     32c+8h+j: every Q/K fragment is a contiguous 16-byte load and the 4 lanes
+//     holding one key read 64 contiguous bytes per instruction (16 half lines
+//     per wave instruction instead of 32 scattered pieces).
 // Decode (one token / seq): each WAVE owns one (seq, kv head, key partition)
 // and streams its pages 64 keys at a time (32 x 16-byte loads in flight per
 // lane group before the first MFMA); partitions are merged by attn_reduce
@@ -84,7 +86,7 @@ __device__ __forceinline__ void chunk(RowState& st, const AttnArgs& a, const int
   const size_t page = ((size_t)blk * a.nkv + kvh);
   const uint16_t* kp = a.kc + page * (size_t)a.BS * D;
   const uint16_t* vp = a.vc + page * (size_t)D * a.BS;
-  // K fragments: sub-chunk u, tile t, row r -> key 32u + 8*(r>>2) + 4t + (r&3); dims 32h+8c..+8
+  // K fragments: sub-chunk u, tile t, row r -> key 32u + 8*(r>>2) + 4t + (r&3); dims 32c+8h..+8
   bf16x8 kf[NSUB][2][4];
 #pragma unroll
   for (int u = 0; u < NSUB; ++u)
@@ -92,7 +94,7 @@ __device__ __forceinline__ void chunk(RowState& st, const AttnArgs& a, const int
     for (int t = 0; t < 2; ++t) {
       const int key = off + 32 * u + 8 * (r >> 2) + 4 * t + (r & 3);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16(kp + (size_t)key * D + 32 * h + 8 * c);
+      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16(kp + (size_t)key * D + 32 * c + 8 * h);
     }
   // V fragments: column d = 16*dt + r, keys off + 32u + 8h .. +8 (transposed page)
   bf16x8 vf[NSUB][8];
@@ -152,7 +154,7 @@ __device__ __forceinline__ void init_state(RowState& st, const AttnArgs& a, int 
   const int h = lane >> 4;
 #pragma unroll
   for (int c = 0; c < 4; ++c)
-    st.qf[c] = valid ? load16(a.q + (size_t)qrow * a.q_stride + head * D + 32 * h + 8 * c) : zero8();
+    st.qf[c] = valid ? load16(a.q + (size_t)qrow * a.q_stride + head * D + 32 * c + 8 * h) : zero8();
 #pragma unroll
   for (int dt = 0; dt < 8; ++dt) st.o[dt] = f32x4{0.f, 0.f, 0.f, 0.f};
   st.m = -INFINITY;

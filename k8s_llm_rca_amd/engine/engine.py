@@ -43,7 +43,7 @@ from .tokenizer import get_tokenizer
 
 log = logging.getLogger(__name__)
 
-PART_SIZE = 256
+PART_SIZE = 512
 
 
 @dataclass
@@ -154,7 +154,8 @@ class LLMEngine:
         self._static = None
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
-                      "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0}
+                      "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
+                      "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0}
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -323,6 +324,7 @@ class LLMEngine:
     def step(self) -> bool:
         t_host0 = time.perf_counter()
         self._admit()
+        self.stats["admit_s"] += time.perf_counter() - t_host0
         active = [s for s in self.seqs.values() if s.req is not None and s.pending > 0]
         if not active:
             return False
@@ -680,9 +682,11 @@ class LLMEngine:
         d_temps = torch.from_numpy(temps).to(self.device)
         tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
                          vocab=self.vocab)
+        t1 = time.perf_counter()
         toks = tok.tolist()
-        self.stats["sample_s"] += time.perf_counter() - t0
         now = time.perf_counter()
+        self.stats["wait_s"] += now - t1
+        self.stats["sample_s"] += now - t0
         for s, t in zip(seqs, toks):
             r = s.req
             if r.t_first is None:
@@ -701,3 +705,4 @@ class LLMEngine:
             s.tokens.append(t)
             r.gs.advance(t)
             self._drive(r)
+        self.stats["post_s"] += time.perf_counter() - now

@@ -78,6 +78,24 @@ def main():
             us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out))
             byts = B * ctxv * nkv * 128 * 2 * 2
             res[f"decode B{B} ctx{ctxv} part{ps}"] = f"{us:.1f}us {byts / us / 1e6:.2f} TB/s"
+        # TLB reach: same work, pages scattered over a huge pool (as in the engine's 240 GB pool)
+        for pool_gb in (4, 64, 160):
+            B, ctxv = 128, 2000
+            nb_needed = B * ((ctxv + BS - 1) // BS)
+            nb_pool = max(nb_needed, int(pool_gb * 2**30 // (nkv * BS * 128 * 2 * 2)))
+            kc = torch.empty(nb_pool, nkv, BS, 128, device=dev, dtype=torch.bfloat16)
+            vc = torch.empty(nb_pool, nkv, 128, BS, device=dev, dtype=torch.bfloat16)
+            sel = torch.randperm(nb_pool)[:nb_needed]
+            kc[sel.to(dev)] = torch.randn(nb_needed, nkv, BS, 128, device=dev).bfloat16()
+            vc[sel.to(dev)] = torch.randn(nb_needed, nkv, 128, BS, device=dev).bfloat16()
+            meta, _ = make_meta([ctxv] * B, [1] * B, nq, nkv, BS, dev, True, 512)
+            meta.block_tables = sel.view(B, -1).int().to(dev)
+            q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+            out = torch.empty(B, nq * 128, device=dev).bfloat16()
+            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out))
+            res[f"decode B{B} ctx{ctxv} pool{pool_gb}GB"] = f"{us:.1f}us {B * ctxv * nkv * 512 / us / 1e6:.2f} TB/s"
+            del kc, vc
+            torch.cuda.empty_cache()
         for T, ctxv in [(512, 3000), (2048, 2048), (64, 3000)]:
             S = max(1, 4096 // T)
             ctx = [ctxv] * S

@@ -287,6 +287,196 @@ __global__ void __launch_bounds__(256) attn_prefill_kernel(AttnArgs a) {
   }
 }
 
+
+// ------------------------------------------------------- prefill (paged, BS 64)
+// The extend/prefill hot path.  Workgroup = 4 waves x 32 rows = 128 (token,
+// q-head) rows of one sequence sharing kv head `kvh` (128/G tokens); one
+// 64-key page per iteration, K and V pages staged ONCE per workgroup through
+// LDS (register-staged double buffer: the next page's global loads are in
+// flight while the current page is computed; one barrier per page).
+//
+// v_mfma_f32_32x32x16_bf16, swapped QK^T (S^T = K . Q^T): lane (r = l&31,
+// hi = l>>5) owns query row r, so the running max / sum / O rescale are
+// lane-local (+1 xor-32 shuffle for the max).  Key permutation: MFMA row rho
+// of 32-key half kt holds key 32kt + 16*(reg>>3) + 8*hi + (reg&7) with
+// reg = (rho&3) + 4*(rho>>3), hi = (rho>>2)&1; S registers 8s..8s+7 of lane
+// half h are then keys 16s+8h..+7, exactly the B operand (P^T) of the PV
+// MFMA O^T += V^T . P^T for k-step s -> bf16 pack only, no permlane.
+// LDS images: K row = 256 B, 16-B chunk c at c ^ (key & 15); V^T row (one
+// head dim) = 128 B, chunk c at c ^ ((d >> 1) & 7): every ds_read_b128 lane
+// group (4 x 16 lanes) and every ds_write_b128 group (8 lanes) is
+// conflict-free for these access patterns.
+constexpr int PF_WAVES = 4;
+constexpr int PF_ROWS = 32 * PF_WAVES;        // rows per workgroup
+constexpr int PF_PAGE = 64;                   // keys per page (== BS)
+constexpr int PF_KBYTES = PF_PAGE * D * 2;    // 16 KB
+constexpr int PF_VBYTES = D * PF_PAGE * 2;    // 16 KB
+
+__device__ __forceinline__ int pf_key(int reg, int hi) { return 16 * (reg >> 3) + 8 * hi + (reg & 7); }
+
+__global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[2][PF_KBYTES + PF_VBYTES];
+  const int kvh = blockIdx.x % a.nkv, tile = blockIdx.x / a.nkv;  // kv head -> XCD (nkv == 8)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hi = lane >> 5;
+  const int seq = a.tile_seq[tile];
+  const int tok0 = a.tile_tok0[tile];
+  const int tlen = a.tile_len[tile];
+  const int qs = a.q_start[seq];
+  const int qlen = a.q_start[seq + 1] - qs;
+  const int ctx = a.ctx_lens[seq];
+  const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
+  const int base_pos = ctx - qlen + (tok0 - qs);   // position of the tile's first token
+
+  const int grow = w * 32 + r;
+  const int tt = grow / a.G, g = grow % a.G;
+  const bool valid = tt < tlen;
+  const int limit = valid ? base_pos + tt + 1 : 0;  // keys < limit visible to this row
+  // wave-uniform key range: rows of wave w are tokens [32w/G, (32w+31)/G]
+  const int wt0 = (w * 32) / a.G, wt1 = min(tlen - 1, (w * 32 + 31) / a.G);
+  const bool wave_live = wt0 < tlen;
+  const int wave_lo = base_pos + wt0 + 1;            // every live row sees keys < wave_lo
+  const int wave_hi = wave_live ? base_pos + wt1 + 1 : 0;
+  const int kv_end = base_pos + tlen;                // workgroup key range
+  const int n_pages = (kv_end + PF_PAGE - 1) / PF_PAGE;
+
+  // Q fragments (B operand of S^T): Q[row][16s + 8hi .. +8]
+  bf16x8 qf[8];
+  {
+    const uint16_t* qp = a.q + (size_t)(tok0 + (valid ? tt : 0)) * a.q_stride + (kvh * a.G + g) * D + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = valid ? load16(qp + 16 * s) : zero8();
+  }
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // cooperative page staging: 1024 + 1024 16-byte chunks, 4 + 4 per thread
+  bf16x8 stg[8];
+  auto load_page = [&](int p) {
+    const size_t page = (size_t)bt[p] * a.nkv + kvh;
+    const uint16_t* kp = a.kc + page * (size_t)(PF_PAGE * D);
+    const uint16_t* vp = a.vc + page * (size_t)(D * PF_PAGE);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stg[i] = load16(kp + (size_t)(tid + 256 * i) * 8);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) stg[4 + i] = load16(vp + (size_t)(tid + 256 * i) * 8);
+  };
+  auto store_page = [&](int b) {
+    unsigned char* kl = lds[b];
+    unsigned char* vl = lds[b] + PF_KBYTES;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, row = q >> 4, c = q & 15;
+      *reinterpret_cast<bf16x8*>(kl + row * 256 + ((c ^ (row & 15)) << 4)) = stg[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int q = tid + 256 * i, d = q >> 3, c = q & 7;
+      *reinterpret_cast<bf16x8*>(vl + d * 128 + ((c ^ ((d >> 1) & 7)) << 4)) = stg[4 + i];
+    }
+  };
+
+  // this lane's K row per half (A operand row rho = r)
+  const int kreg = (r & 3) + 4 * (r >> 3), khi = (r >> 2) & 1;
+  const int krow0 = pf_key(kreg, khi);               // key within a 32-key half
+
+  if (n_pages > 0) {
+    load_page(0);
+    store_page(0);
+  }
+  __syncthreads();
+  for (int p = 0; p < n_pages; ++p) {
+    const int b = p & 1;
+    if (p + 1 < n_pages) load_page(p + 1);
+    const int k0 = p * PF_PAGE;
+    if (wave_live && k0 < wave_hi) {
+      const unsigned char* kl = lds[b];
+      const unsigned char* vl = lds[b] + PF_KBYTES;
+      f32x16 sc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = 32 * kt + krow0;
+        const unsigned char* kr = kl + key * 256;
+        f32x16 acc;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) acc[i] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s + hi) ^ (key & 15)) << 4));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
+        }
+        sc[kt] = acc;
+      }
+      // scores -> log2 domain, causal mask only on pages that cross a row limit
+      const bool need_mask = k0 + PF_PAGE > wave_lo;
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+          float v = sc[kt][i] * a.scale_log2;
+          if (need_mask && k0 + 32 * kt + pf_key(i, hi) >= limit) v = -INFINITY;
+          sc[kt][i] = v;
+          cmax = fmaxf(cmax, v);
+        }
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mnew = fmaxf(m, cmax);
+      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
+      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+      bf16x8 pf[2][2];
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = exp2f(sc[kt][8 * s + j] - msub);
+            psum += e;
+            pf[kt][s][j] = (__bf16)e;
+          }
+      l = l * alpha + psum;
+      m = mnew;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+        const int d = 32 * dt + r;
+        const unsigned char* vr = vl + d * 128;
+        const int sw = (d >> 1) & 7;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
+          }
+      }
+    }
+    if (p + 1 < n_pages) store_page(b ^ 1);
+    __syncthreads();
+  }
+
+  if (!valid) return;
+  l += __shfl_xor(l, 32, 64);
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  // O^T: lane owns query row r; register i of d-tile dt is d = 32dt + (i&3) + 8(i>>2) + 4hi
+  uint16_t* dst = a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      u16x4 v;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * q4 + i] * inv);
+      *reinterpret_cast<u16x4*>(dst + 32 * dt + 8 * q4 + 4 * hi) = v;
+    }
+}
+
 }  // namespace k8s
 
 using namespace k8s;
@@ -345,6 +535,10 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
   a.tile_seq = tile_seq;
   a.tile_tok0 = tile_tok0;
   a.tile_len = tile_len;
-  if (n_tiles > 0) hipLaunchKernelGGL(attn_prefill_kernel, dim3(n_tiles, nkv), dim3(256), 0, stream, a);
+  if (n_tiles <= 0) return (int)hipSuccess;
+  if (BS == PF_PAGE && PF_ROWS % a.G == 0)
+    hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL(attn_prefill_kernel, dim3(n_tiles, nkv), dim3(256), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -448,7 +448,8 @@ class LLMEngine:
         if chunks:
             bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
             maxb_p = bt_p.shape[1]
-            ts, t0, tl = A.build_prefill_tiles(qs_p.tolist(), self.model.nq // self.model.nkv)
+            ts, t0, tl = A.build_prefill_tiles(qs_p.tolist(), self.model.nq // self.model.nkv, self.kv.block_size,
+                                               ctx_p.tolist())
             n_tiles = len(ts)
             arrays += [bt_p, ctx_p, qs_p, np.asarray(ts, np.int32), np.asarray(t0, np.int32),
                        np.asarray(tl, np.int32)]

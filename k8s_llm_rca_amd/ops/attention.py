@@ -112,16 +112,27 @@ def plan_decode_split(max_ctx: int, num_seqs: int, nkv: int, target_wgs: int = 1
     return n_parts, part
 
 
-def build_prefill_tiles(q_start_host: list, G: int) -> tuple:
-    per = max(1, 64 // G)
-    seq, tok0, ln = [], [], []
+def prefill_tile_tokens(G: int, block_size: int) -> int:
+    """Tokens per prefill tile: the paged-64 kernel covers 128 (token, q-head)
+    rows per workgroup, the generic one 64."""
+    return max(1, (128 if block_size == 64 and 128 % G == 0 else 64) // G)
+
+
+def build_prefill_tiles(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host: Optional[list] = None) -> tuple:
+    """Split every prefill chunk into query tiles.  With ``ctx_lens_host`` the
+    tiles are ordered longest-key-range first (causal tiles near the end of a
+    long context carry the most work; dispatching them first shortens the tail)."""
+    per = prefill_tile_tokens(G, block_size)
+    tiles = []
     for s in range(len(q_start_host) - 1):
         a, b = q_start_host[s], q_start_host[s + 1]
+        base = (ctx_lens_host[s] - (b - a)) if ctx_lens_host is not None else 0
         for t in range(a, b, per):
-            seq.append(s)
-            tok0.append(t)
-            ln.append(min(per, b - t))
-    return seq, tok0, ln
+            n = min(per, b - t)
+            tiles.append((base + (t - a) + n, s, t, n))
+    if ctx_lens_host is not None:
+        tiles.sort(key=lambda x: -x[0])
+    return [x[1] for x in tiles], [x[2] for x in tiles], [x[3] for x in tiles]
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta, nq: int,

@@ -91,7 +91,7 @@ def _meta(ctx, qlen, nq, nkv, BS, nblocks_total, device, decode):
         meta.part_o = torch.empty(S * nq * n_parts * 128, dtype=torch.float32, device=device)
         meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)
     else:
-        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv)
+        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv, BS, list(ctx))
         meta.tile_seq = torch.tensor(ts, dtype=torch.int32, device=device)
         meta.tile_tok0 = torch.tensor(t0, dtype=torch.int32, device=device)
         meta.tile_len = torch.tensor(tl, dtype=torch.int32, device=device)
@@ -122,13 +122,13 @@ def test_paged_decode(nq, nkv, ctx):
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1)])
+@pytest.mark.parametrize("BS", [64, 32])  # 64: paged-64 32x32x16 kernel; 32: generic kernel
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
 @pytest.mark.parametrize("ctx,qlen", [([7], [7]), ([300, 40], [300, 13]), ([1500, 90, 33], [64, 90, 1]),
-                                      ([2049], [129])])
-def test_paged_prefill(nq, nkv, ctx, qlen):
+                                      ([2049], [129]), ([130, 64, 3000], [66, 64, 700])])
+def test_paged_prefill(nq, nkv, ctx, qlen, BS):
     _need_gpu()
     torch.manual_seed(2)
-    BS = 64
     NB = sum((c + BS - 1) // BS for c in ctx) + 4
     kc, vc = _setup_cache(nkv, BS, NB, dev)
     meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
@@ -152,6 +152,24 @@ def test_attention_spike_rescale():
     q = torch.randn(1, (nq + 2 * nkv) * 128, device=dev).bfloat16()
     blk = meta.block_tables[0, 650 // BS].item()
     kc[blk, 0, 650 % BS] = (q[0, :128] * 4).bfloat16()
+    out = A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128))
+    ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, 1 / math.sqrt(128))
+    torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+def test_prefill_spike_rescale():
+    """Prefill rows whose max jumps on a late page (online rescale across pages)."""
+    _need_gpu()
+    nq, nkv, BS = 32, 8, 64
+    ctx, qlen = [900], [200]
+    NB = 20
+    kc, vc = _setup_cache(nkv, BS, NB, dev)
+    kc.mul_(0.1)
+    meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
+    q = torch.randn(200, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+    for key in (650, 770):
+        blk = meta.block_tables[0, key // BS].item()
+        kc[blk, 1, key % BS] = (q[150, 4 * 128:5 * 128] * 4).bfloat16()
     out = A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128))
     ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, 1 / math.sqrt(128))
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)

@@ -46,7 +46,7 @@ def test_forward_gpu_matches_cpu(name):
     import k8s_llm_rca_amd.ops.attention as A
     md = inp.meta_decode
     md.n_parts, md.part_size = 1, 256
-    ts, t0, tl = A.build_prefill_tiles(inp.meta_prefill.q_start_host, cfg.n_heads // cfg.n_kv_heads)
+    ts, t0, tl = A.build_prefill_tiles(inp.meta_prefill.q_start_host, cfg.n_heads // cfg.n_kv_heads, BS)
     inp.meta_prefill.tile_seq = torch.tensor(ts, dtype=torch.int32).cuda()
     inp.meta_prefill.tile_tok0 = torch.tensor(t0, dtype=torch.int32).cuda()
     inp.meta_prefill.tile_len = torch.tensor(tl, dtype=torch.int32).cuda()

@@ -51,7 +51,7 @@ def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
         meta.part_o = torch.empty(S * nq * meta.n_parts * 128, dtype=torch.float32, device=dev)
         meta.part_ml = torch.empty(S * nq * meta.n_parts * 2, dtype=torch.float32, device=dev)
     else:
-        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv)
+        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv, BS, list(ctx))
         meta.tile_seq = torch.tensor(ts, dtype=torch.int32, device=dev)
         meta.tile_tok0 = torch.tensor(t0, dtype=torch.int32, device=dev)
         meta.tile_len = torch.tensor(tl, dtype=torch.int32, device=dev)

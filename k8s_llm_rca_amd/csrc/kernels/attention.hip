@@ -55,6 +55,16 @@ struct AttnArgs {
   const int* tile_seq;    // [n_tiles]
   const int* tile_tok0;   // [n_tiles] q row of the tile's first token
   const int* tile_len;    // [n_tiles] tokens in the tile
+  // prefill split-KV (paged-64 kernel): page range + partial slot per tile
+  const int* tile_kv0;    // [n_tiles] first page
+  const int* tile_kv1;    // [n_tiles] end page (exclusive, clamped to the causal end)
+  const int* tile_slot;   // [n_tiles] -1: write the final rows; else partial slot
+  float* pf_o;            // [slots][nkv][128 rows][128] unnormalised partial O
+  float* pf_ml;           // [slots][nkv][128 rows][2]   (max, sum) in log2 domain
+  const int* m_tok0;      // merge list: q row of the split tile's first token
+  const int* m_len;       //   tokens
+  const int* m_slot0;     //   first slot; its parts are slot0 .. slot0+np-1
+  const int* m_np;
 };
 
 struct RowState {
@@ -338,7 +348,9 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
   const int wave_lo = base_pos + wt0 + 1;            // every live row sees keys < wave_lo
   const int wave_hi = wave_live ? base_pos + wt1 + 1 : 0;
   const int kv_end = base_pos + tlen;                // workgroup key range
-  const int n_pages = (kv_end + PF_PAGE - 1) / PF_PAGE;
+  const int p_begin = a.tile_kv0[tile];
+  const int n_pages = min(a.tile_kv1[tile], (kv_end + PF_PAGE - 1) / PF_PAGE);
+  const int slot = a.tile_slot[tile];
 
   // Q fragments (B operand of S^T): Q[row][16s + 8hi .. +8]
   bf16x8 qf[8];
@@ -356,8 +368,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
 
   // cooperative page staging: 1024 + 1024 16-byte chunks, 4 + 4 per thread
   bf16x8 stg[8];
-  auto load_page = [&](int p) {
-    const size_t page = (size_t)bt[p] * a.nkv + kvh;
+  auto load_page = [&](int blk) {
+    const size_t page = (size_t)blk * a.nkv + kvh;
     const uint16_t* kp = a.kc + page * (size_t)(PF_PAGE * D);
     const uint16_t* vp = a.vc + page * (size_t)(D * PF_PAGE);
 #pragma unroll
@@ -384,14 +396,25 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
   const int kreg = (r & 3) + 4 * (r >> 3), khi = (r >> 2) & 1;
   const int krow0 = pf_key(kreg, khi);               // key within a 32-key half
 
-  if (n_pages > 0) {
-    load_page(0);
+  // Q must be resident before the loop: otherwise the waitcnt pass cannot
+  // order the Q loads against the in-loop page loads and waits vmcnt(0) at the
+  // first QK^T MFMA, serialising the prefetch with compute.
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
+  int blk_next = 0;
+  if (p_begin < n_pages) {
+    load_page(bt[p_begin]);
+    blk_next = bt[min(p_begin + 1, n_pages - 1)];
     store_page(0);
   }
   __syncthreads();
-  for (int p = 0; p < n_pages; ++p) {
-    const int b = p & 1;
-    if (p + 1 < n_pages) load_page(p + 1);
+  for (int p = p_begin; p < n_pages; ++p) {
+    const int b = (p - p_begin) & 1;
+    // block id two pages ahead: its latency hides under this page's compute
+    const int blk_after = bt[min(p + 2, n_pages - 1)];
+    // unconditional (the last iteration re-reads a valid page): a conditional
+    // load would again leave the outstanding-load count ambiguous
+    load_page(blk_next);
     const int k0 = p * PF_PAGE;
     if (wave_live && k0 < wave_hi) {
       const unsigned char* kl = lds[b];
@@ -411,22 +434,29 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
         }
         sc[kt] = acc;
       }
-      // scores -> log2 domain, causal mask only on pages that cross a row limit
-      const bool need_mask = k0 + PF_PAGE > wave_lo;
+      // causal mask only on pages that cross a row limit (raw scores; scale > 0
+      // so the max commutes with it)
+      if (k0 + PF_PAGE > wave_lo) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i)
+            if (k0 + 32 * kt + pf_key(i, hi) >= limit) sc[kt][i] = -INFINITY;
+      }
       float cmax = -INFINITY;
 #pragma unroll
       for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-        for (int i = 0; i < 16; ++i) {
-          float v = sc[kt][i] * a.scale_log2;
-          if (need_mask && k0 + 32 * kt + pf_key(i, hi) >= limit) v = -INFINITY;
-          sc[kt][i] = v;
-          cmax = fmaxf(cmax, v);
-        }
+        for (int i = 0; i < 16; ++i) cmax = fmaxf(cmax, sc[kt][i]);
       cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-      const float mnew = fmaxf(m, cmax);
-      const float alpha = (mnew == -INFINITY) ? 1.f : exp2f(m - mnew);
-      const float msub = (mnew == -INFINITY) ? 0.f : mnew;
+      // deferred max (T13): move the reference only when the row max grows by
+      // more than 2^8, so P <= 256 (exact in bf16 / fp32 sums) and most pages
+      // skip the O rescale entirely.
+      const float mcand = cmax * a.scale_log2;
+      const bool upd = mcand > m + 8.f;
+      const float mnew = upd ? mcand : m;
+      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
+      const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
       bf16x8 pf[2][2];
       float psum = 0.f;
 #pragma unroll
@@ -435,16 +465,20 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
         for (int s = 0; s < 2; ++s)
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            const float e = exp2f(sc[kt][8 * s + j] - msub);
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
             psum += e;
             pf[kt][s][j] = (__bf16)e;
           }
       l = l * alpha + psum;
       m = mnew;
+      if (__ballot(upd)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
+      }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
-#pragma unroll
-        for (int i = 0; i < 16; ++i) o[dt][i] *= alpha;
         const int d = 32 * dt + r;
         const unsigned char* vr = vl + d * 128;
         const int sw = (d >> 1) & 7;
@@ -457,12 +491,28 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
           }
       }
     }
-    if (p + 1 < n_pages) store_page(b ^ 1);
+    store_page(b ^ 1);
+    blk_next = blk_after;
     __syncthreads();
   }
 
   if (!valid) return;
   l += __shfl_xor(l, 32, 64);
+  if (slot >= 0) {  // split tile: unnormalised partial, merged by attn_prefill_merge
+    const size_t rbase = ((size_t)slot * a.nkv + kvh) * PF_ROWS + grow;
+    float* po = a.pf_o + rbase * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * q4 + 4 * hi) =
+            f32x4{o[dt][4 * q4], o[dt][4 * q4 + 1], o[dt][4 * q4 + 2], o[dt][4 * q4 + 3]};
+    if (hi == 0) {
+      a.pf_ml[rbase * 2] = m;
+      a.pf_ml[rbase * 2 + 1] = l;
+    }
+    return;
+  }
   const float inv = l > 0.f ? 1.f / l : 0.f;
   // O^T: lane owns query row r; register i of d-tile dt is d = 32dt + (i&3) + 8(i>>2) + 4hi
   uint16_t* dst = a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D;
@@ -475,6 +525,35 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
       for (int i = 0; i < 4; ++i) v[i] = f2bf(o[dt][4 * q4 + i] * inv);
       *reinterpret_cast<u16x4*>(dst + 32 * dt + 8 * q4 + 4 * hi) = v;
     }
+}
+
+// grid: (n_merge * nkv, PF_ROWS / 4); block 256: ONE WAVE PER ROW (a wave
+// walking many rows serialises np dependent loads per row).  Single online
+// pass: O = sum_p o_p 2^(m_p - M) / sum_p l_p 2^(m_p - M), 2 dims per lane.
+__global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
+  const int kvh = blockIdx.x % a.nkv, mi = blockIdx.x / a.nkv;
+  const int lane = threadIdx.x & 63, row = blockIdx.y * 4 + (threadIdx.x >> 6);
+  const int rows = a.m_len[mi] * a.G;
+  if (row >= rows) return;
+  const int tok0 = a.m_tok0[mi], slot0 = a.m_slot0[mi], np = a.m_np[mi];
+  float M = -INFINITY, L = 0.f, o0 = 0.f, o1 = 0.f;
+  for (int p = 0; p < np; ++p) {
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * PF_ROWS + row;
+    const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
+    const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
+    if (ml.x == -INFINITY) continue;  // this part saw no key of the row
+    const float Mn = fmaxf(M, ml.x);
+    const float fo = __builtin_amdgcn_exp2f(M - Mn), fp = __builtin_amdgcn_exp2f(ml.x - Mn);
+    L = L * fo + ml.y * fp;
+    o0 = o0 * fo + v.x * fp;
+    o1 = o1 * fo + v.y * fp;
+    M = Mn;
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int tt = row / a.G, g = row % a.G;
+  uint16_t* dst = a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D + 2 * lane;
+  dst[0] = f2bf(o0 * inv);
+  dst[1] = f2bf(o1 * inv);
 }
 
 }  // namespace k8s
@@ -513,8 +592,10 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
 
 K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                              int bt_stride, const int* ctx_lens, const int* q_start, const int* tile_seq,
-                             const int* tile_tok0, const int* tile_len, int n_tiles, int nq, int nkv, int BS,
-                             float scale, void* out, int out_stride, hipStream_t stream) {
+                             const int* tile_tok0, const int* tile_len, const int* tile_kv0, const int* tile_kv1,
+                             const int* tile_slot, int n_tiles, const int* m_tok0, const int* m_len,
+                             const int* m_slot0, const int* m_np, int n_merge, float* pf_o, float* pf_ml, int nq,
+                             int nkv, int BS, float scale, void* out, int out_stride, hipStream_t stream) {
   if (nq % nkv || (nq / nkv) > 16 || BS % 32) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const uint16_t*)q;
@@ -535,10 +616,23 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
   a.tile_seq = tile_seq;
   a.tile_tok0 = tile_tok0;
   a.tile_len = tile_len;
+  a.tile_kv0 = tile_kv0;
+  a.tile_kv1 = tile_kv1;
+  a.tile_slot = tile_slot;
+  a.m_tok0 = m_tok0;
+  a.m_len = m_len;
+  a.m_slot0 = m_slot0;
+  a.m_np = m_np;
+  a.pf_o = pf_o;
+  a.pf_ml = pf_ml;
   if (n_tiles <= 0) return (int)hipSuccess;
-  if (BS == PF_PAGE && PF_ROWS % a.G == 0)
+  if (BS == PF_PAGE && PF_ROWS % a.G == 0) {
+    if (n_merge > 0 && (!pf_o || !pf_ml)) return (int)hipErrorInvalidValue;
     hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
-  else
+    if (n_merge > 0) hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(n_merge * nkv, PF_ROWS / 4), dim3(256), 0, stream, a);
+  } else {
+    if (n_merge > 0) return (int)hipErrorInvalidValue;  // the generic kernel does not split
     hipLaunchKernelGGL(attn_prefill_kernel, dim3(n_tiles, nkv), dim3(256), 0, stream, a);
+  }
   return (int)hipGetLastError();
 }

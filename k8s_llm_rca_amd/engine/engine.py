@@ -152,6 +152,7 @@ class LLMEngine:
         self._graphs: Dict[tuple, tuple] = {}
         self._graph_pool = None
         self._static = None
+        self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
@@ -438,7 +439,7 @@ class LLMEngine:
         ids, pos, slots = self._token_arrays(rows)
         arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
         nd = len(decode)
-        maxb_d = maxb_p = n_tiles = 0
+        maxb_d = maxb_p = n_tiles = n_merge = 0
         n_parts = 1
         if decode:
             bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
@@ -448,21 +449,20 @@ class LLMEngine:
         if chunks:
             bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
             maxb_p = bt_p.shape[1]
-            ts, t0, tl = A.build_prefill_tiles(qs_p.tolist(), self.model.nq // self.model.nkv, self.kv.block_size,
-                                               ctx_p.tolist())
-            n_tiles = len(ts)
-            arrays += [bt_p, ctx_p, qs_p, np.asarray(ts, np.int32), np.asarray(t0, np.int32),
-                       np.asarray(tl, np.int32)]
+            plan = A.plan_prefill(qs_p.tolist(), self.model.nq // self.model.nkv, self.kv.block_size,
+                                  ctx_p.tolist(), nkv=self.model.nkv)
+            n_tiles, n_merge = plan.n_tiles, plan.n_merge
+            arrays += [bt_p, ctx_p, qs_p] + [np.asarray(x, np.int32) for x in plan.arrays()]
         flat = np.concatenate([x.reshape(-1).astype(np.int32, copy=False) for x in arrays])
         header = np.array([1, flat.size, len(ids), nd, nd, maxb_d, len(chunks), maxb_p, n_tiles,
-                           len(sample_idx), n_parts, 0], dtype=np.int64)
+                           len(sample_idx), n_parts, n_merge], dtype=np.int64)
         return header, flat
 
     def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor):
         """Build StepInputs from the wire format and run the forward (every TP rank)."""
         from ..models.llama import StepInputs
 
-        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, _ = [int(v) for v in header]
+        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge = [int(v) for v in header]
         o = 0
 
         def take(n, shape=None):
@@ -496,13 +496,19 @@ class LLMEngine:
             bt, _ = take(n_pre * maxb_p, (n_pre, maxb_p))
             ctx, ctx_h = take(n_pre)
             qs, qs_h = take(n_pre + 1)
-            tsd, _ = take(n_tiles)
-            t0d, _ = take(n_tiles)
-            tld, _ = take(n_tiles)
+            tiles = [take(n_tiles)[0] for _ in range(6)]
+            merges = [take(n_merge)[0] for _ in range(4)]
             pmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=n_pre, decode=False,
-                               tile_seq=tsd, tile_tok0=t0d, tile_len=tld, n_tiles=n_tiles,
+                               n_tiles=n_tiles, n_merge=n_merge,
                                ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
                                q_start_host=None if qs_h is None else qs_h.tolist())
+            (pmeta.tile_seq, pmeta.tile_tok0, pmeta.tile_len, pmeta.tile_kv0, pmeta.tile_kv1,
+             pmeta.tile_slot) = tiles
+            pmeta.m_tok0, pmeta.m_len, pmeta.m_slot0, pmeta.m_np = merges
+            if n_merge:
+                if self._pf_ws is None:
+                    self._pf_ws = A.prefill_workspace(self.model.nkv, self.device)
+                pmeta.pf_o, pmeta.pf_ml = self._pf_ws
         inp = StepInputs(d_ids, d_pos, d_slots, nd, dmeta, pmeta, d_sidx.long())
         return self.model.forward(inp, self.kv.k, self.kv.v)
 

@@ -9,7 +9,7 @@ from __future__ import annotations
 
 import math
 from dataclasses import dataclass
-from typing import Optional
+from typing import List, Optional
 
 import torch
 
@@ -93,6 +93,17 @@ class AttnMeta:
     tile_tok0: Optional[torch.Tensor] = None
     tile_len: Optional[torch.Tensor] = None
     n_tiles: int = 0
+    # prefill split-KV (paged-64 kernel): see :func:`plan_prefill`
+    tile_kv0: Optional[torch.Tensor] = None
+    tile_kv1: Optional[torch.Tensor] = None
+    tile_slot: Optional[torch.Tensor] = None
+    m_tok0: Optional[torch.Tensor] = None
+    m_len: Optional[torch.Tensor] = None
+    m_slot0: Optional[torch.Tensor] = None
+    m_np: Optional[torch.Tensor] = None
+    n_merge: int = 0
+    pf_o: Optional[torch.Tensor] = None
+    pf_ml: Optional[torch.Tensor] = None
     # decode split-KV
     n_parts: int = 1
     part_size: int = 512
@@ -101,6 +112,13 @@ class AttnMeta:
     # host copies for the reference path
     ctx_lens_host: Optional[list] = None
     q_start_host: Optional[list] = None
+
+    def m_slot0_end(self) -> int:
+        """Slots used by the merge list (workspace size when allocated lazily)."""
+        if not self.n_merge:
+            return 0
+        s0, npp = self.m_slot0.tolist(), self.m_np.tolist()
+        return max(a + b for a, b in zip(s0, npp))
 
 
 def plan_decode_split(max_ctx: int, num_seqs: int, nkv: int, target_wgs: int = 1024) -> tuple:
@@ -118,10 +136,60 @@ def prefill_tile_tokens(G: int, block_size: int) -> int:
     return max(1, (128 if block_size == 64 and 128 % G == 0 else 64) // G)
 
 
-def build_prefill_tiles(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host: Optional[list] = None) -> tuple:
-    """Split every prefill chunk into query tiles.  With ``ctx_lens_host`` the
-    tiles are ordered longest-key-range first (causal tiles near the end of a
-    long context carry the most work; dispatching them first shortens the tail)."""
+PF_ROWS = 128               # (token, q-head) rows per paged-64 prefill workgroup
+PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
+PF_TARGET_WGS = 512         # split long key ranges until a prefill launch has about this many workgroups
+_NO_END = 1 << 30
+
+
+@dataclass
+class PrefillPlan:
+    """Work list of one prefill/extend attention launch.
+
+    Item i covers query tokens ``tok0[i] .. tok0[i]+length[i]`` of sequence
+    ``seq[i]`` against key pages ``kv0[i] .. kv1[i]``; ``slot[i] == -1`` means
+    the item owns the whole key range and writes final rows, otherwise it
+    writes an fp32 partial into ``slot`` and the merge list combines the
+    ``np`` consecutive slots of each split tile (flash-decoding for extend).
+
+    Dispatch order = list order, and the kernel maps kv head -> XCD, so items
+    are grouped by sequence and key range: every query tile of a sequence
+    streams the same pages at about the same time and the pages are read
+    from HBM once per XCD instead of once per tile (the L2 is 4 MB per XCD; a
+    3k-token context is 1.5 MB per kv head)."""
+    seq: List[int]
+    tok0: List[int]
+    length: List[int]
+    kv0: List[int]
+    kv1: List[int]
+    slot: List[int]
+    m_tok0: List[int]
+    m_len: List[int]
+    m_slot0: List[int]
+    m_np: List[int]
+
+    @property
+    def n_tiles(self) -> int:
+        return len(self.seq)
+
+    @property
+    def n_merge(self) -> int:
+        return len(self.m_tok0)
+
+    def arrays(self) -> List[list]:
+        return [self.seq, self.tok0, self.length, self.kv0, self.kv1, self.slot,
+                self.m_tok0, self.m_len, self.m_slot0, self.m_np]
+
+
+def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host: Optional[list] = None,
+                 nkv: int = 8, max_slots: int = PF_MAX_SLOTS, target_wgs: Optional[int] = None) -> PrefillPlan:
+    """Tile every prefill chunk (``prefill_tile_tokens`` tokens per tile) and,
+    for the paged-64 kernel, split long key ranges so the launch has about
+    ``target_wgs`` workgroups: extend steps in an RCA batch are small (a few
+    hundred new tokens over ~3k cached ones), so without splitting a handful
+    of workgroups walk 50+ pages each while most CUs idle.  Items are ordered
+    most-pages first so the longest ones start first."""
+    target_wgs = target_wgs or PF_TARGET_WGS
     per = prefill_tile_tokens(G, block_size)
     tiles = []
     for s in range(len(q_start_host) - 1):
@@ -130,9 +198,64 @@ def build_prefill_tiles(q_start_host: list, G: int, block_size: int = 64, ctx_le
         for t in range(a, b, per):
             n = min(per, b - t)
             tiles.append((base + (t - a) + n, s, t, n))
-    if ctx_lens_host is not None:
-        tiles.sort(key=lambda x: -x[0])
-    return [x[1] for x in tiles], [x[2] for x in tiles], [x[3] for x in tiles]
+    plan = PrefillPlan(*[[] for _ in range(10)])
+    split = block_size == 64 and ctx_lens_host is not None and 128 % G == 0
+    # sequences with the most work first; inside a sequence, longest tile first
+    work = {}
+    for end, s, _, n in tiles:
+        work[s] = work.get(s, 0) + end * n
+    rank = {s: i for i, s in enumerate(sorted(work, key=lambda s: -work[s]))}
+    if not split:
+        if ctx_lens_host is not None:
+            tiles.sort(key=lambda x: (rank[x[1]], -x[0]))
+        for _, s, t, n in tiles:
+            for lst, v in zip(plan.arrays()[:6], (s, t, n, 0, _NO_END, -1)):
+                lst.append(v)
+        return plan
+    pages = [(end + 63) // 64 for end, _, _, _ in tiles]
+    total = sum(pages)
+    # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
+    part = max(pages) if pages and len(tiles) * nkv >= target_wgs // 2 else max(4, -(-total * nkv // target_wgs))
+    while sum(-(-p // part) for p in pages if p > part) > max_slots:
+        part *= 2
+    items = []
+    slot = 0
+    for (end, s, t, n), p in zip(tiles, pages):
+        k = -(-p // part)
+        if k == 1:
+            items.append((p, s, t, n, 0, p, -1))
+            continue
+        bounds = [(i * p) // k for i in range(k + 1)]
+        for i in range(k):
+            items.append((bounds[i + 1] - bounds[i], s, t, n, bounds[i], bounds[i + 1], slot + i))
+        plan.m_tok0.append(t)
+        plan.m_len.append(n)
+        plan.m_slot0.append(slot)
+        plan.m_np.append(k)
+        slot += k
+    items.sort(key=lambda x: (rank[x[1]], x[4], -x[0]))
+    for _, s, t, n, k0, k1, sl in items:
+        for lst, v in zip(plan.arrays()[:6], (s, t, n, k0, k1, sl)):
+            lst.append(v)
+    return plan
+
+
+def attach_plan(meta: "AttnMeta", plan: PrefillPlan, device, workspace: Optional[tuple] = None) -> "AttnMeta":
+    """Upload ``plan`` into ``meta`` (tests / tools; the engine ships the same
+    arrays inside its one-copy step buffer)."""
+    t = [torch.tensor(x if x else [0], dtype=torch.int32, device=device) for x in plan.arrays()]
+    (meta.tile_seq, meta.tile_tok0, meta.tile_len, meta.tile_kv0, meta.tile_kv1, meta.tile_slot,
+     meta.m_tok0, meta.m_len, meta.m_slot0, meta.m_np) = t
+    meta.n_tiles, meta.n_merge = plan.n_tiles, plan.n_merge
+    if workspace is not None:
+        meta.pf_o, meta.pf_ml = workspace
+    return meta
+
+
+def prefill_workspace(nkv: int, device, slots: int = PF_MAX_SLOTS, D: int = HEAD_DIM) -> tuple:
+    """fp32 partial-O / (max, sum) buffers for ``slots`` split-tile parts."""
+    return (torch.empty(slots * nkv * PF_ROWS * D, dtype=torch.float32, device=device),
+            torch.empty(slots * nkv * PF_ROWS * 2, dtype=torch.float32, device=device))
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta, nq: int,
@@ -155,10 +278,15 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
                                     ptr(meta.part_o), ptr(meta.part_ml), meta.n_parts, meta.part_size,
                                     stream_ptr(q)), "attn_decode")
         else:
+            if meta.n_merge and meta.pf_o is None:
+                meta.pf_o, meta.pf_ml = prefill_workspace(nkv, q.device, max(meta.m_slot0_end(), 1))
             check(L.k8s_attn_prefill(ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(meta.block_tables),
                                      meta.block_tables.stride(0), ptr(meta.ctx_lens), ptr(meta.q_start),
-                                     ptr(meta.tile_seq), ptr(meta.tile_tok0), ptr(meta.tile_len), meta.n_tiles,
-                                     nq, nkv, BS, float(scale), ptr(out), out.stride(0), stream_ptr(q)),
+                                     ptr(meta.tile_seq), ptr(meta.tile_tok0), ptr(meta.tile_len),
+                                     ptr(meta.tile_kv0), ptr(meta.tile_kv1), ptr(meta.tile_slot), meta.n_tiles,
+                                     ptr(meta.m_tok0), ptr(meta.m_len), ptr(meta.m_slot0), ptr(meta.m_np),
+                                     meta.n_merge, ptr(meta.pf_o), ptr(meta.pf_ml), nq, nkv, BS, float(scale),
+                                     ptr(out), out.stride(0), stream_ptr(q)),
                   "attn_prefill")
         return out
     return _attention_ref(q, k_cache, v_cache, meta, nq, nkv, scale, out)

@@ -91,11 +91,7 @@ def _meta(ctx, qlen, nq, nkv, BS, nblocks_total, device, decode):
         meta.part_o = torch.empty(S * nq * n_parts * 128, dtype=torch.float32, device=device)
         meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)
     else:
-        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv, BS, list(ctx))
-        meta.tile_seq = torch.tensor(ts, dtype=torch.int32, device=device)
-        meta.tile_tok0 = torch.tensor(t0, dtype=torch.int32, device=device)
-        meta.tile_len = torch.tensor(tl, dtype=torch.int32, device=device)
-        meta.n_tiles = len(ts)
+        A.attach_plan(meta, A.plan_prefill(qs, nq // nkv, BS, list(ctx), nkv=nkv), device)
     return meta
 
 

@@ -46,11 +46,9 @@ def test_forward_gpu_matches_cpu(name):
     import k8s_llm_rca_amd.ops.attention as A
     md = inp.meta_decode
     md.n_parts, md.part_size = 1, 256
-    ts, t0, tl = A.build_prefill_tiles(inp.meta_prefill.q_start_host, cfg.n_heads // cfg.n_kv_heads, BS)
-    inp.meta_prefill.tile_seq = torch.tensor(ts, dtype=torch.int32).cuda()
-    inp.meta_prefill.tile_tok0 = torch.tensor(t0, dtype=torch.int32).cuda()
-    inp.meta_prefill.tile_len = torch.tensor(tl, dtype=torch.int32).cuda()
-    inp.meta_prefill.n_tiles = len(ts)
+    mp_ = inp.meta_prefill
+    A.attach_plan(mp_, A.plan_prefill(mp_.q_start_host, cfg.n_heads // cfg.n_kv_heads, BS, mp_.ctx_lens_host,
+                                      nkv=cfg.n_kv_heads), "cuda")
     inp.input_ids, inp.positions, inp.slots, inp.logits_idx = (inp.input_ids.cuda(), inp.positions.cuda(),
                                                                inp.slots.cuda(), inp.logits_idx.cuda())
     out = gm.forward(inp, kf.cuda().bfloat16(), vf.cuda().bfloat16())[:, : cfg.vocab_size].float().cpu()

@@ -51,11 +51,7 @@ def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
         meta.part_o = torch.empty(S * nq * meta.n_parts * 128, dtype=torch.float32, device=dev)
         meta.part_ml = torch.empty(S * nq * meta.n_parts * 2, dtype=torch.float32, device=dev)
     else:
-        ts, t0, tl = A.build_prefill_tiles(qs, nq // nkv, BS, list(ctx))
-        meta.tile_seq = torch.tensor(ts, dtype=torch.int32, device=dev)
-        meta.tile_tok0 = torch.tensor(t0, dtype=torch.int32, device=dev)
-        meta.tile_len = torch.tensor(tl, dtype=torch.int32, device=dev)
-        meta.n_tiles = len(ts)
+        A.attach_plan(meta, A.plan_prefill(qs, nq // nkv, BS, list(ctx), nkv=nkv), dev)
     return meta, sum(nbs)
 
 
@@ -96,8 +92,11 @@ def main():
             res[f"decode B{B} ctx{ctxv} pool{pool_gb}GB"] = f"{us:.1f}us {B * ctxv * nkv * 512 / us / 1e6:.2f} TB/s"
             del kc, vc
             torch.cuda.empty_cache()
-        for T, ctxv in [(512, 3000), (2048, 2048), (64, 3000)]:
-            S = max(1, 4096 // T)
+        cases = [(512, 3000, 8, 512), (2048, 2048, 2, 512), (64, 3000, 64, 512)]
+        cases += [(T, c, S, tw) for (T, c, S) in [(4, 3000, 16), (300, 3000, 2), (600, 3500, 1), (48, 3000, 4)]
+                  for tw in (512, 1024, 2048)]
+        for T, ctxv, S, tw in cases:
+            A.PF_TARGET_WGS = tw
             ctx = [ctxv] * S
             meta, nb = make_meta(ctx, [T] * S, nq, nkv, BS, dev, False)
             kc = torch.randn(nb, nkv, BS, 128, device=dev).bfloat16()
@@ -108,7 +107,10 @@ def main():
             # causal-ish flops: each query attends to (ctx - T + i) keys
             pairs = S * sum(ctxv - T + i + 1 for i in range(T))
             fl = pairs * nq * 128 * 4
-            res[f"prefill S{S} q{T} ctx{ctxv}"] = f"{us:.1f}us {fl / us / 1e6:.1f} TFLOP/s"
+            kvb = S * ctxv * nkv * 128 * 2 * 2
+            res[f"prefill S{S} q{T} ctx{ctxv} tw{tw} merge{meta.n_merge}"] = \
+                f"{us:.1f}us {fl / us / 1e6:.1f} TFLOP/s {kvb / us / 1e6:.2f} TB/s-kv"
+        A.PF_TARGET_WGS = 512
     if args.what in ("all", "gemm"):
         for M in (1, 16, 64, 128):
             for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:

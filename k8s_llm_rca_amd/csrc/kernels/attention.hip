@@ -172,13 +172,128 @@ __device__ __forceinline__ void init_state(RowState& st, const AttnArgs& a, int 
 }
 
 // ---------------------------------------------------------------- decode
-// grid: (n_parts / 4, nkv, S); block 256.  Each WAVE owns one key partition of
-// `part_size` keys (a multiple of the page size): no LDS, no barriers; it
-// writes an unnormalised partial (O, m, l) merged by attn_reduce, or the final
-// bf16 row when n_parts == 1.
-__global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int part = blockIdx.x * 4 + w, kvh = blockIdx.y, seq = blockIdx.z;
+// Software-pipelined 64-key stream for paged caches with BS % 64 == 0 (every
+// 64-key chunk inside one page).  K registers are refilled with chunk c+1
+// right after chunk c's QK^T and V registers right after its PV, so a wave
+// always has the next chunk's 16-32 KB in flight while it computes (a plain
+// load -> wait -> compute loop leaves the wave's memory pipe idle during
+// compute and decode is bound by bytes in flight per CU).
+__device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs& a, const int* bt, int kvh, int kb,
+                                           int lane) {
+  const int r = lane & 15, h = lane >> 4;
+  const size_t page = (size_t)bt[kb / a.BS] * a.nkv + kvh;
+  const uint16_t* kp = a.kc + page * (size_t)a.BS * D;
+  const int off = kb % a.BS;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const int key = off + 32 * u + 8 * (r >> 2) + 4 * t + (r & 3);
+#pragma unroll
+      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16(kp + (size_t)key * D + 32 * c + 8 * h);
+    }
+}
+
+__device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a, const int* bt, int kvh, int kb,
+                                           int lane) {
+  const int r = lane & 15, h = lane >> 4;
+  const size_t page = (size_t)bt[kb / a.BS] * a.nkv + kvh;
+  const uint16_t* vp = a.vc + page * (size_t)D * a.BS;
+  const int off = kb % a.BS;
+#pragma unroll
+  for (int u = 0; u < 2; ++u)
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt) vf[u][dt] = load16(vp + (size_t)(16 * dt + r) * a.BS + off + 32 * u + 8 * h);
+}
+
+__device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a, const int* bt, int kvh, int k0,
+                                                int k1, int lane) {
+  const int h = lane >> 4;
+  const int nch = (k1 - k0 + 63) >> 6;
+  bf16x8 kf[2][2][4], vf[2][8];
+  dec_load_k(kf, a, bt, kvh, k0, lane);
+  dec_load_v(vf, a, bt, kvh, k0, lane);
+  for (int c = 0; c < nch; ++c) {
+    const int kb = k0 + 64 * c;
+    const int kbn = k0 + 64 * min(c + 1, nch - 1);  // unconditional prefetch (last one re-reads)
+    f32x4 sc[2][2];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) {
+        f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][t][q], st.qf[q], acc, 0, 0, 0);
+        sc[u][t] = acc;
+      }
+    dec_load_k(kf, a, bt, kvh, kbn, lane);
+    float cmax = -INFINITY;
+    if (kb + 64 > k1) {  // tail chunk: keys >= k1 are not part of this partition
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            if (kb + 32 * u + 8 * h + 4 * t + i >= k1) sc[u][t][i] = -INFINITY;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cmax = fmaxf(cmax, sc[u][t][i]);
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 16, 64));
+    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+    // deferred max (see the prefill kernel): P <= 2^8
+    const float mcand = cmax * a.scale_log2;
+    const bool upd = mcand > st.m + 8.f;
+    const float mnew = upd ? mcand : st.m;
+    const float alpha = upd ? __builtin_amdgcn_exp2f(st.m - mnew) : 1.f;
+    const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
+    bf16x8 pf[2];
+    float psum = 0.f;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const float e = __builtin_amdgcn_exp2f(fmaf(sc[u][t][i], a.scale_log2, nmsub));
+          psum += e;
+          pf[u][4 * t + i] = (__bf16)e;
+        }
+    st.l = st.l * alpha + psum;
+    st.m = mnew;
+    if (__ballot(upd)) {
+      float ar[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) ar[i] = __shfl(alpha, 4 * h + i, 64);
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) st.o[dt][i] *= ar[i];
+    }
+#pragma unroll
+    for (int dt = 0; dt < 8; ++dt)
+#pragma unroll
+      for (int u = 0; u < 2; ++u) st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[u], vf[u][dt], st.o[dt], 0, 0, 0);
+    dec_load_v(vf, a, bt, kvh, kbn, lane);
+  }
+}
+
+// grid: S * nkv * n_parts one-wave workgroups.  Each wave owns one
+// (seq, kv head, key partition of `part_size` keys) item of a FLAT item list:
+// decode is bound by per-CU load throughput, so waves (not 4-wave groups with
+// idle members) are what the dispatcher must spread evenly over the CUs.  No LDS, no barriers; a wave writes an
+// unnormalised partial (O, m, l) merged by attn_reduce, or the final bf16 row
+// when n_parts == 1.
+template <bool STREAM64>
+__global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
+  const int lane = threadIdx.x & 63;
+  const int item = blockIdx.x;
+  const int part = item % a.n_parts, kvh = (item / a.n_parts) % a.nkv, seq = item / (a.n_parts * a.nkv);
+  if (seq >= S) return;
   const int r = lane & 15, h = lane >> 4;
   const int ctx = a.ctx_lens[seq];
   const int k0 = part * a.part_size;
@@ -191,9 +306,13 @@ __global__ void __launch_bounds__(256) attn_decode_kernel(AttnArgs a) {
 
   RowState st;
   init_state(st, a, qrow, head, valid, lane);
-  int kb = k0;
-  for (; kb + 64 <= k1 && ((kb % a.BS) + 64 <= a.BS); kb += 64) chunk<2>(st, a, bt, kvh, kb, k1, lane);
-  for (; kb < k1; kb += 32) chunk<1>(st, a, bt, kvh, kb, k1, lane);
+  if constexpr (STREAM64) {
+    decode_stream64(st, a, bt, kvh, k0, k1, lane);
+  } else {
+    int kb = k0;
+    for (; kb + 64 <= k1 && ((kb % a.BS) + 64 <= a.BS); kb += 64) chunk<2>(st, a, bt, kvh, kb, k1, lane);
+    for (; kb < k1; kb += 32) chunk<1>(st, a, bt, kvh, kb, k1, lane);
+  }
 
   float l = st.l + __shfl_xor(st.l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -585,7 +704,11 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   a.part_ml = part_ml;
   a.n_parts = n_parts;
   a.part_size = part_size;
-  hipLaunchKernelGGL(attn_decode_kernel, dim3((n_parts + 3) / 4, nkv, S), dim3(256), 0, stream, a);
+  const long items = (long)S * nkv * n_parts;
+  if (BS % 64 == 0)
+    hipLaunchKernelGGL(attn_decode_kernel<true>, dim3((unsigned)items), dim3(64), 0, stream, a, S);
+  else
+    hipLaunchKernelGGL(attn_decode_kernel<false>, dim3((unsigned)items), dim3(64), 0, stream, a, S);
   if (n_parts > 1) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
   return (int)hipGetLastError();
 }

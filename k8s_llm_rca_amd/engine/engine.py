@@ -43,7 +43,7 @@ from .tokenizer import get_tokenizer
 
 log = logging.getLogger(__name__)
 
-PART_SIZE = 512
+PART_MIN = min(A.DECODE_PARTS)  # smallest decode partition: sizes the split-KV buffers
 
 
 @dataclass
@@ -156,7 +156,7 @@ class LLMEngine:
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
-                      "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0}
+                      "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0}
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -432,7 +432,7 @@ class LLMEngine:
 
     # Step wire format (also the TP broadcast): header int64[12] + one int32 payload
     # = ids[T] pos[T] slots[T] sidx[ns] | bt_d ctx_d qs_d | bt_p ctx_p qs_p tseq ttok0 tlen
-    HDR = 12
+    HDR = 13
 
     def _pack_step(self, decode, chunks, sample_idx):
         rows = [(s, 1) for s in decode] + list(chunks)
@@ -440,11 +440,11 @@ class LLMEngine:
         arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
         nd = len(decode)
         maxb_d = maxb_p = n_tiles = n_merge = 0
-        n_parts = 1
+        n_parts, part = 1, PART_MIN
         if decode:
             bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
             maxb_d = bt_d.shape[1]
-            n_parts = self._n_parts(int(ctx_d.max()))
+            n_parts, part = A.plan_decode_split(ctx_d, self.model.nkv)
             arrays += [bt_d, ctx_d, qs_d]
         if chunks:
             bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
@@ -455,14 +455,14 @@ class LLMEngine:
             arrays += [bt_p, ctx_p, qs_p] + [np.asarray(x, np.int32) for x in plan.arrays()]
         flat = np.concatenate([x.reshape(-1).astype(np.int32, copy=False) for x in arrays])
         header = np.array([1, flat.size, len(ids), nd, nd, maxb_d, len(chunks), maxb_p, n_tiles,
-                           len(sample_idx), n_parts, n_merge], dtype=np.int64)
+                           len(sample_idx), n_parts, n_merge, part], dtype=np.int64)
         return header, flat
 
     def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor):
         """Build StepInputs from the wire format and run the forward (every TP rank)."""
         from ..models.llama import StepInputs
 
-        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge = [int(v) for v in header]
+        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge, part = [int(v) for v in header]
         o = 0
 
         def take(n, shape=None):
@@ -484,7 +484,7 @@ class LLMEngine:
             ctx, ctx_h = take(n_dec)
             qs, qs_h = take(n_dec + 1)
             dmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=n_dec, decode=True,
-                               n_parts=n_parts, part_size=PART_SIZE,
+                               n_parts=n_parts, part_size=part,
                                ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
                                q_start_host=None if qs_h is None else qs_h.tolist())
             if n_parts > 1:
@@ -551,7 +551,8 @@ class LLMEngine:
 
     @staticmethod
     def _n_parts(max_ctx: int) -> int:
-        n = max(1, (max_ctx + PART_SIZE - 1) // PART_SIZE)
+        """Partition count bound at the smallest partition size (buffer sizing)."""
+        n = max(1, (max_ctx + PART_MIN - 1) // PART_MIN)
         return 1 << (n - 1).bit_length()
 
     # ---------------------------------------------------------- HIP graphs
@@ -583,21 +584,22 @@ class LLMEngine:
         self._static = st
         return st
 
-    def _graph_inputs(self, B: int, n_parts: int):
+    def _graph_inputs(self, B: int, n_parts: int, part: int):
         from ..models.llama import StepInputs
 
         st = self._static
         meta = A.AttnMeta(block_tables=st["bt"][:B], ctx_lens=st["ctx"][:B], q_start=st["qs"][:B + 1], num_seqs=B,
-                          decode=True, n_parts=n_parts, part_size=PART_SIZE, part_o=st["part_o"],
+                          decode=True, n_parts=n_parts, part_size=part, part_o=st["part_o"],
                           part_ml=st["part_ml"])
         return StepInputs(st["ids"][:B], st["pos"][:B], st["slots"][:B], B, meta, None, st["sidx"][:B])
 
-    def _capture(self, B: int, n_parts: int):
-        key = (B, n_parts)
+    def _capture(self, B: int, n_parts: int, part: int):
+        key = (B, n_parts, part)
         g = self._graphs.get(key)
         if g is not None:
             return g
-        inp = self._graph_inputs(B, n_parts)
+        t0 = time.perf_counter()
+        inp = self._graph_inputs(B, n_parts, part)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -610,6 +612,8 @@ class LLMEngine:
         with torch.cuda.graph(graph, pool=self._graph_pool):
             out = self.model.forward(inp, self.kv.k, self.kv.v)
         self._graphs[key] = (graph, out)
+        self.stats["captures"] += 1
+        self.stats["capture_s"] += time.perf_counter() - t0
         return self._graphs[key]
 
     def _forward_graph(self, decode: List[Sequence]):
@@ -632,7 +636,8 @@ class LLMEngine:
             slots[i] = s.blocks[p // BS] * BS + p % BS
             ctx[i] = p + 1
             bt[i, : len(s.blocks)] = s.blocks
-        n_parts = self._n_parts(int(ctx.max()))
+        # padded rows (ctx 1) cost one near-empty wave each: plan on the real rows
+        n_parts, part = A.plan_decode_split(ctx[:B], self.model.nkv)
         host = st["host"]
         hv = host.numpy()
         o = 0
@@ -648,7 +653,7 @@ class LLMEngine:
         st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
         st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
         st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
-        graph, out = self._capture(Bb, n_parts)
+        graph, out = self._capture(Bb, n_parts, part)
         graph.replay()
         return out[:B]
 

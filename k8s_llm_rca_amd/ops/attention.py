@@ -121,13 +121,33 @@ class AttnMeta:
         return max(a + b for a, b in zip(s0, npp))
 
 
-def plan_decode_split(max_ctx: int, num_seqs: int, nkv: int, target_wgs: int = 1024) -> tuple:
-    """Pick a key-partition size (multiple of 64) so the grid fills the chip."""
-    part = 512
-    while part > 64 and num_seqs * nkv * max(1, (max_ctx + part - 1) // part) < target_wgs:
-        part //= 2
-    n_parts = max(1, (max_ctx + part - 1) // part)
-    return n_parts, part
+DECODE_PARTS = (256, 512, 1024, 1536)   # candidate keys per decode wave
+DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (239 VGPRs)
+
+
+def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=DECODE_PARTS) -> tuple:
+    """Keys per decode wave for one step -> (n_parts rounded up to a power of
+    two, part_size).
+
+    Decode attention is bound by per-CU load throughput, so the step costs
+    about (waves / resident slots, rounded up) x (keys per wave): measured on
+    MI355X, B64 x ctx3400 runs 5.6 TB/s at 1024 keys/wave (2048 waves = one
+    round) but B72 drops to 4.8 TB/s (2304 waves = 1.1 rounds) where 512
+    keys/wave (4608 waves, 2.25 rounds) does 5.1.  Ties go to the larger
+    partition (fewer partial rows to merge)."""
+    import numpy as np
+    c = np.asarray(ctx_lens, dtype=np.int64)
+    mx = int(c.max()) if c.size else 1
+    best = None
+    for P in candidates:
+        waves = nkv * int(((c + P - 1) // P).sum())
+        rounds = -(-waves // slots)
+        cost = (rounds * min(P, mx), -P)
+        if best is None or cost < best[0]:
+            best = (cost, P)
+    P = best[1]
+    n = max(1, -(-mx // P))
+    return 1 << (n - 1).bit_length(), P
 
 
 def prefill_tile_tokens(G: int, block_size: int) -> int:

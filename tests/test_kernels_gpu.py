@@ -86,7 +86,7 @@ def _meta(ctx, qlen, nq, nkv, BS, nblocks_total, device, decode):
                       q_start=torch.tensor(qs, dtype=torch.int32, device=device), num_seqs=S, decode=decode,
                       ctx_lens_host=list(ctx), q_start_host=qs)
     if decode:
-        n_parts, part = A.plan_decode_split(max(ctx), S, nkv)
+        n_parts, part = A.plan_decode_split(ctx, nkv)
         meta.n_parts, meta.part_size = n_parts, part
         meta.part_o = torch.empty(S * nq * n_parts * 128, dtype=torch.float32, device=device)
         meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)

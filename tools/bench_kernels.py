@@ -111,6 +111,20 @@ def main():
             res[f"prefill S{S} q{T} ctx{ctxv} tw{tw} merge{meta.n_merge}"] = \
                 f"{us:.1f}us {fl / us / 1e6:.1f} TFLOP/s {kvb / us / 1e6:.2f} TB/s-kv"
         A.PF_TARGET_WGS = 512
+    if args.what == "decode_sweep":
+        for B in (32, 48, 56, 64, 72, 96, 128):
+            for ctxv in (1000, 3400):
+                for part in (512, 1024):
+                    ctx = [ctxv] * B
+                    meta, nb = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True, part_size=part)
+                    kc = torch.randn(nb, nkv, BS, 128, device=dev).bfloat16()
+                    vc = torch.randn(nb, nkv, 128, BS, device=dev).bfloat16()
+                    q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+                    out = torch.empty(B, nq * 128, device=dev).bfloat16()
+                    us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out))
+                    waves = B * nkv * meta.n_parts
+                    res[f"decode B{B} ctx{ctxv} part{part} waves{waves}"] = \
+                        f"{us:.1f}us {B * ctxv * nkv * 512 / us / 1e6:.2f} TB/s"
     if args.what in ("all", "gemm"):
         for M in (1, 16, 64, 128):
             for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:

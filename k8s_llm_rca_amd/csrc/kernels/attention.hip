@@ -65,6 +65,10 @@ struct AttnArgs {
   const int* m_len;       //   tokens
   const int* m_slot0;     //   first slot; its parts are slot0 .. slot0+np-1
   const int* m_np;
+  // decode work list (persistent kernel): int4 (seq, part | -1 = whole row, k1, qrow)
+  const int4* items;
+  int n_items;
+  const int* d_n_items;   // device count (HIP graphs: the grid stays fixed), or null
 };
 
 struct RowState {
@@ -178,10 +182,10 @@ __device__ __forceinline__ void init_state(RowState& st, const AttnArgs& a, int 
 // always has the next chunk's 16-32 KB in flight while it computes (a plain
 // load -> wait -> compute loop leaves the wave's memory pipe idle during
 // compute and decode is bound by bytes in flight per CU).
-__device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs& a, const int* bt, int kvh, int kb,
+__device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs& a, int blk, int kvh, int kb,
                                            int lane) {
   const int r = lane & 15, h = lane >> 4;
-  const size_t page = (size_t)bt[kb / a.BS] * a.nkv + kvh;
+  const size_t page = (size_t)blk * a.nkv + kvh;
   const uint16_t* kp = a.kc + page * (size_t)a.BS * D;
   const int off = kb % a.BS;
 #pragma unroll
@@ -194,10 +198,10 @@ __device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs
     }
 }
 
-__device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a, const int* bt, int kvh, int kb,
+__device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a, int blk, int kvh, int kb,
                                            int lane) {
   const int r = lane & 15, h = lane >> 4;
-  const size_t page = (size_t)bt[kb / a.BS] * a.nkv + kvh;
+  const size_t page = (size_t)blk * a.nkv + kvh;
   const uint16_t* vp = a.vc + page * (size_t)D * a.BS;
   const int off = kb % a.BS;
 #pragma unroll
@@ -206,16 +210,24 @@ __device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a
     for (int dt = 0; dt < 8; ++dt) vf[u][dt] = load16(vp + (size_t)(16 * dt + r) * a.BS + off + 32 * u + 8 * h);
 }
 
-__device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a, const int* bt, int kvh, int k0,
+// `blkv`: lane j holds the block id of the partition's j-th page (fetched
+// once per work item: a per-chunk block-table load would put a dependent
+// memory latency in front of every chunk's K/V loads).
+__device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a, int blkv, int kvh, int k0,
                                                 int k1, int lane) {
   const int h = lane >> 4;
   const int nch = (k1 - k0 + 63) >> 6;
+  const int pg0 = k0 / a.BS;
   bf16x8 kf[2][2][4], vf[2][8];
-  dec_load_k(kf, a, bt, kvh, k0, lane);
-  dec_load_v(vf, a, bt, kvh, k0, lane);
+  {
+    const int b0 = __builtin_amdgcn_readfirstlane(blkv);
+    dec_load_k(kf, a, b0, kvh, k0, lane);
+    dec_load_v(vf, a, b0, kvh, k0, lane);
+  }
   for (int c = 0; c < nch; ++c) {
     const int kb = k0 + 64 * c;
     const int kbn = k0 + 64 * min(c + 1, nch - 1);  // unconditional prefetch (last one re-reads)
+    const int bn = __builtin_amdgcn_readlane(blkv, kbn / a.BS - pg0);
     f32x4 sc[2][2];
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -226,7 +238,7 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
         for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][t][q], st.qf[q], acc, 0, 0, 0);
         sc[u][t] = acc;
       }
-    dec_load_k(kf, a, bt, kvh, kbn, lane);
+    dec_load_k(kf, a, bn, kvh, kbn, lane);
     float cmax = -INFINITY;
     if (kb + 64 > k1) {  // tail chunk: keys >= k1 are not part of this partition
 #pragma unroll
@@ -278,7 +290,7 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
     for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[u], vf[u][dt], st.o[dt], 0, 0, 0);
-    dec_load_v(vf, a, bt, kvh, kbn, lane);
+    dec_load_v(vf, a, bn, kvh, kbn, lane);
   }
 }
 
@@ -288,7 +300,6 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
 // idle members) are what the dispatcher must spread evenly over the CUs.  No LDS, no barriers; a wave writes an
 // unnormalised partial (O, m, l) merged by attn_reduce, or the final bf16 row
 // when n_parts == 1.
-template <bool STREAM64>
 __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
   const int lane = threadIdx.x & 63;
   const int item = blockIdx.x;
@@ -306,9 +317,7 @@ __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
 
   RowState st;
   init_state(st, a, qrow, head, valid, lane);
-  if constexpr (STREAM64) {
-    decode_stream64(st, a, bt, kvh, k0, k1, lane);
-  } else {
+  {
     int kb = k0;
     for (; kb + 64 <= k1 && ((kb % a.BS) + 64 <= a.BS); kb += 64) chunk<2>(st, a, bt, kvh, kb, k1, lane);
     for (; kb < k1; kb += 32) chunk<1>(st, a, bt, kvh, kb, k1, lane);
@@ -346,11 +355,76 @@ __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
   }
 }
 
+// Persistent decode over a host-built work list (BS % 64 == 0): grid = at
+// most the resident-wave count (2048 one-wave workgroups: 256 CUs x 4 SIMDs x
+// 2); wave g takes work units g, g + grid, ... where unit = item * nkv + kv
+// head.  Items come longest-first, so the round-robin assignment is close to
+// LPT scheduling, and no wave is ever launched for an empty partition (a
+// (seq, parts) grid with the partition count of the longest sequence spent
+// most of its waves on nothing when context lengths vary 1k..6k).
+__device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnArgs& a, int seq, int part, int qrow,
+                                                int kvh, bool whole, int lane) {
+  const int r = lane & 15, h = lane >> 4;
+  float l = st.l + __shfl_xor(st.l, 16, 64);
+  l += __shfl_xor(l, 32, 64);
+  float mr[4], lr[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    mr[i] = __shfl(st.m, 4 * h + i, 64);
+    lr[i] = __shfl(l, 4 * h + i, 64);
+  }
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = 4 * h + i;
+    if (row >= a.G) continue;
+    const int qh = kvh * a.G + row;
+    if (whole) {
+      const float inv = lr[i] > 0.f ? 1.f / lr[i] : 0.f;
+      uint16_t* dst = a.out + (size_t)qrow * a.out_stride + qh * D;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) dst[16 * dt + r] = f2bf(st.o[dt][i] * inv);
+    } else {
+      const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts + part;
+      float* po = a.part_o + base * D;
+#pragma unroll
+      for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
+      if (r == 0) {
+        a.part_ml[base * 2 + 0] = mr[i];
+        a.part_ml[base * 2 + 1] = lr[i];
+      }
+    }
+  }
+}
+
+__global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
+  const int lane = threadIdx.x;
+  const int r = lane & 15;
+  const int n_items = a.d_n_items ? __builtin_amdgcn_readfirstlane(*a.d_n_items) : a.n_items;
+  const int total = n_items * a.nkv;
+  const bool valid = r < a.G;
+  for (int w = blockIdx.x; w < total; w += gridDim.x) {
+    const int it = w / a.nkv, kvh = w - it * a.nkv;
+    const int4 item = a.items[it];
+    const int seq = item.x, k1 = item.z, qrow = item.w;
+    const bool whole = item.y < 0;
+    const int part = whole ? 0 : item.y;
+    const int k0 = part * a.part_size;
+    const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
+    const int pg0 = k0 / a.BS, npg = (k1 - 1) / a.BS - pg0 + 1;
+    const int blkv = lane < npg ? bt[pg0 + lane] : 0;
+    RowState st;
+    init_state(st, a, qrow, kvh * a.G + (valid ? r : 0), valid, lane);
+    decode_stream64(st, a, blkv, kvh, k0, k1, lane);
+    decode_epilogue(st, a, seq, part, qrow, kvh, whole, lane);
+  }
+}
+
 // grid: (nq, S); block 128 (one thread per output column)
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   const int qh = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
   const int ctx = a.ctx_lens[seq];
   const int np = min(a.n_parts, (ctx + a.part_size - 1) / a.part_size);
+  if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
   float M = -INFINITY;
   for (int p = 0; p < np; ++p) M = fmaxf(M, a.part_ml[(base + p) * 2]);
@@ -682,7 +756,8 @@ using namespace k8s;
 K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                             int bt_stride, const int* ctx_lens, const int* q_start, int S, int nq, int nkv, int BS,
                             float scale, void* out, int out_stride, float* part_o, float* part_ml, int n_parts,
-                            int part_size, hipStream_t stream) {
+                            int part_size, const int* items, int n_items, const int* d_n_items, int grid_waves,
+                            hipStream_t stream) {
   if (nq % nkv || (nq / nkv) > 16 || BS % 32 || part_size % 32) return (int)hipErrorInvalidValue;
   AttnArgs a{};
   a.q = (const uint16_t*)q;
@@ -704,11 +779,16 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   a.part_ml = part_ml;
   a.n_parts = n_parts;
   a.part_size = part_size;
-  const long items = (long)S * nkv * n_parts;
-  if (BS % 64 == 0)
-    hipLaunchKernelGGL(attn_decode_kernel<true>, dim3((unsigned)items), dim3(64), 0, stream, a, S);
-  else
-    hipLaunchKernelGGL(attn_decode_kernel<false>, dim3((unsigned)items), dim3(64), 0, stream, a, S);
+  if (items) {  // work-list path (BS % 64 == 0, part_size % 64 == 0, <= 64 pages per item)
+    if (BS % 64 || part_size % 64 || part_size / BS > 64 || grid_waves <= 0) return (int)hipErrorInvalidValue;
+    a.items = reinterpret_cast<const int4*>(items);
+    a.n_items = n_items;
+    a.d_n_items = d_n_items;
+    hipLaunchKernelGGL(attn_decode_items_kernel, dim3(grid_waves), dim3(64), 0, stream, a);
+  } else {
+    const long nw = (long)S * nkv * n_parts;
+    hipLaunchKernelGGL(attn_decode_kernel, dim3((unsigned)nw), dim3(64), 0, stream, a, S);
+  }
   if (n_parts > 1) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
   return (int)hipGetLastError();
 }

@@ -22,8 +22,10 @@ explicitly (:meth:`step`); :meth:`submit` is thread-safe.
 """
 from __future__ import annotations
 
+import json
 import logging
 import math
+import os
 import threading
 import time
 from dataclasses import dataclass, field
@@ -153,6 +155,9 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
+        # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
+        # lines (replayed by tools/bench_kernels.py --what replay)
+        self._shape_trace = os.environ.get("K8S_RCA_SHAPE_TRACE")
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
@@ -353,6 +358,10 @@ class LLMEngine:
         if not decode and not chunks:
             raise MemoryError("KV pool exhausted with no evictable sequence")
         rows = [(s, 1) for s in decode] + chunks
+        if self._shape_trace:
+            with open(self._shape_trace, "a") as f:
+                f.write(json.dumps({"d": [s.n_cached + 1 for s in decode],
+                                    "p": [[s.n_cached + q, q] for s, q in chunks]}) + "\n")
         sample_rows = []  # (row index in batch, seq)
         off = 0
         for s, q in rows:
@@ -402,7 +411,8 @@ class LLMEngine:
 
     def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int]):
         t0 = time.perf_counter()
-        if not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1:
+        if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1
+                and self.kv.block_size % 64 == 0):
             out = self._forward_graph(decode)
             self.stats["graph_steps"] += 1
             self.stats["decode_steps"] += 1
@@ -432,20 +442,26 @@ class LLMEngine:
 
     # Step wire format (also the TP broadcast): header int64[12] + one int32 payload
     # = ids[T] pos[T] slots[T] sidx[ns] | bt_d ctx_d qs_d | bt_p ctx_p qs_p tseq ttok0 tlen
-    HDR = 13
+    HDR = 14
 
     def _pack_step(self, decode, chunks, sample_idx):
         rows = [(s, 1) for s in decode] + list(chunks)
         ids, pos, slots = self._token_arrays(rows)
         arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
         nd = len(decode)
-        maxb_d = maxb_p = n_tiles = n_merge = 0
+        maxb_d = maxb_p = n_tiles = n_merge = n_items = 0
         n_parts, part = 1, PART_MIN
         if decode:
             bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
             maxb_d = bt_d.shape[1]
             n_parts, part = A.plan_decode_split(ctx_d, self.model.nkv)
             arrays += [bt_d, ctx_d, qs_d]
+            if self.kv.block_size % 64 == 0:
+                items = A.build_decode_items(ctx_d, np.arange(nd), part)
+                n_items = items.shape[0]
+                arrays.append(items)
+            else:
+                n_parts = 1 << (n_parts - 1).bit_length()
         if chunks:
             bt_p, ctx_p, qs_p = self._meta_arrays(chunks)
             maxb_p = bt_p.shape[1]
@@ -455,14 +471,15 @@ class LLMEngine:
             arrays += [bt_p, ctx_p, qs_p] + [np.asarray(x, np.int32) for x in plan.arrays()]
         flat = np.concatenate([x.reshape(-1).astype(np.int32, copy=False) for x in arrays])
         header = np.array([1, flat.size, len(ids), nd, nd, maxb_d, len(chunks), maxb_p, n_tiles,
-                           len(sample_idx), n_parts, n_merge, part], dtype=np.int64)
+                           len(sample_idx), n_parts, n_merge, part, n_items], dtype=np.int64)
         return header, flat
 
     def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor):
         """Build StepInputs from the wire format and run the forward (every TP rank)."""
         from ..models.llama import StepInputs
 
-        _, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge, part = [int(v) for v in header]
+        (_, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge, part,
+         n_items) = [int(v) for v in header]
         o = 0
 
         def take(n, shape=None):
@@ -483,8 +500,9 @@ class LLMEngine:
             bt, _ = take(n_dec * maxb_d, (n_dec, maxb_d))
             ctx, ctx_h = take(n_dec)
             qs, qs_h = take(n_dec + 1)
+            items = take(n_items * 4, (n_items, 4))[0] if n_items else None
             dmeta = A.AttnMeta(block_tables=bt, ctx_lens=ctx, q_start=qs, num_seqs=n_dec, decode=True,
-                               n_parts=n_parts, part_size=part,
+                               n_parts=n_parts, part_size=part, items=items, n_items=n_items,
                                ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
                                q_start_host=None if qs_h is None else qs_h.tolist())
             if n_parts > 1:
@@ -568,6 +586,7 @@ class LLMEngine:
         Bmax = max(self.cfg.graph_batch_sizes)
         mb = self.max_blocks_per_seq
         npmax = self._n_parts(self.max_context)
+        self._max_items = Bmax * npmax
         dev = self.device
         st = {
             "ids": torch.zeros(Bmax, dtype=torch.int32, device=dev),
@@ -579,27 +598,32 @@ class LLMEngine:
             "sidx": torch.arange(Bmax, dtype=torch.int64, device=dev),
             "part_o": torch.empty(Bmax * self.model.nq * npmax * self.model.D, dtype=torch.float32, device=dev),
             "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
-            "host": torch.zeros(Bmax * (3 + mb + 1), dtype=torch.int32).pin_memory(),
+            "items": torch.zeros(Bmax * npmax, 4, dtype=torch.int32, device=dev),
+            "n_items": torch.zeros(1, dtype=torch.int32, device=dev),
+            "host": torch.zeros(Bmax * (3 + mb + 1) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory(),
         }
         self._static = st
         return st
 
-    def _graph_inputs(self, B: int, n_parts: int, part: int):
+    def _graph_inputs(self, B: int, part: int):
         from ..models.llama import StepInputs
 
         st = self._static
+        # work-list decode: the grid is the resident-wave count and the item
+        # count is read on the device, so one graph serves every item list
         meta = A.AttnMeta(block_tables=st["bt"][:B], ctx_lens=st["ctx"][:B], q_start=st["qs"][:B + 1], num_seqs=B,
-                          decode=True, n_parts=n_parts, part_size=part, part_o=st["part_o"],
-                          part_ml=st["part_ml"])
+                          decode=True, n_parts=self._n_parts(self.max_context), part_size=part,
+                          part_o=st["part_o"], part_ml=st["part_ml"], items=st["items"], n_items=0,
+                          d_n_items=st["n_items"], grid_waves=A.DECODE_WAVE_SLOTS)
         return StepInputs(st["ids"][:B], st["pos"][:B], st["slots"][:B], B, meta, None, st["sidx"][:B])
 
-    def _capture(self, B: int, n_parts: int, part: int):
-        key = (B, n_parts, part)
+    def _capture(self, B: int, part: int):
+        key = (B, part)
         g = self._graphs.get(key)
         if g is not None:
             return g
         t0 = time.perf_counter()
-        inp = self._graph_inputs(B, n_parts, part)
+        inp = self._graph_inputs(B, part)
         s = torch.cuda.Stream(self.device)
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
@@ -636,8 +660,12 @@ class LLMEngine:
             slots[i] = s.blocks[p // BS] * BS + p % BS
             ctx[i] = p + 1
             bt[i, : len(s.blocks)] = s.blocks
-        # padded rows (ctx 1) cost one near-empty wave each: plan on the real rows
-        n_parts, part = A.plan_decode_split(ctx[:B], self.model.nkv)
+        # plan on the real rows; padded rows (ctx 1) still get a one-key item
+        # (sorted last) so every output row the graph produces is finite
+        _, part = A.plan_decode_split(ctx[:B], self.model.nkv)
+        items = A.build_decode_items(ctx, np.arange(Bb), part)
+        n_items = items.shape[0]
+        assert n_items <= self._max_items
         host = st["host"]
         hv = host.numpy()
         o = 0
@@ -645,15 +673,20 @@ class LLMEngine:
             hv[o:o + Bb] = arr
             o += Bb
         hv[o:o + Bb * mb] = bt.reshape(-1)
-        stream = torch.cuda.current_stream(self.device)
-        dev_flat = torch.empty(o + Bb * mb, dtype=torch.int32, device=self.device)
-        dev_flat.copy_(host[: o + Bb * mb], non_blocking=True)
+        o += Bb * mb
+        hv[o] = n_items
+        hv[o + 1:o + 1 + n_items * 4] = items.reshape(-1)
+        n = o + 1 + n_items * 4
+        dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
+        dev_flat.copy_(host[:n], non_blocking=True)
         st["ids"][:Bb].copy_(dev_flat[0:Bb])
         st["pos"][:Bb].copy_(dev_flat[Bb:2 * Bb])
         st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
         st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
         st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
-        graph, out = self._capture(Bb, n_parts, part)
+        st["n_items"].copy_(dev_flat[o:o + 1])
+        st["items"][:n_items].copy_(dev_flat[o + 1:n].view(n_items, 4))
+        graph, out = self._capture(Bb, part)
         graph.replay()
         return out[:B]
 

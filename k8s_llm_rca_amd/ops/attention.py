@@ -109,6 +109,11 @@ class AttnMeta:
     part_size: int = 512
     part_o: Optional[torch.Tensor] = None
     part_ml: Optional[torch.Tensor] = None
+    # decode work list (persistent kernel, BS % 64 == 0): see build_decode_items
+    items: Optional[torch.Tensor] = None      # [n_items, 4] int32
+    n_items: int = 0
+    d_n_items: Optional[torch.Tensor] = None  # [1] int32 device count (HIP graphs)
+    grid_waves: int = 0
     # host copies for the reference path
     ctx_lens_host: Optional[list] = None
     q_start_host: Optional[list] = None
@@ -121,33 +126,78 @@ class AttnMeta:
         return max(a + b for a, b in zip(s0, npp))
 
 
-DECODE_PARTS = (256, 512, 1024, 1536)   # candidate keys per decode wave
-DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (239 VGPRs)
+DECODE_PARTS = (512, 768, 1024)         # candidate keys per decode work item
+DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (<= 256 VGPRs)
+DECODE_ITEM_OVERHEAD = 256               # per-item start cost in key-equivalents (replay-calibrated)
 
 
 def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=DECODE_PARTS) -> tuple:
-    """Keys per decode wave for one step -> (n_parts rounded up to a power of
-    two, part_size).
+    """Keys per decode work item for one step -> (max items per sequence, part_size).
 
-    Decode attention is bound by per-CU load throughput, so the step costs
-    about (waves / resident slots, rounded up) x (keys per wave): measured on
-    MI355X, B64 x ctx3400 runs 5.6 TB/s at 1024 keys/wave (2048 waves = one
-    round) but B72 drops to 4.8 TB/s (2304 waves = 1.1 rounds) where 512
-    keys/wave (4608 waves, 2.25 rounds) does 5.1.  Ties go to the larger
-    partition (fewer partial rows to merge)."""
+    The persistent decode kernel runs ``slots`` waves over a longest-first
+    work list, so a step costs about (total keys + per-item start overhead)
+    / slots + one item (the LPT tail): smaller items balance better until the
+    start latency and the partial rows to merge dominate.  Measured on
+    recorded RCA decode steps (``tools/bench_kernels.py --what replay``)."""
     import numpy as np
     c = np.asarray(ctx_lens, dtype=np.int64)
     mx = int(c.max()) if c.size else 1
+    total = nkv * int(c.sum())
     best = None
     for P in candidates:
-        waves = nkv * int(((c + P - 1) // P).sum())
-        rounds = -(-waves // slots)
-        cost = (rounds * min(P, mx), -P)
-        if best is None or cost < best[0]:
+        items = nkv * int(((c + P - 1) // P).sum())
+        cost = (total + items * DECODE_ITEM_OVERHEAD) / slots + min(P, mx)
+        if best is None or cost < best[0] - 1e-9:
             best = (cost, P)
     P = best[1]
-    n = max(1, -(-mx // P))
-    return 1 << (n - 1).bit_length(), P
+    return max(1, -(-mx // P)), P
+
+
+def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size: int, device,
+                       q_rows=None, part: Optional[int] = None) -> "AttnMeta":
+    """Plan + upload the decode split for ``meta`` (tests / tools; the engine
+    ships the same arrays in its step buffer).  Paged-64 caches use the
+    persistent work-list kernel; other page sizes the (seq, part) grid."""
+    import numpy as np
+    ctx_host = [int(c) for c in ctx_host]
+    S = len(ctx_host)
+    if block_size % 64 == 0:
+        n_parts, P = plan_decode_split(ctx_host, nkv)
+        if part is not None:
+            P = part
+            n_parts = max(1, -(-max(ctx_host) // P))
+        items = build_decode_items(ctx_host, q_rows if q_rows is not None else np.arange(S), P)
+        meta.items = torch.from_numpy(items).to(device)
+        meta.n_items = items.shape[0]
+    else:
+        P = part or 512
+        n = max(1, -(-max(ctx_host) // P))
+        n_parts = 1 << (n - 1).bit_length()
+    meta.n_parts, meta.part_size = n_parts, P
+    if n_parts > 1:
+        meta.part_o = torch.empty(S * nq * n_parts * HEAD_DIM, dtype=torch.float32, device=device)
+        meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)
+    return meta
+
+
+def build_decode_items(ctx_lens, q_rows, part: int):
+    """Work list [n_items, 4] int32 = (seq, part | -1 for a one-item row, end
+    key, q row), longest first."""
+    import numpy as np
+    c = np.asarray(ctx_lens, dtype=np.int64)
+    n = (c + part - 1) // part
+    seq = np.repeat(np.arange(c.size), n)
+    first = np.repeat(np.cumsum(n) - n, n)
+    pidx = np.arange(seq.size) - first
+    k0 = pidx * part
+    k1 = np.minimum(c[seq], k0 + part)
+    out = np.empty((seq.size, 4), dtype=np.int32)
+    out[:, 0] = seq
+    out[:, 1] = np.where(n[seq] == 1, -1, pidx)
+    out[:, 2] = k1
+    out[:, 3] = np.asarray(q_rows, dtype=np.int64)[seq]
+    order = np.argsort(-(k1 - k0), kind="stable")
+    return out[order]
 
 
 def prefill_tile_tokens(G: int, block_size: int) -> int:
@@ -292,10 +342,12 @@ def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tenso
         L = lib()
         if meta.decode:
             assert T == meta.num_seqs
+            grid = meta.grid_waves or min(DECODE_WAVE_SLOTS, meta.n_items * nkv)
             check(L.k8s_attn_decode(ptr(q), q.stride(0), ptr(k_cache), ptr(v_cache), ptr(meta.block_tables),
                                     meta.block_tables.stride(0), ptr(meta.ctx_lens), ptr(meta.q_start),
                                     meta.num_seqs, nq, nkv, BS, float(scale), ptr(out), out.stride(0),
                                     ptr(meta.part_o), ptr(meta.part_ml), meta.n_parts, meta.part_size,
+                                    ptr(meta.items), meta.n_items, ptr(meta.d_n_items), grid,
                                     stream_ptr(q)), "attn_decode")
         else:
             if meta.n_merge and meta.pf_o is None:

@@ -86,10 +86,7 @@ def _meta(ctx, qlen, nq, nkv, BS, nblocks_total, device, decode):
                       q_start=torch.tensor(qs, dtype=torch.int32, device=device), num_seqs=S, decode=decode,
                       ctx_lens_host=list(ctx), q_start_host=qs)
     if decode:
-        n_parts, part = A.plan_decode_split(ctx, nkv)
-        meta.n_parts, meta.part_size = n_parts, part
-        meta.part_o = torch.empty(S * nq * n_parts * 128, dtype=torch.float32, device=device)
-        meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)
+        A.attach_decode_plan(meta, ctx, nq, nkv, BS, device)
     else:
         A.attach_plan(meta, A.plan_prefill(qs, nq // nkv, BS, list(ctx), nkv=nkv), device)
     return meta
@@ -102,12 +99,12 @@ def _cpu_meta(meta):
     return m
 
 
+@pytest.mark.parametrize("BS", [64, 32])  # 64: persistent work-list kernel; 32: (seq, part) grid kernel
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 8)])
-@pytest.mark.parametrize("ctx", [[1], [17, 64, 65], [1000, 3, 2500, 128], [5000]])
-def test_paged_decode(nq, nkv, ctx):
+@pytest.mark.parametrize("ctx", [[1], [17, 64, 65], [1000, 3, 2500, 128], [5000], [130] * 300])
+def test_paged_decode(nq, nkv, ctx, BS):
     _need_gpu()
     torch.manual_seed(1)
-    BS = 64
     NB = sum((c + BS - 1) // BS for c in ctx) + 4
     kc, vc = _setup_cache(nkv, BS, NB, dev)
     meta = _meta(ctx, [1] * len(ctx), nq, nkv, BS, NB, dev, decode=True)

@@ -29,7 +29,7 @@ def timeit(fn, iters=50, warm=5):
     return e0.elapsed_time(e1) / iters * 1e3  # us
 
 
-def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
+def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=None):
     S = len(ctx)
     nbs = [(c + BS - 1) // BS for c in ctx]
     maxb = max(nbs)
@@ -45,11 +45,7 @@ def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
     meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
                       q_start=torch.tensor(qs, dtype=torch.int32, device=dev), num_seqs=S, decode=decode)
     if decode:
-        n = max(1, (max(ctx) + part_size - 1) // part_size)
-        meta.n_parts = 1 << (n - 1).bit_length()
-        meta.part_size = part_size
-        meta.part_o = torch.empty(S * nq * meta.n_parts * 128, dtype=torch.float32, device=dev)
-        meta.part_ml = torch.empty(S * nq * meta.n_parts * 2, dtype=torch.float32, device=dev)
+        A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev, part=part_size)
     else:
         A.attach_plan(meta, A.plan_prefill(qs, nq // nkv, BS, list(ctx), nkv=nkv), dev)
     return meta, sum(nbs)
@@ -58,6 +54,8 @@ def make_meta(ctx, qlen, nq, nkv, BS, dev, decode, part_size=256):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--what", default="all")
+    ap.add_argument("--trace", default="profiles/r1_shape_trace_128.jsonl")
+    ap.add_argument("--samples", type=int, default=80)
     args = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -111,6 +109,55 @@ def main():
             res[f"prefill S{S} q{T} ctx{ctxv} tw{tw} merge{meta.n_merge}"] = \
                 f"{us:.1f}us {fl / us / 1e6:.1f} TFLOP/s {kvb / us / 1e6:.2f} TB/s-kv"
         A.PF_TARGET_WGS = 512
+    if args.what == "replay":
+        # replay the attention shapes of a recorded run (K8S_RCA_SHAPE_TRACE)
+        steps = [json.loads(l) for l in open(args.trace)]
+        rng = torch.Generator().manual_seed(0)
+        dec = [s["d"] for s in steps if s["d"]]
+        pre = [s["p"] for s in steps if s["p"]]
+        idx = torch.randperm(len(dec), generator=rng)[: args.samples].tolist()
+        tot_us = tot_bytes = 0.0
+        variants = {"fixed512": 512, "fixed768": 768, "fixed1024": 1024}
+
+        buckets = [(1, 16), (17, 48), (49, 96), (97, 256)]
+        for name, fn in variants.items():
+            agg = {b: [0.0, 0.0, 0] for b in buckets}
+            for i in idx:
+                ctx = dec[i]
+                B = len(ctx)
+                meta, nb = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True, part_size=fn)
+                kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
+                vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
+                q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+                out = torch.empty(B, nq * 128, device=dev).bfloat16()
+                us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
+                            iters=10, warm=2)
+                b = next(bb for bb in buckets if bb[0] <= B <= bb[1])
+                agg[b][0] += us
+                agg[b][1] += sum(ctx) * nkv * 512
+                agg[b][2] += 1
+            tu = sum(v[0] for v in agg.values())
+            tb = sum(v[1] for v in agg.values())
+            res[f"replay decode {name} all"] = f"{tu / len(idx):.1f}us/step {tb / tu / 1e6:.2f} TB/s"
+            for b, (u, by, n) in agg.items():
+                if n:
+                    res[f"replay decode {name} B{b[0]}-{b[1]}"] = f"n={n} {u / n:.1f}us/step {by / u / 1e6:.2f} TB/s"
+        tot_us = fl = 0.0
+        idx = torch.randperm(len(pre), generator=rng)[: args.samples].tolist()
+        for i in idx:
+            ctx = [c for c, q in pre[i]]
+            ql = [q for c, q in pre[i]]
+            meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
+            kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
+            vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
+            T = sum(ql)
+            q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+            out = torch.empty(T, nq * 128, device=dev).bfloat16()
+            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
+                        iters=10, warm=2)
+            tot_us += us
+            fl += sum(sum(c - qq + j + 1 for j in range(qq)) for c, qq in zip(ctx, ql)) * nq * 128 * 4
+        res[f"replay prefill {len(idx)} steps"] = f"{tot_us / len(idx):.1f}us/step {fl / tot_us / 1e6:.1f} TFLOP/s"
     if args.what == "decode_sweep":
         for B in (32, 48, 56, 64, 72, 96, 128):
             for ctxv in (1000, 3400):

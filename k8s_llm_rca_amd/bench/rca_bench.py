@@ -197,7 +197,7 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (one engine over all ranks)")
     p.add_argument("--device", default="cuda")
-    p.add_argument("--incidents", type=int, default=64, help="concurrent RCA analyses per GPU per step")
+    p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses per GPU per step")
     p.add_argument("--graph-nodes", type=int, default=10_000)
     p.add_argument("--graph-device", action="store_true", help="mirror the stategraph to HBM (HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)

@@ -158,6 +158,57 @@ def main():
             tot_us += us
             fl += sum(sum(c - qq + j + 1 for j in range(qq)) for c, qq in zip(ctx, ql)) * nq * 128 * 4
         res[f"replay prefill {len(idx)} steps"] = f"{tot_us / len(idx):.1f}us/step {fl / tot_us / 1e6:.1f} TFLOP/s"
+    if args.what == "gemm_big":
+        for M in (512, 1024, 2048, 4096, 8192):
+            for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:
+                x = torch.randn(M, k, device=dev).bfloat16()
+                w = torch.randn(n, k, device=dev).bfloat16()
+                wt = w.t().contiguous()
+                fl = 2 * M * n * k
+                us = timeit(lambda: torch.nn.functional.linear(x, w), iters=10)
+                us2 = timeit(lambda: torch.mm(x, wt), iters=10)
+                res[f"big M{M} N{n} K{k}"] = f"NT {fl / us / 1e6:.0f} TF | NN {fl / us2 / 1e6:.0f} TF"
+    if args.what == "gemm_replay":
+        # per-step projection GEMMs of a recorded run: M = decode rows + prefill tokens
+        from k8s_llm_rca_amd.ops.linear import linear
+        steps = [json.loads(l) for l in open(args.trace)]
+        Ms = [len(s["d"]) + sum(q for _, q in s["p"]) for s in steps]
+        Ss = [len(s["d"]) + len(s["p"]) for s in steps]
+        shapes = {"qkv": (6144, 4096), "o": (4096, 4096), "gate_up": (28672, 4096), "down": (4096, 14336)}
+        W = {k: torch.randn(n, kk, device=dev).bfloat16() for k, (n, kk) in shapes.items()}
+        lm = torch.randn(128256, 4096, device=dev).bfloat16()
+        cache = {}
+
+        def t_of(name, M):
+            key = (name, M)
+            if key not in cache:
+                w = lm if name == "lm" else W[name]
+                x = torch.randn(M, w.shape[1], device=dev).bfloat16()
+                cache[key] = timeit(lambda: linear(x, w), iters=10, warm=2)
+            return cache[key]
+
+        def bucket(M):  # quantise M to keep the run short (<= 3% error)
+            if M <= 64:
+                return M
+            b = 1 << (M.bit_length() - 1)
+            step = max(1, b // 32)
+            return (M + step - 1) // step * step
+
+        tot = {k: 0.0 for k in list(shapes) + ["lm"]}
+        by_range = {}
+        for M, S in zip(Ms, Ss):
+            Mb = bucket(M)
+            rng = "M<=16" if M <= 16 else "M<=64" if M <= 64 else "M<=256" if M <= 256 else "M<=1024" if M <= 1024 \
+                else "M>1024"
+            for k in shapes:
+                us = t_of(k, Mb) * 32
+                tot[k] += us
+                by_range[rng] = by_range.get(rng, 0.0) + us
+            tot["lm"] += t_of("lm", bucket(S))
+        for k, v in tot.items():
+            res[f"gemm_replay {k}"] = f"{v / 1e6:.3f} s over {len(Ms)} steps"
+        for k, v in sorted(by_range.items()):
+            res[f"gemm_replay range {k}"] = f"{v / 1e6:.3f} s ({sum(1 for M in Ms if (k == 'M<=16' and M <= 16) or (k == 'M<=64' and 16 < M <= 64) or (k == 'M<=256' and 64 < M <= 256) or (k == 'M<=1024' and 256 < M <= 1024) or (k == 'M>1024' and M > 1024))} steps)"
     if args.what == "decode_sweep":
         for B in (32, 48, 56, 64, 72, 96, 128):
             for ctxv in (1000, 3400):

@@ -179,7 +179,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "post_s": round(d["post_s"], 3), "admit_s": round(d["admit_s"], 3),
-                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3)},
+                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
+                   **{k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}},
         "setup_s": round(setup_s, 1),
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }

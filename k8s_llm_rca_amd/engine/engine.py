@@ -61,6 +61,7 @@ class EngineConfig:
     max_decode_seqs: int = 256
     max_context: Optional[int] = None
     use_graphs: bool = True
+    gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
     temperature: float = 0.7
@@ -145,6 +146,7 @@ class LLMEngine:
         self.seqs: Dict[int, Sequence] = {}
         self._next_sid = 0
         self._incoming: List[tuple] = []
+        self._releases: List[int] = []
         self._lock = threading.Lock()
         self._cv = threading.Condition(self._lock)
         self._thread: Optional[threading.Thread] = None
@@ -158,10 +160,14 @@ class LLMEngine:
         # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
         # lines (replayed by tools/bench_kernels.py --what replay)
         self._shape_trace = os.environ.get("K8S_RCA_SHAPE_TRACE")
+        # K8S_RCA_STEP_TIMING=1: per-path host-issue vs GPU time of the forward
+        self._step_timing = os.environ.get("K8S_RCA_STEP_TIMING") == "1"
+        self._pending_ev: list = []
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
-                      "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0}
+                      "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
+                      "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0}
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -182,10 +188,33 @@ class LLMEngine:
         return sid
 
     def release_sequence(self, sid: int) -> None:
+        """Drop a sequence and its KV.  Callable from any thread: the engine
+        thread performs it (the KV pool is owned by the engine thread), after
+        the sequence's active request, if any, has finished."""
+        with self._cv:
+            self._releases.append(sid)
+            self._cv.notify()
+        if self._thread is None:  # synchronous use (run_until_idle / tests)
+            self._apply_releases()
+
+    def _apply_releases(self) -> None:
         with self._lock:
-            s = self.seqs.pop(sid, None)
-        if s is not None:
-            self.kv.release(s.blocks)
+            rel, self._releases = self._releases, []
+            keep = []
+            for sid in rel:
+                s = self.seqs.get(sid)
+                if s is not None and s.req is not None:
+                    keep.append(sid)  # still generating: release after it finishes
+                    continue
+                s = self.seqs.pop(sid, None)
+                if s is not None:
+                    self.kv.release(s.blocks)
+                    s.blocks = []
+            self._releases = keep + self._releases
+
+    def _snapshot(self) -> List[Sequence]:
+        with self._lock:
+            return list(self.seqs.values())
 
     def submit(self, sid: int, tokens: List[int], grammar=None, max_new: int = 256,
                temperature: Optional[float] = None, seed: int = 0,
@@ -199,6 +228,13 @@ class LLMEngine:
     def start(self) -> None:
         if self._thread is not None:
             return
+        # The engine thread shares the GIL with the callers' pipeline threads;
+        # CPython's default 5 ms switch interval can leave the GPU idle while
+        # the engine waits to reacquire it after each device sync.
+        si = float(os.environ.get("K8S_RCA_SWITCH_INTERVAL", self.cfg.gil_switch_interval or 0))
+        if si > 0:
+            import sys
+            sys.setswitchinterval(si)
         self._stop = False
         self._thread = threading.Thread(target=self._loop, name="llm-engine", daemon=True)
         self._thread.start()
@@ -216,7 +252,7 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         while True:
             with self._cv:
-                while not self._stop and not self._incoming and not self._has_work():
+                while not self._stop and not self._incoming and not self._releases and not self._has_work():
                     self._cv.wait(0.05)
                 if self._stop:
                     return
@@ -228,7 +264,7 @@ class LLMEngine:
                 self._fail_all(repr(e))
 
     def _fail_all(self, err: str) -> None:
-        for s in list(self.seqs.values()):
+        for s in self._snapshot():
             r = s.req
             if r is not None:
                 s.req = None
@@ -250,8 +286,9 @@ class LLMEngine:
     def _admit(self) -> None:
         with self._lock:
             inc, self._incoming = self._incoming, []
+            seqs = {sid: self.seqs[sid] for sid, *_ in inc}
         for sid, toks, grammar, max_new, temp, seed, on_done in inc:
-            s = self.seqs[sid]
+            s = seqs[sid]
             if s.req is not None:
                 raise RuntimeError(f"sequence {sid} already has an active request")
             # longest common prefix with what is cached -> keep that KV
@@ -315,7 +352,7 @@ class LLMEngine:
         return True
 
     def _evict(self, n_blocks: int, protect: set) -> None:
-        idle = sorted((s for s in self.seqs.values() if s.req is None and s.blocks and s.id not in protect),
+        idle = sorted((s for s in self._snapshot() if s.req is None and s.blocks and s.id not in protect),
                       key=lambda s: s.last_used)
         freed = 0
         for s in idle:
@@ -331,7 +368,9 @@ class LLMEngine:
         t_host0 = time.perf_counter()
         self._admit()
         self.stats["admit_s"] += time.perf_counter() - t_host0
-        active = [s for s in self.seqs.values() if s.req is not None and s.pending > 0]
+        if self._releases:
+            self._apply_releases()
+        active = [s for s in self._snapshot() if s.req is not None and s.pending > 0]
         if not active:
             return False
         BS = self.kv.block_size
@@ -411,17 +450,34 @@ class LLMEngine:
 
     def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int]):
         t0 = time.perf_counter()
+        timed = self._step_timing and self.device.type == "cuda"
+        if timed:
+            ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            ev[0].record()
         if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1
                 and self.kv.block_size % 64 == 0):
             out = self._forward_graph(decode)
             self.stats["graph_steps"] += 1
             self.stats["decode_steps"] += 1
+            kind = "graph"
         else:
             out = self._forward_eager(decode, chunks, sample_idx)
             if not chunks:
                 self.stats["decode_steps"] += 1
-        self.stats["forward_s"] += time.perf_counter() - t0
+            kind = "eager"
+        dt = time.perf_counter() - t0
+        self.stats["forward_s"] += dt
+        if timed:
+            ev[1].record()
+            self._pending_ev.append((kind, dt, ev))
         return out
+
+    def _collect_timing(self) -> None:
+        """Fold finished step events into stats (called after the step's sync)."""
+        for kind, dt, (e0, e1) in self._pending_ev:
+            self.stats[kind + "_issue_s"] += dt
+            self.stats[kind + "_gpu_s"] += e0.elapsed_time(e1) / 1e3
+        self._pending_ev = []
 
     def _to_dev(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
         """One H2D copy for all int32 metadata arrays."""
@@ -723,13 +779,16 @@ class LLMEngine:
         table = self._mask_table()
         if not lists:
             lists = [0]
-        ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps])
-        d_temps = torch.from_numpy(temps).to(self.device)
+        ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps,
+                             temps.view(np.int32)])
+        d_temps = ints[6].view(torch.float32)
         tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
                          vocab=self.vocab)
         t1 = time.perf_counter()
         toks = tok.tolist()
         now = time.perf_counter()
+        if self._pending_ev:
+            self._collect_timing()
         self.stats["wait_s"] += now - t1
         self.stats["sample_s"] += now - t0
         for s, t in zip(seqs, toks):

@@ -151,3 +151,50 @@ def test_mixtral_and_opt_engines_generate():
                    on_done=lambda gen, st: out.setdefault("t", eng.tok.decode(gen)))
         eng.run_until_idle()
         assert json.loads(out["t"])["a"] in ("x", "yy")
+
+
+def test_concurrent_clients_race_stress():
+    """Race detection: many client threads create / submit / release sequences
+    while the engine thread steps, with a tiny GIL switch interval to force
+    interleavings; every request must finish and every KV block come back."""
+    import sys
+    import threading
+    eng = _engine(num_blocks=256, max_batch_tokens=64)
+    free0 = eng.kv.free_blocks
+    old = sys.getswitchinterval()
+    sys.setswitchinterval(1e-6)
+    errors, done = [], []
+    eng.start()
+
+    def client(k):
+        try:
+            for i in range(6):
+                sid = eng.new_sequence()
+                ev = threading.Event()
+                p = eng.tok.system_prefix("s") + eng.tok.message("user", f"client {k} run {i} " * (3 + i)) + \
+                    eng.tok.header("assistant")
+                eng.submit(sid, p, None, 5, on_done=lambda g, st: ev.set())
+                if not ev.wait(60):
+                    errors.append(f"client {k} run {i} timed out")
+                    return
+                done.append((k, i))
+                eng.release_sequence(sid)
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    ths = [threading.Thread(target=client, args=(k,)) for k in range(8)]
+    try:
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join(120)
+    finally:
+        sys.setswitchinterval(old)
+    import time as _t
+    t0 = _t.time()
+    while eng.seqs and _t.time() - t0 < 10:
+        _t.sleep(0.01)
+    eng.stop()
+    assert not errors and eng.error is None, (errors, eng.error)
+    assert len(done) == 48
+    assert not eng.seqs and eng.kv.free_blocks == free0

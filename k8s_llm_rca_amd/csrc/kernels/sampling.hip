@@ -7,6 +7,10 @@
 //   * bitmap: mask_table[mask_id[row]] is a [V/32] uint32 allow-bitmap
 //   * list:   an explicit allow-list slice (list_off, list_len) of token ids
 // Logits are bf16 [B][ld]; one 256-thread workgroup per row.
+// Vocab-parallel (TP) form: the rank holds columns [vocab_off, vocab_off + V)
+// of the vocabulary; noise and masks are keyed by the GLOBAL token id, so the
+// per-rank (score, id) winners combined by max over ranks give exactly the
+// token the unsharded kernel would sample (B10 without a logits all-gather).
 #include "common.h"
 
 namespace k8s {
@@ -36,14 +40,15 @@ __device__ __forceinline__ Best better(Best a, Best b) {
   return a;
 }
 
-__global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict__ logits, int ld, int V,
+__global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict__ logits, int ld, int V, int vocab_off,
                                                      const float* __restrict__ temperature,
                                                      const uint32_t* __restrict__ seeds,
                                                      const int* __restrict__ steps,
                                                      const int* __restrict__ mask_id,
                                                      const uint32_t* __restrict__ mask_table, int mask_words,
                                                      const int* __restrict__ list_off, const int* __restrict__ list_len,
-                                                     const int* __restrict__ lists, int* __restrict__ out) {
+                                                     const int* __restrict__ lists, int* __restrict__ out,
+                                                     float2* __restrict__ out_pair) {
   const int row = blockIdx.x;
   const uint16_t* lr = logits + (size_t)row * ld;
   const float temp = temperature ? temperature[row] : 0.f;
@@ -56,35 +61,37 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
   if (ll > 0) {
     const int* lst = lists + list_off[row];
     for (int k = threadIdx.x; k < ll; k += blockDim.x) {
-      const int i = lst[k];
+      const int gi = lst[k];
+      const int i = gi - vocab_off;
       if (i < 0 || i >= V) continue;
       float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, row, step, i);
-      best = better(best, Best{v, i});
+      if (!greedy) v += gumbel(seed, row, step, gi);
+      best = better(best, Best{v, gi});
     }
   } else {
     const int mid = mask_id ? mask_id[row] : -1;
     const uint32_t* mk = (mid >= 0) ? mask_table + (size_t)mid * mask_words : nullptr;
     const int nv = V >> 3;
     for (int c = threadIdx.x; c < nv; c += blockDim.x) {
-      const int i0 = c * 8;
+      const int i0 = c * 8, g0 = vocab_off + i0;  // vocab_off % 8 == 0 (host-checked)
       uint32_t bits = 0xFFu;
-      if (mk) bits = (mk[i0 >> 5] >> (i0 & 31)) & 0xFFu;
+      if (mk) bits = (mk[g0 >> 5] >> (g0 & 31)) & 0xFFu;
       if (!bits) continue;
       u16x8 x = *reinterpret_cast<const u16x8*>(lr + i0);
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         if (!((bits >> j) & 1u)) continue;
         float v = bf2f(x[j]) * it;
-        if (!greedy) v += gumbel(seed, row, step, i0 + j);
-        best = better(best, Best{v, i0 + j});
+        if (!greedy) v += gumbel(seed, row, step, g0 + j);
+        best = better(best, Best{v, g0 + j});
       }
     }
     for (int i = (nv << 3) + threadIdx.x; i < V; i += blockDim.x) {  // tail (V % 8)
-      if (mk && !((mk[i >> 5] >> (i & 31)) & 1u)) continue;
+      const int gi = vocab_off + i;
+      if (mk && !((mk[gi >> 5] >> (gi & 31)) & 1u)) continue;
       float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, row, step, i);
-      best = better(best, Best{v, i});
+      if (!greedy) v += gumbel(seed, row, step, gi);
+      best = better(best, Best{v, gi});
     }
   }
   // block argmax
@@ -104,7 +111,8 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
   if (threadIdx.x == 0) {
     Best b{sv[0], si[0]};
     for (int k = 1; k < (int)(blockDim.x >> 6); ++k) b = better(b, Best{sv[k], si[k]});
-    out[row] = b.i;
+    if (out) out[row] = b.i;
+    if (out_pair) out_pair[row] = make_float2(b.v, (float)b.i);  // ids < 2^24: exact in f32
   }
 }
 
@@ -112,11 +120,14 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
 
 using namespace k8s;
 
-K8S_API int k8s_sample(const void* logits, int ld, int B, int V, const float* temperature, const uint32_t* seeds,
-                       const int* steps, const int* mask_id, const uint32_t* mask_table, int mask_words,
-                       const int* list_off, const int* list_len, const int* lists, int* out, hipStream_t s) {
+K8S_API int k8s_sample(const void* logits, int ld, int B, int V, int vocab_off, const float* temperature,
+                       const uint32_t* seeds, const int* steps, const int* mask_id, const uint32_t* mask_table,
+                       int mask_words, const int* list_off, const int* list_len, const int* lists, int* out,
+                       float* out_pair, hipStream_t s) {
   if (B <= 0) return 0;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, ld, V, temperature, seeds,
-                     steps, mask_id, mask_table, mask_words, list_off, list_len, lists, out);
+  if (vocab_off % 8 || (vocab_off + V) >= (1 << 24)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, ld, V, vocab_off, temperature,
+                     seeds, steps, mask_id, mask_table, mask_words, list_off, list_len, lists, out,
+                     reinterpret_cast<float2*>(out_pair));
   return (int)hipGetLastError();
 }

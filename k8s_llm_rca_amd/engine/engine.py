@@ -157,6 +157,11 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
+        # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
+        self._dist_sample = (self.pc.tp_size > 1 and hasattr(self.model, "vocab_local")
+                             and self.model.vocab_local % 8 == 0)
+        self._mask_sent = 0      # rank 0: mask-table rows already broadcast to the workers
+        self._wmask = None       # TP ranks: device copy of the mask table (rows received so far)
         # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
         # lines (replayed by tools/bench_kernels.py --what replay)
         self._shape_trace = os.environ.get("K8S_RCA_SHAPE_TRACE")
@@ -584,7 +589,58 @@ class LLMEngine:
                     self._pf_ws = A.prefill_workspace(self.model.nkv, self.device)
                 pmeta.pf_o, pmeta.pf_ml = self._pf_ws
         inp = StepInputs(d_ids, d_pos, d_slots, nd, dmeta, pmeta, d_sidx.long())
+        if self._dist_sample:
+            return self.model.forward(inp, self.kv.k, self.kv.v, gather_logits=False)
         return self.model.forward(inp, self.kv.k, self.kv.v)
+
+    # ------------------------------------------------- TP vocab-parallel sampling
+    SHDR = 4
+
+    def _tp_sample(self, logits, mask_id, list_off, list_len, lists, seeds, steps, temps) -> torch.Tensor:
+        """Rank 0: broadcast this step's sampling inputs (plus mask rows the
+        workers have not seen), then sample on every rank's vocab shard."""
+        import numpy as np_
+        table = self.grt.masks.array() if self.grt.masks.rows else np_.zeros((0, self.grt.masks.words), np_.int32)
+        new = table[self._mask_sent:]
+        self._mask_sent = table.shape[0]
+        B = mask_id.shape[0]
+        hdr = np_.array([B, len(lists), new.shape[0], self.grt.masks.words], dtype=np_.int64)
+        flat = np_.concatenate([mask_id, list_off, list_len, lists, seeds, steps, temps.view(np_.int32),
+                                new.reshape(-1).astype(np_.int32)])
+        h = torch.from_numpy(hdr).to(self._comm_device())
+        self._bcast(h)
+        dev = self._to_dev([flat])[0]
+        self._bcast(dev)
+        return self._sample_shard(logits, hdr, dev)
+
+    def _sample_shard(self, logits, hdr, dev) -> torch.Tensor:
+        """Every TP rank: masked Gumbel-max over its vocab shard, then an
+        all-gather of the [B, 2] winners (a few bytes per row instead of the
+        [B, vocab] logits)."""
+        import torch.distributed as dist
+        B, L, nr, words = (int(x) for x in hdr)
+        o = 0
+
+        def take(n):
+            nonlocal o
+            t = dev[o:o + n]
+            o += n
+            return t
+
+        mask_id, list_off, list_len, lists, seeds, steps = (take(B), take(B), take(B), take(L), take(B), take(B))
+        temps = take(B).view(torch.float32)
+        rows = take(nr * words).view(nr, words)
+        if nr:
+            self._wmask = rows.clone() if self._wmask is None else torch.cat([self._wmask, rows])
+        table = self._wmask if self._wmask is not None else torch.zeros(1, words, dtype=torch.int32,
+                                                                         device=self.device)
+        off = self.pc.tp_rank * self.model.vocab_local
+        pairs = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
+                           vocab_off=off, pairs=True)
+        comm = pairs.to(self._comm_device())
+        parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
+        dist.all_gather(parts, comm, group=self.pc.tp_group)
+        return SMP.combine_pairs(torch.stack(parts)).to(self.device)
 
     def _bcast(self, t: torch.Tensor) -> None:
         import torch.distributed as dist
@@ -616,7 +672,15 @@ class LLMEngine:
             dev = torch.empty(int(header[1]), dtype=torch.int32, device=self.device)
             self._bcast(dev)
             host = dev.numpy() if self.device.type == "cpu" else None
-            self._exec_step(header, host, dev)
+            logits = self._exec_step(header, host, dev)
+            if self._dist_sample and int(header[9]) > 0:  # rank 0 samples these rows: join it
+                sh = torch.empty(self.SHDR, dtype=torch.int64, device=cd)
+                self._bcast(sh)
+                shdr = sh.cpu().numpy()
+                n = int(shdr[0]) * 6 + int(shdr[1]) + int(shdr[2]) * int(shdr[3])
+                sdev = torch.empty(n, dtype=torch.int32, device=self.device)
+                self._bcast(sdev)
+                self._sample_shard(logits, shdr, sdev)
 
     def stop_workers(self) -> None:
         if self.pc.tp_size > 1 and self.pc.tp_rank == 0:
@@ -776,14 +840,18 @@ class LLMEngine:
             temps[i] = r.temperature
             seeds[i] = (r.seed * 2654435761 + s.id) & 0x7FFFFFFF
             steps[i] = len(r.generated)
-        table = self._mask_table()
         if not lists:
             lists = [0]
-        ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps,
-                             temps.view(np.int32)])
-        d_temps = ints[6].view(torch.float32)
-        tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
-                         vocab=self.vocab)
+        if self._dist_sample:
+            tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
+                                  seeds, steps, temps)
+        else:
+            table = self._mask_table()
+            ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps,
+                                 temps.view(np.int32)])
+            d_temps = ints[6].view(torch.float32)
+            tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
+                             vocab=self.vocab)
         t1 = time.perf_counter()
         toks = tok.tolist()
         now = time.perf_counter()

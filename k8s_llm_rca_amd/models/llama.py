@@ -144,8 +144,11 @@ class LlamaModel:
         return n
 
     # -------------------------------------------------------------- forward
-    def forward(self, inp: StepInputs, k_cache: torch.Tensor, v_cache: torch.Tensor) -> torch.Tensor:
-        """k_cache/v_cache: [n_layers, NB, nkv, BS, D] / [n_layers, NB, nkv, D, BS]."""
+    def forward(self, inp: StepInputs, k_cache: torch.Tensor, v_cache: torch.Tensor,
+                gather_logits: bool = True) -> torch.Tensor:
+        """k_cache/v_cache: [n_layers, NB, nkv, BS, D] / [n_layers, NB, nkv, D, BS].
+        ``gather_logits=False`` under TP returns this rank's vocab shard
+        (columns ``tp_rank * vocab_local ..``) for distributed sampling."""
         cfg = self.cfg
         T = inp.input_ids.shape[0]
         H = cfg.hidden
@@ -180,4 +183,4 @@ class LlamaModel:
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
         logits = linear(sel, self.lm_head)
-        return self.pc.all_gather_last(logits)
+        return self.pc.all_gather_last(logits) if gather_logits else logits

@@ -199,6 +199,35 @@ def test_sampling(temp):
         assert (o == r).float().mean() >= 0.6  # fast-log vs log ties aside
 
 
+@pytest.mark.parametrize("tp", [2, 8])
+def test_sampling_vocab_parallel_matches_full(tp):
+    """B10: per-shard (score, id) winners combined across ranks == the
+    single-device kernel on the full logits (same noise, masks by global id)."""
+    _need_gpu()
+    B, V = 6, 128256
+    logits = torch.randn(B, V, device=dev).bfloat16()
+    words = (V + 31) // 32
+    table = torch.zeros(2, words, dtype=torch.int32)
+    table[0] = -1
+    bits = torch.zeros(words * 32, dtype=torch.bool)
+    bits[torch.randperm(V)[:900]] = True
+    table[1] = (bits.view(words, 32).long() << torch.arange(32)).sum(1).to(torch.int64).to(torch.int32)
+    mask_id = torch.tensor([-1, 0, 1, 1, 0, -1], dtype=torch.int32)
+    lists = torch.tensor([5, 20000, 127000, 64000], dtype=torch.int32)
+    list_off = torch.zeros(B, dtype=torch.int32)
+    list_len = torch.tensor([0, 0, 0, 4, 0, 0], dtype=torch.int32)
+    temps = torch.tensor([0.0, 0.7, 0.9, 1.0, 0.0, 1.3])
+    seeds = torch.arange(B, dtype=torch.int32) * 3 + 1
+    steps = torch.arange(B, dtype=torch.int32) + 11
+    args = [a.to(dev) for a in (temps, seeds, steps, mask_id, table, list_off, list_len, lists)]
+    full = SMP.sample(logits, *args, vocab=V)
+    vl = V // tp
+    parts = [SMP.sample(logits[:, r * vl:(r + 1) * vl].contiguous(), *args, vocab=V, vocab_off=r * vl, pairs=True)
+             for r in range(tp)]
+    got = SMP.combine_pairs(torch.stack(parts))
+    assert torch.equal(got.cpu(), full.cpu())
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (512, 14336), (1280, 8192)])
 def test_gemm_skinny(M, N, K):

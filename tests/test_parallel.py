@@ -87,7 +87,7 @@ def test_tp2_matches_tp1(name):
     torch.testing.assert_close(got, ref, atol=2e-4, rtol=2e-4)
 
 
-def _run_engine(rank, world, port, out_path):
+def _run_engine(rank, world, port, out_path, temperature=0.0, grammar=False):
     import torch.distributed as dist
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
     from k8s_llm_rca_amd.models.config import get_config
@@ -100,7 +100,7 @@ def _run_engine(rank, world, port, out_path):
     else:
         pc = None
     cfg = EngineConfig(model="tiny-llama", device="cpu", dtype=torch.float32, num_blocks=32, block_size=32,
-                       max_batch_tokens=64, temperature=0.0)
+                       max_batch_tokens=64, temperature=temperature)
     model = LlamaModel(get_config("tiny-llama"), "cpu", torch.float32, pc, seed=5, init_mode="full_slice")
     eng = LLMEngine(cfg, pc, model=model)
     if rank > 0:
@@ -111,7 +111,13 @@ def _run_engine(rank, world, port, out_path):
             sid = eng.new_sequence()
             toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "message %d " % i * (5 + 9 * i)) + \
                 eng.tok.header("assistant")
-            eng.submit(sid, toks, None, 12, temperature=0.0, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+            g = None
+            if grammar:  # exercises list and bitmap masks in the distributed sampler
+                from k8s_llm_rca_amd.engine.grammar import Choice, Free, Grammar, Lit
+                g = Grammar([Lit('{"k": '), Choice(['"alpha"', '"beta"', '"gamma"'], "c"), Lit(', "t": "'),
+                             Free(6, name="t"), Lit('"}')])
+            eng.submit(sid, toks, g, 12, temperature=temperature, seed=7,
+                       on_done=lambda g, st, i=i: outs.__setitem__(i, g))
         eng.run_until_idle()
         eng.stop_workers()
         torch.save(outs, out_path)
@@ -127,3 +133,15 @@ def test_tp2_engine_generation_matches_tp1():
         a = torch.load(o2, weights_only=True)
         b = torch.load(o1, weights_only=True)
     assert a == b and all(len(v) == 12 for v in a.values())
+
+
+def test_tp2_distributed_sampling_with_grammar_matches_tp1():
+    """Vocab-parallel Gumbel-max sampling (masks keyed by global id) must pick
+    the same tokens as single-device sampling of the gathered logits."""
+    with tempfile.TemporaryDirectory() as d:
+        o2, o1 = os.path.join(d, "tp2.pt"), os.path.join(d, "tp1.pt")
+        mp.spawn(_run_engine, args=(2, _free_port(), o2, 0.9, True), nprocs=2, join=True)
+        _run_engine(0, 1, _free_port(), o1, 0.9, True)
+        a = torch.load(o2, weights_only=True)
+        b = torch.load(o1, weights_only=True)
+    assert a == b and len(a) == 3

@@ -94,11 +94,11 @@ def run(args) -> Optional[Dict[str, Any]]:
     tp_mode = args.tp > 1
     if tp_mode:
         import torch.distributed as dist
-        from ..parallel.groups import ParallelContext
+        from ..parallel.groups import ParallelContext, attach_custom_allreduce
         if world != args.tp:
             raise SystemExit(f"--tp {args.tp} needs WORLD_SIZE={args.tp} (one TP engine over all ranks)")
-        pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, ep_size=world, ep_rank=rank,
-                             ep_group=dist.group.WORLD)
+        pc = attach_custom_allreduce(ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD,
+                                                     ep_size=world, ep_rank=rank, ep_group=dist.group.WORLD))
     eng = LLMEngine(EngineConfig(model=args.model, device=str(device),
                                  dtype=torch.bfloat16 if cuda else torch.float32,
                                  kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,

@@ -1,0 +1,224 @@
+// Custom all-reduce over xGMI peer memory (B14 in SURVEY.md §2 Part B; §5.8).
+//
+// For the latency-bound TP all-reduces of decode (16 KiB .. a few MiB, two per
+// layer) RCCL's ring pays per-step launch + protocol latency; on a full xGMI
+// mesh every GPU can instead READ all its peers directly (7 links at once).
+// Each rank owns one IPC-exported, uncached buffer:
+//
+//   [FLAGS_A 8x256 u32][FLAGS_B 8x256 u32][EPOCH 256 u32][STATUS][DATA 2 x max][RES 2 x max]
+//
+// and every rank maps every peer's buffer (hipIpcOpenMemHandle).  Work is
+// split into per-block slices; block b of every rank only ever synchronises
+// with block b of the other ranks, through per-(source rank, block) flags, so
+// there is no grid-wide barrier:
+//   one-shot : stage own slice -> signal(A) -> wait(A) -> sum the slice from all
+//              ranks (fixed rank order: bit-identical results on every rank)
+//   two-shot : stage -> A -> reduce my 1/N part of the slice into RES ->
+//              signal(B) -> wait(B) -> gather the N reduced parts
+// (two-shot moves 2(N-1)/N of the data per rank instead of N-1: mid sizes).
+// Epochs live in device memory (one counter per block, touched only by that
+// block), so the kernel is HIP-graph capturable; DATA / RES are double
+// buffered by epoch parity: a rank re-writes a parity buffer only after every
+// peer has signalled the following epoch, i.e. finished reading it.
+// Signals are system-scope release stores into the PEER's flag array, waits
+// are system-scope acquire loads of our own; spins are bounded (wall clock)
+// and record a timeout in STATUS instead of hanging the GPU.
+#include <cstring>
+
+#include "common.h"
+
+namespace k8s {
+
+constexpr int AR_MAX_WORLD = 8;
+constexpr int AR_MAX_BLOCKS = 256;
+constexpr int AR_THREADS = 512;
+constexpr size_t AR_FLAGS_A = 0;
+constexpr size_t AR_FLAGS_B = AR_FLAGS_A + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
+constexpr size_t AR_EPOCH = AR_FLAGS_B + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
+constexpr size_t AR_STATUS = AR_EPOCH + 4 * AR_MAX_BLOCKS;
+constexpr size_t AR_DATA = 32768;
+
+struct ARPeers {
+  unsigned char* base[AR_MAX_WORLD];
+};
+
+struct ARCtx {
+  ARPeers peers;
+  int world, rank;
+  long max_bytes;
+  uint64_t timeout_ticks;
+  bool used;
+};
+
+static ARCtx g_ctx[16];
+
+__device__ __forceinline__ void ar_signal(const ARPeers& P, size_t flags, int world, int rank, int b, uint32_t e) {
+  const int t = threadIdx.x;
+  if (t < world) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(P.base[t] + flags) + rank * AR_MAX_BLOCKS + b;
+    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  }
+}
+
+__device__ __forceinline__ void ar_wait(unsigned char* own, size_t flags, int world, int b, uint32_t e,
+                                        uint64_t timeout_ticks) {
+  const int t = threadIdx.x;
+  if (t < world) {
+    uint32_t* f = reinterpret_cast<uint32_t*>(own + flags) + t * AR_MAX_BLOCKS + b;
+    const uint64_t t0 = wall_clock64();
+    while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (wall_clock64() - t0 > timeout_ticks) {
+        __hip_atomic_store(reinterpret_cast<uint32_t*>(own + AR_STATUS), 1u, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(2);
+    }
+  }
+  __syncthreads();
+}
+
+// sum of `world` bf16 vectors [i, i+8) at byte offset `off` of every rank's buffer
+__device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off) {
+  float acc[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) acc[j] = 0.f;
+  for (int p = 0; p < world; ++p) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(P.base[p] + off);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+  }
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(acc[j]);
+  return r;
+}
+
+// n % 8 == 0 (host-checked); slice = elements per block (multiple of 8 * world)
+template <bool TWO_SHOT>
+__global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
+                                                         long n, long slice, int world, int rank, ARPeers P,
+                                                         long max_bytes, uint64_t timeout_ticks) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  unsigned char* own = P.base[rank];
+  uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH) + b;
+  __shared__ uint32_t s_e;
+  if (t == 0) s_e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t data = AR_DATA + (size_t)(e & 1u) * max_bytes;
+  const size_t res = AR_DATA + 2 * (size_t)max_bytes + (size_t)(e & 1u) * max_bytes;
+  const long i0 = (long)b * slice, i1 = min(n, i0 + slice);
+
+  // 1) stage this rank's slice
+  for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
+    *reinterpret_cast<u16x8*>(own + data + 2 * i) = *reinterpret_cast<const u16x8*>(in + i);
+  __threadfence_system();
+  __syncthreads();
+  ar_signal(P, AR_FLAGS_A, world, rank, b, e);
+  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks);
+
+  if (!TWO_SHOT) {
+    for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
+      *reinterpret_cast<u16x8*>(out + i) = ar_sum8(P, world, data + 2 * i);
+  } else {
+    const long part = slice / world;
+    const long p0 = i0 + (long)rank * part, p1 = min(i1, p0 + part);
+    for (long i = p0 + 8L * t; i < p1; i += 8L * AR_THREADS)
+      *reinterpret_cast<u16x8*>(own + res + 2 * i) = ar_sum8(P, world, data + 2 * i);
+    __threadfence_system();
+    __syncthreads();
+    ar_signal(P, AR_FLAGS_B, world, rank, b, e);
+    ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks);
+    for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS) {
+      const int owner = (int)((i - i0) / part);
+      *reinterpret_cast<u16x8*>(out + i) = *reinterpret_cast<const u16x8*>(P.base[owner] + res + 2 * i);
+    }
+  }
+  __syncthreads();
+  if (t == 0) __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+}  // namespace k8s
+
+using namespace k8s;
+
+K8S_API long k8s_ar_buffer_bytes(long max_bytes) { return (long)AR_DATA + 4 * max_bytes; }
+
+K8S_API int k8s_ar_alloc(long bytes, void** out) {
+  hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached);
+  if (e != hipSuccess) return (int)e;
+  return (int)hipMemset(*out, 0, (size_t)bytes);
+}
+
+K8S_API int k8s_ar_free(void* p) { return (int)hipFree(p); }
+
+K8S_API int k8s_ar_get_handle(void* p, void* handle64) {
+  return (int)hipIpcGetMemHandle(reinterpret_cast<hipIpcMemHandle_t*>(handle64), p);
+}
+
+K8S_API int k8s_ar_open_handle(const void* handle64, void** out) {
+  hipIpcMemHandle_t h;
+  memcpy(&h, handle64, sizeof(h));
+  return (int)hipIpcOpenMemHandle(out, h, hipIpcMemLazyEnablePeerAccess);
+}
+
+K8S_API int k8s_ar_close_handle(void* p) { return (int)hipIpcCloseMemHandle(p); }
+
+K8S_API int k8s_ar_handle_size() { return (int)sizeof(hipIpcMemHandle_t); }
+
+// Register the mapped buffers of one communicator; returns an id >= 0.
+K8S_API int k8s_ar_register(int world, int rank, void** bases, long max_bytes, double timeout_s) {
+  if (world < 1 || world > AR_MAX_WORLD || rank < 0 || rank >= world || max_bytes % 16) return -1;
+  int dev = 0, khz = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return -1;
+  if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, dev) != hipSuccess || khz <= 0) khz = 100000;
+  for (int id = 0; id < 16; ++id) {
+    if (g_ctx[id].used) continue;
+    ARCtx& c = g_ctx[id];
+    for (int p = 0; p < AR_MAX_WORLD; ++p) c.peers.base[p] = p < world ? (unsigned char*)bases[p] : nullptr;
+    c.world = world;
+    c.rank = rank;
+    c.max_bytes = max_bytes;
+    c.timeout_ticks = (uint64_t)(timeout_s * khz * 1000.0);
+    c.used = true;
+    return id;
+  }
+  return -1;
+}
+
+K8S_API int k8s_ar_unregister(int id) {
+  if (id < 0 || id >= 16) return (int)hipErrorInvalidValue;
+  g_ctx[id].used = false;
+  return 0;
+}
+
+// bf16 all-reduce (sum) of n elements; in == out is allowed.  mode: 1 one-shot, 2 two-shot.
+K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int mode, hipStream_t s) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  const ARCtx& c = g_ctx[id];
+  if (n <= 0) return 0;
+  if (n % 8 || 2 * n > c.max_bytes) return (int)hipErrorInvalidValue;
+  const long unit = 8L * (mode == 2 ? c.world : 1);
+  long nb = (n + 4095) / 4096;  // >= 8 KB of bf16 per block
+  if (nb > AR_MAX_BLOCKS) nb = AR_MAX_BLOCKS;
+  long slice = (n + nb - 1) / nb;
+  slice = (slice + unit - 1) / unit * unit;
+  nb = (n + slice - 1) / slice;
+  if (mode == 2)
+    hipLaunchKernelGGL(ar_kernel<true>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+  else
+    hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+  return (int)hipGetLastError();
+}
+
+// 0 = healthy, 1 = a wait timed out (a peer never arrived); synchronous read.
+K8S_API int k8s_ar_status(int id, int* out) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  uint32_t v = 0;
+  hipError_t e = hipMemcpy(&v, g_ctx[id].peers.base[g_ctx[id].rank] + AR_STATUS, 4, hipMemcpyDeviceToHost);
+  *out = (int)v;
+  return (int)e;
+}

@@ -25,6 +25,7 @@ class ParallelContext:
     ep_rank: int = 0
     ep_group: Optional[object] = None
     comm_stream: Optional[object] = None  # HIP stream for overlapped collectives
+    custom_ar: Optional[object] = None    # parallel.xgmi.XgmiAllReduce for small TP messages
 
     @property
     def is_tp(self) -> bool:
@@ -32,6 +33,9 @@ class ParallelContext:
 
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
+            car = self.custom_ar
+            if car is not None and car.mode_for(t):
+                return car(t)
             dist.all_reduce(t, group=self.tp_group)
         return t
 
@@ -58,8 +62,24 @@ def init_distributed(backend: Optional[str] = None) -> ParallelContext:
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         dist.init_process_group(backend)
     r = dist.get_rank()
-    return ParallelContext(tp_size=world, tp_rank=r, tp_group=dist.group.WORLD, ep_size=world, ep_rank=r,
-                           ep_group=dist.group.WORLD)
+    pc = ParallelContext(tp_size=world, tp_rank=r, tp_group=dist.group.WORLD, ep_size=world, ep_rank=r,
+                         ep_group=dist.group.WORLD)
+    attach_custom_allreduce(pc)
+    return pc
+
+
+def attach_custom_allreduce(pc: ParallelContext) -> ParallelContext:
+    """Give a GPU TP context the xGMI one/two-shot all-reduce for small
+    messages (``K8S_RCA_CUSTOM_AR=0`` keeps every all-reduce on RCCL)."""
+    if (pc.tp_size > 1 and torch.cuda.is_available() and os.environ.get("K8S_RCA_CUSTOM_AR", "1") != "0"
+            and dist.get_backend(pc.tp_group) == "nccl"):
+        try:
+            from .xgmi import XgmiAllReduce
+            pc.custom_ar = XgmiAllReduce(pc.tp_group)
+        except Exception as e:  # noqa: BLE001 - RCCL remains correct, only slower for small messages
+            import logging
+            logging.getLogger(__name__).warning("xGMI all-reduce unavailable (%s); using RCCL", e)
+    return pc
 
 
 def single() -> ParallelContext:

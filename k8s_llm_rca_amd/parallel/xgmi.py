@@ -1,0 +1,124 @@
+"""Custom one-shot / two-shot all-reduce over xGMI peer memory (B14).
+
+``csrc/kernels/allreduce.hip`` does the work; this module sets up the IPC
+buffers: every rank allocates one uncached buffer, exports it with
+``hipIpcGetMemHandle``, the 64-byte handles are exchanged with
+``all_gather_object`` on the TP group, and every rank maps every peer's buffer.
+
+Selection (``XgmiAllReduce.mode_for``): one-shot up to 512 KiB (each rank reads
+all peers: latency-optimal), two-shot up to ``max_bytes`` (reduce-scatter +
+all-gather through the same buffers: 2(N-1)/N of the bytes), RCCL beyond.
+The TP decode all-reduces of the 70B config (16 KiB .. 4 MiB) land in the
+custom path; prefill-sized messages stay on RCCL's multi-channel rings.
+"""
+from __future__ import annotations
+
+import ctypes
+import logging
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops._lib import lib, stream_ptr
+
+log = logging.getLogger(__name__)
+
+ONE_SHOT_MAX = 512 << 10
+
+
+def _bind(L) -> None:
+    if getattr(L, "_ar_bound", False):
+        return
+    c_long, c_int, P = ctypes.c_long, ctypes.c_int, ctypes.c_void_p
+    sigs = {
+        "k8s_ar_buffer_bytes": ([c_long], c_long),
+        "k8s_ar_alloc": ([c_long, ctypes.POINTER(P)], c_int),
+        "k8s_ar_free": ([P], c_int),
+        "k8s_ar_get_handle": ([P, ctypes.c_char_p], c_int),
+        "k8s_ar_open_handle": ([ctypes.c_char_p, ctypes.POINTER(P)], c_int),
+        "k8s_ar_close_handle": ([P], c_int),
+        "k8s_ar_handle_size": ([], c_int),
+        "k8s_ar_register": ([c_int, c_int, ctypes.POINTER(P), c_long, ctypes.c_double], c_int),
+        "k8s_ar_unregister": ([c_int], c_int),
+        "k8s_ar_allreduce_bf16": ([c_int, P, P, c_long, c_int, P], c_int),
+        "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    L._ar_bound = True
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise RuntimeError(f"{what} failed (hip error {rc})")
+
+
+class XgmiAllReduce:
+    """In-place bf16 sum over a process group whose ranks share an xGMI mesh
+    (one process per GPU, all in one node)."""
+
+    def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 10.0):
+        L = lib()
+        _bind(L)
+        self.L = L
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+        if self.world > 8:
+            raise ValueError("xGMI all-reduce supports up to 8 ranks (one node)")
+        self.max_bytes = int(max_bytes)
+        self._own = ctypes.c_void_p()
+        _check(L.k8s_ar_alloc(L.k8s_ar_buffer_bytes(self.max_bytes), ctypes.byref(self._own)), "k8s_ar_alloc")
+        hs = L.k8s_ar_handle_size()
+        h = ctypes.create_string_buffer(hs)
+        _check(L.k8s_ar_get_handle(self._own, h), "hipIpcGetMemHandle")
+        handles: List[Optional[bytes]] = [None] * self.world
+        dist.all_gather_object(handles, h.raw, group=group)
+        self._bases = (ctypes.c_void_p * self.world)()
+        self._opened = []
+        for r in range(self.world):
+            if r == self.rank:
+                self._bases[r] = self._own.value
+                continue
+            q = ctypes.c_void_p()
+            _check(L.k8s_ar_open_handle(handles[r], ctypes.byref(q)), "hipIpcOpenMemHandle")
+            self._opened.append(q)
+            self._bases[r] = q.value
+        self.id = L.k8s_ar_register(self.world, self.rank, self._bases, self.max_bytes, float(timeout_s))
+        if self.id < 0:
+            raise RuntimeError("k8s_ar_register failed")
+        torch.cuda.synchronize()
+        dist.barrier(group=group)
+
+    def mode_for(self, t: torch.Tensor) -> int:
+        """1 one-shot, 2 two-shot, 0 = not applicable (use RCCL)."""
+        nb = t.numel() * t.element_size()
+        if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() % 8 or nb > self.max_bytes:
+            return 0
+        return 1 if nb <= ONE_SHOT_MAX else 2
+
+    def __call__(self, t: torch.Tensor, mode: Optional[int] = None) -> torch.Tensor:
+        m = self.mode_for(t) if mode is None else mode
+        if m == 0:
+            raise ValueError("tensor not eligible for the xGMI all-reduce")
+        _check(self.L.k8s_ar_allreduce_bf16(self.id, t.data_ptr(), t.data_ptr(), t.numel(), m, stream_ptr(t)),
+               "k8s_ar_allreduce_bf16")
+        return t
+
+    def status(self) -> int:
+        v = ctypes.c_int(0)
+        _check(self.L.k8s_ar_status(self.id, ctypes.byref(v)), "k8s_ar_status")
+        return v.value
+
+    def close(self) -> None:
+        if self.id < 0:
+            return
+        torch.cuda.synchronize()
+        self.L.k8s_ar_unregister(self.id)
+        for q in self._opened:
+            self.L.k8s_ar_close_handle(q)
+        self.L.k8s_ar_free(self._own)
+        self.id = -1

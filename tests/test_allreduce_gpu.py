@@ -1,0 +1,65 @@
+"""Custom xGMI all-reduce (B14): IPC buffers, flag protocol, one-/two-shot.
+
+The box has one GPU, so the ranks are processes sharing cuda:0: the IPC
+export/open, the cross-process release/acquire flags and the parity double
+buffering are exercised for real; only the xGMI link itself is not.  Results
+must be bit-identical to a fixed-order fp32 sum rounded to bf16 on every rank.
+"""
+import os
+import socket
+import tempfile
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.gpu
+
+
+def _free_port() -> int:
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _inp(rank, n, it, mode):
+    g = torch.Generator().manual_seed(rank * 1_000_003 + n * 31 + it * 7 + mode)
+    return torch.randn(n, generator=g).bfloat16()
+
+
+def _worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.parallel.xgmi import XgmiAllReduce
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ar = XgmiAllReduce(dist.group.WORLD, max_bytes=4 << 20, timeout_s=20.0)
+    bad = []
+    for mode in (1, 2):
+        for n in (8, 4096, 65536 + 8 * 13, 1 << 20):
+            for it in range(6):  # > 2 epochs per block: exercises parity reuse
+                x = _inp(rank, n, it, mode).cuda()
+                ar(x, mode=mode)
+                ref = sum(_inp(r, n, it, mode).float() for r in range(world)).bfloat16()
+                if not torch.equal(x.cpu(), ref):
+                    bad.append((mode, n, it, (x.cpu().float() - ref.float()).abs().max().item()))
+    torch.cuda.synchronize()
+    status = ar.status()
+    ar.close()
+    torch.save({"bad": bad, "status": status}, os.path.join(out_dir, f"r{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_xgmi_allreduce_processes_sharing_one_gpu(world):
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_worker, args=(world, _free_port(), d), nprocs=world, join=True)
+        res = [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
+    for r, v in enumerate(res):
+        assert v["status"] == 0, f"rank {r}: a flag wait timed out"
+        assert not v["bad"], (r, v["bad"][:4])

@@ -1,7 +1,7 @@
 """MoE routing ops (B11/B12): top-k router, expert permutation, weighted combine."""
 from __future__ import annotations
 
-from typing import Tuple
+from typing import Optional, Tuple
 
 import torch
 
@@ -53,4 +53,35 @@ def combine(y_perm: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k:
         return out
     g = y_perm.float()[inv.long()].view(T, k, H)
     out.copy_((g * w.view(T, k, 1)).sum(1).to(out.dtype))
+    return out
+
+
+def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, fuse_silu: bool = False,
+                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """B13: rows offsets[e]..offsets[e+1] of ``a`` times ``w[e]^T`` for every
+    expert in one launch (``w`` [E, N, K]).  ``fuse_silu``: ``a`` is the
+    gate_up output [rows, 2K] and the activation silu(gate) * up is formed on
+    the fly.  Offsets stay on the device (no host sync)."""
+    E, N, K = w.shape
+    rows = a.shape[0]
+    if out is None:
+        out = torch.empty(rows, N, dtype=a.dtype, device=a.device)
+    if rows == 0:
+        return out
+    if use_hip(a) and N % 128 == 0 and K % 64 == 0:
+        assert a.dtype == torch.bfloat16 and w.is_contiguous() and a.stride(1) == 1 and out.is_contiguous()
+        assert a.shape[1] == (2 * K if fuse_silu else K)
+        max_tiles = (rows + 63) // 64 + E
+        check(lib().k8s_grouped_gemm(ptr(a), a.stride(0), ptr(w), ptr(out), out.stride(0), ptr(offsets), E, N, K,
+                                     max_tiles, int(fuse_silu), stream_ptr(a)), "grouped_gemm")
+        return out
+    offs = offsets.tolist()
+    for e in range(E):
+        lo, hi = offs[e], offs[e + 1]
+        if hi <= lo:
+            continue
+        x = a[lo:hi].float()
+        if fuse_silu:
+            x = torch.nn.functional.silu(x[:, :K]) * x[:, K:]
+        out[lo:hi] = (x @ w[e].float().t()).to(out.dtype)
     return out

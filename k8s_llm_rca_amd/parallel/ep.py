@@ -53,7 +53,7 @@ def ep_moe_forward(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids
     if recv_x.shape[0]:
         o2, inv2, offs = M.align(recv_e.view(-1, 1), moe.E_local)
         xs = recv_x.index_select(0, o2.long())
-        ys = moe.experts(li, xs, offs.tolist())
+        ys = moe.experts(li, xs, offs)
         out_recv = ys.index_select(0, inv2.long())
     back = y.new_empty((sum(sc), H))
     dist.all_to_all_single(back, out_recv.contiguous(), sc, rc, group=grp)

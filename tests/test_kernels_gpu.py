@@ -247,3 +247,22 @@ def test_gemm_skinny(M, N, K):
     y2 = LIN.linear(e, w)
     exp = torch.stack([w[:, (i * 37) % K] for i in range(e.shape[0])])
     torch.testing.assert_close(y2.float(), exp.float(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])
+@pytest.mark.parametrize("fuse", [False, True])
+def test_grouped_gemm_matches_per_expert(E, N, K, fuse):
+    """B13: one launch over all experts (device offsets, empty experts, ragged
+    64-row tiles) == per-expert fp32 GEMMs; fused SwiGLU operand load."""
+    from k8s_llm_rca_amd.ops import moe as MO
+    _need_gpu()
+    torch.manual_seed(5)
+    counts = torch.tensor([0, 70, 1, 130, 64, 0, 5, 200][:E])
+    offs = torch.zeros(E + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(counts, 0)
+    rows = int(offs[-1])
+    a = (torch.randn(rows, 2 * K if fuse else K) * 0.5).bfloat16()
+    w = (torch.randn(E, N, K) / K ** 0.5).bfloat16()
+    got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), fuse_silu=fuse).float().cpu()
+    ref = MO.grouped_gemm(a, w, offs, fuse_silu=fuse).float()
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)

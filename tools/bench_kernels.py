@@ -158,6 +158,34 @@ def main():
             tot_us += us
             fl += sum(sum(c - qq + j + 1 for j in range(qq)) for c, qq in zip(ctx, ql)) * nq * 128 * 4
         res[f"replay prefill {len(idx)} steps"] = f"{tot_us / len(idx):.1f}us/step {fl / tot_us / 1e6:.1f} TFLOP/s"
+    if args.what == "moe":
+        from k8s_llm_rca_amd.ops import moe as MO
+        E, H, I = 8, 4096, 14336
+        w13 = (torch.randn(E, 2 * I, H, device=dev) * 0.02).bfloat16()
+        w2 = (torch.randn(E, H, I, device=dev) * 0.02).bfloat16()
+        for rows in (16, 64, 256, 1024, 8192):
+            counts = torch.full((E,), rows // E)
+            counts[: rows % E] += 1
+            offs = torch.zeros(E + 1, dtype=torch.int32)
+            offs[1:] = torch.cumsum(counts, 0)
+            offs_d = offs.to(dev)
+            x = torch.randn(rows, H, device=dev).bfloat16()
+            gu = torch.randn(rows, 2 * I, device=dev).bfloat16()
+            o = offs.tolist()
+
+            def loop():
+                for e in range(E):
+                    if o[e + 1] > o[e]:
+                        g = torch.nn.functional.linear(x[o[e]:o[e + 1]], w13[e])
+                        torch.nn.functional.linear(g[:, :I], w2[e])
+
+            us_g = timeit(lambda: (MO.grouped_gemm(x, w13, offs_d), MO.grouped_gemm(gu, w2, offs_d, fuse_silu=True)),
+                          iters=10)
+            us_l = timeit(loop, iters=10)
+            wbytes = (w13.numel() + w2.numel()) * 2
+            fl = 2 * rows * 3 * I * H
+            res[f"moe rows{rows}"] = (f"grouped {us_g:.0f}us ({wbytes / us_g / 1e6:.2f} TB/s-w, "
+                                      f"{fl / us_g / 1e6:.0f} TF) | hipBLASLt loop {us_l:.0f}us")
     if args.what == "gemm_big":
         for M in (512, 1024, 2048, 4096, 8192):
             for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:

@@ -1,8 +1,11 @@
 // Masked sampling over the vocabulary (B9): greedy argmax or exact softmax
 // sampling via the Gumbel-max trick in ONE pass over the logits:
 //   tok = argmax_i  logit_i / T + G_i,   G_i = -log(-log(U_i)),
-// U_i from a counter-based hash of (seed, row, step, i) -> reproducible and
-// graph-capturable (the seed/step live in device memory).
+// U_i from a counter-based hash of (seed, step, i) -> reproducible and
+// graph-capturable (the seed/step live in device memory).  The per-request
+// seed already includes the sequence id, so the noise does not depend on the
+// row's position in the batch: a sequence samples the same tokens however the
+// scheduler batches it (sync or overlapped steps, any batch mix).
 // Constrained decoding masks (grammar states) come in two forms per row:
 //   * bitmap: mask_table[mask_id[row]] is a [V/32] uint32 allow-bitmap
 //   * list:   an explicit allow-list slice (list_off, list_len) of token ids
@@ -65,7 +68,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
       const int i = gi - vocab_off;
       if (i < 0 || i >= V) continue;
       float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, row, step, gi);
+      if (!greedy) v += gumbel(seed, 0u, step, gi);
       best = better(best, Best{v, gi});
     }
   } else {
@@ -82,7 +85,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
       for (int j = 0; j < 8; ++j) {
         if (!((bits >> j) & 1u)) continue;
         float v = bf2f(x[j]) * it;
-        if (!greedy) v += gumbel(seed, row, step, g0 + j);
+        if (!greedy) v += gumbel(seed, 0u, step, g0 + j);
         best = better(best, Best{v, g0 + j});
       }
     }
@@ -90,7 +93,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
       const int gi = vocab_off + i;
       if (mk && !((mk[gi >> 5] >> (gi & 31)) & 1u)) continue;
       float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, row, step, gi);
+      if (!greedy) v += gumbel(seed, 0u, step, gi);
       best = better(best, Best{v, gi});
     }
   }

@@ -46,6 +46,19 @@ from .tokenizer import get_tokenizer
 log = logging.getLogger(__name__)
 
 PART_MIN = min(A.DECODE_PARTS)  # smallest decode partition: sizes the split-KV buffers
+SPEC = -1  # placeholder token: "the token sampled by the in-flight step" (device-side until processed)
+
+
+class InFlight:
+    """A sampled step whose tokens have not been processed on the host yet."""
+    __slots__ = ("seqs", "tok", "tok_host", "event", "t0")
+
+    def __init__(self, seqs, tok, tok_host, event, t0):
+        self.seqs = seqs
+        self.tok = tok            # [B] int32 on the device (feeds the next forward)
+        self.tok_host = tok_host  # [B] int32 host copy (pinned on GPU), valid once `event` completes
+        self.event = event
+        self.t0 = t0
 
 
 @dataclass
@@ -61,6 +74,9 @@ class EngineConfig:
     max_decode_seqs: int = 256
     max_context: Optional[int] = None
     use_graphs: bool = True
+    # overlap the host's token processing of step n with the GPU's forward of
+    # step n+1 (decode inputs taken from the device-side sampled tokens)
+    async_steps: bool = True
     gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
@@ -157,6 +173,8 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
+        self._inflight: Optional[InFlight] = None
+        self._async = cfg.async_steps and self.pc.tp_size == 1
         # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
         self._dist_sample = (self.pc.tp_size > 1 and hasattr(self.model, "vocab_local")
                              and self.model.vocab_local % 8 == 0)
@@ -253,6 +271,20 @@ class LLMEngine:
             self._thread = None
 
     def _loop(self) -> None:
+        prof_path = os.environ.get("K8S_RCA_PROFILE_ENGINE")
+        if prof_path:  # cProfile of the engine thread only (host turnaround analysis)
+            import cProfile
+            pr = cProfile.Profile()
+            pr.enable()
+            try:
+                self._loop_inner()
+            finally:
+                pr.disable()
+                pr.dump_stats(prof_path)
+            return
+        self._loop_inner()
+
+    def _loop_inner(self) -> None:
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
         while True:
@@ -370,13 +402,27 @@ class LLMEngine:
                 return
 
     def step(self) -> bool:
+        """One engine step.  In async mode the sequences sampled by the previous
+        step (still in flight: their tokens are on the device only) join this
+        step as decode rows fed straight from the device tokens, and the host
+        processes those tokens while this step's forward runs on the GPU."""
         t_host0 = time.perf_counter()
         self._admit()
         self.stats["admit_s"] += time.perf_counter() - t_host0
         if self._releases:
             self._apply_releases()
+        infl = self._inflight
+        self._inflight = None
+        if infl is not None:
+            for s in infl.seqs:
+                s.tokens.append(SPEC)
         active = [s for s in self._snapshot() if s.req is not None and s.pending > 0]
         if not active:
+            if infl is not None:  # nothing else to run: just finish the in-flight step
+                for s in infl.seqs:
+                    s.tokens.pop()
+                self._process_tokens(infl)
+                return True
             return False
         BS = self.kv.block_size
         decode, prefill = [], []
@@ -388,8 +434,8 @@ class LLMEngine:
                     decode.append(s)
         budget -= len(decode)
         chunks: List[Tuple[Sequence, int]] = []
-        for s in sorted((s for s in active if s.pending > 1 or (s.pending == 1 and s not in decode)),
-                        key=lambda s: s.req.t_submit):
+        for s in sorted((s for s in active if (s.pending > 1 or (s.pending == 1 and s not in decode))
+                         and s.tokens[-1] != SPEC), key=lambda s: s.req.t_submit):
             if budget <= 0:
                 break
             q = min(s.pending, budget)
@@ -412,9 +458,18 @@ class LLMEngine:
             off += q
             if s.n_cached + q == len(s.tokens):
                 sample_rows.append((off - 1, s))
+        spec = None
+        if infl is not None:
+            pos_in = {s.id: j for j, s in enumerate(infl.seqs)}
+            src = np.array([pos_in.get(s.id, -1) if s.tokens[s.n_cached] == SPEC else -1 for s in decode],
+                           dtype=np.int32)
+            spec = (src, infl.tok)
         self.stats["host_s"] += time.perf_counter() - t_host0
-        logits = self._forward(decode, chunks, [i for i, _ in sample_rows])
+        logits = self._forward(decode, chunks, [i for i, _ in sample_rows], spec)
+        spec_pos = {}
         for s, q in rows:
+            if q == 1 and s.tokens[s.n_cached] == SPEC:
+                spec_pos[s.id] = s.n_cached
             s.n_cached += q
             s.last_used = time.perf_counter()
         self.stats["steps"] += 1
@@ -422,8 +477,24 @@ class LLMEngine:
         self.stats["decode_tokens"] += len(decode)
         self.stats["decode_ctx_tokens"] += sum(s.n_cached for s in decode)
         self.stats["prefill_ctx_tokens"] += sum(s.n_cached * q for s, q in chunks)
-        if sample_rows:
-            self._sample_and_advance(logits, [s for _, s in sample_rows])
+        if infl is not None:
+            # host side of the previous step, overlapped with this step's forward
+            toks = self._process_tokens(infl, placeholders=True)
+            for s, t in zip(infl.seqs, toks):
+                p = spec_pos.get(s.id)
+                if p is not None and (len(s.tokens) <= p or s.tokens[p] != t):
+                    s.n_cached = p  # the speculative KV at p is not this sequence's token (it finished)
+        # rows still waiting for a sample (a finished or newly-forced sequence is not)
+        keep = [(i, s) for i, (ri, s) in enumerate(sample_rows)
+                if s.req is not None and s.n_cached == len(s.tokens)]
+        if keep:
+            if len(keep) != len(sample_rows):
+                logits = logits.index_select(0, torch.tensor([i for i, _ in keep], device=logits.device))
+            fl = self._launch_sample(logits, [s for _, s in keep])
+            if self._async:
+                self._inflight = fl
+            else:
+                self._process_tokens(fl)
         return True
 
     # ------------------------------------------------------------- forward
@@ -453,7 +524,11 @@ class LLMEngine:
         return (np.asarray(ids, dtype=np.int32), np.concatenate(pos).astype(np.int32),
                 np.concatenate(slots).astype(np.int32))
 
-    def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int]):
+    def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int],
+                 spec=None):
+        """``spec`` = (src[nd], tok): decode row i takes its input id from the
+        device tensor ``tok[src[i]]`` when ``src[i] >= 0`` (tokens sampled by
+        the in-flight step, not yet on the host)."""
         t0 = time.perf_counter()
         timed = self._step_timing and self.device.type == "cuda"
         if timed:
@@ -461,12 +536,12 @@ class LLMEngine:
             ev[0].record()
         if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1
                 and self.kv.block_size % 64 == 0):
-            out = self._forward_graph(decode)
+            out = self._forward_graph(decode, spec)
             self.stats["graph_steps"] += 1
             self.stats["decode_steps"] += 1
             kind = "graph"
         else:
-            out = self._forward_eager(decode, chunks, sample_idx)
+            out = self._forward_eager(decode, chunks, sample_idx, spec)
             if not chunks:
                 self.stats["decode_steps"] += 1
             kind = "eager"
@@ -535,7 +610,8 @@ class LLMEngine:
                            len(sample_idx), n_parts, n_merge, part, n_items], dtype=np.int64)
         return header, flat
 
-    def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor):
+    def _exec_step(self, header: np.ndarray, flat_host: Optional[np.ndarray], flat_dev: torch.Tensor,
+                   spec=None):
         """Build StepInputs from the wire format and run the forward (every TP rank)."""
         from ..models.llama import StepInputs
 
@@ -553,6 +629,9 @@ class LLMEngine:
             return d, h
 
         d_ids, _ = take(T)
+        if spec is not None:
+            d_ids = d_ids.clone()
+            self._apply_spec(d_ids, spec[0], spec[1])
         d_pos, _ = take(T)
         d_slots, _ = take(T)
         d_sidx, _ = take(ns)
@@ -649,15 +728,28 @@ class LLMEngine:
     def _comm_device(self):
         return self.device if self.device.type == "cuda" else torch.device("cpu")
 
-    def _forward_eager(self, decode, chunks, sample_idx):
+    def _forward_eager(self, decode, chunks, sample_idx, spec=None):
         header, flat = self._pack_step(decode, chunks, sample_idx)
         if self.pc.tp_size > 1:
+            assert spec is None, "async steps are single-rank"
             h = torch.from_numpy(header).to(self._comm_device())
             self._bcast(h)
-        dev = self._to_dev([flat])[0]
+        if spec is not None:
+            dev, src = self._to_dev([flat, spec[0]])
+            spec = (src, spec[1])
+        else:
+            dev = self._to_dev([flat])[0]
         if self.pc.tp_size > 1:
             self._bcast(dev)
-        return self._exec_step(header, flat, dev)
+        return self._exec_step(header, flat, dev, spec)
+
+    @staticmethod
+    def _apply_spec(ids: torch.Tensor, src: torch.Tensor, tok: torch.Tensor) -> None:
+        """ids[i] = tok[src[i]] where src[i] >= 0 (device-side, stream-ordered
+        after the sampling kernel that produced ``tok``)."""
+        n = src.shape[0]
+        pick = tok.index_select(0, src.clamp(min=0).long()).clamp(min=0).to(ids.dtype)
+        ids[:n] = torch.where(src >= 0, pick, ids[:n])
 
     def serve_worker(self) -> None:
         """TP ranks > 0: replay every step rank 0 schedules until it sends STOP."""
@@ -720,7 +812,7 @@ class LLMEngine:
             "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
             "items": torch.zeros(Bmax * npmax, 4, dtype=torch.int32, device=dev),
             "n_items": torch.zeros(1, dtype=torch.int32, device=dev),
-            "host": torch.zeros(Bmax * (3 + mb + 1) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory(),
+            "host": torch.zeros(Bmax * (3 + mb + 2) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory(),
         }
         self._static = st
         return st
@@ -760,7 +852,7 @@ class LLMEngine:
         self.stats["capture_s"] += time.perf_counter() - t0
         return self._graphs[key]
 
-    def _forward_graph(self, decode: List[Sequence]):
+    def _forward_graph(self, decode: List[Sequence], spec=None):
         st = self._ensure_static()
         B = len(decode)
         Bb = self._bucket(B)
@@ -797,6 +889,10 @@ class LLMEngine:
         hv[o] = n_items
         hv[o + 1:o + 1 + n_items * 4] = items.reshape(-1)
         n = o + 1 + n_items * 4
+        if spec is not None:
+            hv[n:n + B] = spec[0]
+            n_src = n
+            n += B
         dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
         dev_flat.copy_(host[:n], non_blocking=True)
         st["ids"][:Bb].copy_(dev_flat[0:Bb])
@@ -805,7 +901,9 @@ class LLMEngine:
         st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
         st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
         st["n_items"].copy_(dev_flat[o:o + 1])
-        st["items"][:n_items].copy_(dev_flat[o + 1:n].view(n_items, 4))
+        st["items"][:n_items].copy_(dev_flat[o + 1:o + 1 + n_items * 4].view(n_items, 4))
+        if spec is not None:
+            self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], spec[1])
         graph, out = self._capture(Bb, part)
         graph.replay()
         return out[:B]
@@ -818,7 +916,9 @@ class LLMEngine:
             self._mask_ver = self.grt.masks.version
         return self._mask_dev
 
-    def _sample_and_advance(self, logits: torch.Tensor, seqs: List[Sequence]) -> None:
+    def _launch_sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> InFlight:
+        """Launch masked sampling for ``seqs`` (rows of ``logits``) and an async
+        device -> host copy of the tokens; nothing waits here."""
         t0 = time.perf_counter()
         B = len(seqs)
         mask_id = np.full(B, -1, dtype=np.int32)
@@ -852,14 +952,32 @@ class LLMEngine:
             d_temps = ints[6].view(torch.float32)
             tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
                              vocab=self.vocab)
+        if tok.is_cuda:
+            host = torch.empty(B, dtype=torch.int32, pin_memory=True)
+            host.copy_(tok, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record()
+        else:
+            host, ev = tok, None
+        self.stats["sample_s"] += time.perf_counter() - t0
+        return InFlight(seqs, tok, host, ev, t0)
+
+    def _process_tokens(self, fl: InFlight, placeholders: bool = False) -> List[int]:
+        """Host side of a sampled step: wait for its tokens (not for later GPU
+        work), append them, advance grammars, jump-forward, finish requests.
+        ``placeholders``: the sequences carry a SPEC token that the sampled
+        token replaces."""
         t1 = time.perf_counter()
-        toks = tok.tolist()
+        if fl.event is not None:
+            fl.event.synchronize()
+        toks = fl.tok_host.tolist()
         now = time.perf_counter()
         if self._pending_ev:
             self._collect_timing()
         self.stats["wait_s"] += now - t1
-        self.stats["sample_s"] += now - t0
-        for s, t in zip(seqs, toks):
+        for s, t in zip(fl.seqs, toks):
+            if placeholders and s.tokens and s.tokens[-1] == SPEC:
+                s.tokens.pop()
             r = s.req
             if r.t_first is None:
                 r.t_first = now
@@ -878,3 +996,4 @@ class LLMEngine:
             r.gs.advance(t)
             self._drive(r)
         self.stats["post_s"] += time.perf_counter() - now
+        return toks

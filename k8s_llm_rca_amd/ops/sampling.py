@@ -103,7 +103,7 @@ def _sample_ref(logits, temperature, seeds, steps, mask_id, mask_table, list_off
             continue
         v = lg[cand]
         if temp > 0:
-            v = v / temp + gumbel_ref(int(seeds[b]), b, int(steps[b]), cand + vocab_off)
+            v = v / temp + gumbel_ref(int(seeds[b]), 0, int(steps[b]), cand + vocab_off)
         best = torch.max(v)
         tok = int(cand[torch.nonzero(v == best).flatten()[0]]) + vocab_off
         if pairs:

@@ -198,3 +198,33 @@ def test_concurrent_clients_race_stress():
     assert not errors and eng.error is None, (errors, eng.error)
     assert len(done) == 48
     assert not eng.seqs and eng.kv.free_blocks == free0
+
+
+@pytest.mark.parametrize("temperature", [0.0, 0.8])
+def test_async_steps_match_sync(temperature):
+    """Overlapped steps (decode inputs fed from the in-flight device tokens,
+    host processing of step n during forward n+1) generate exactly what the
+    synchronous engine generates, including grammar jump-forward and finishes."""
+    outs = []
+    for async_steps in (False, True):
+        eng = _engine(temperature=temperature, async_steps=async_steps, num_blocks=128)
+        res = {}
+        for i in range(6):
+            sid = eng.new_sequence()
+            g = None
+            if i % 2:
+                g = Grammar([Lit('{"k": '), Choice(['"aa"', '"b"', '"cccc"'], "c"), Lit(', "t": "'),
+                             Free(5 + i, name="t"), Lit('"}')])
+            p = eng.tok.system_prefix("s") + eng.tok.message("user", "req %d " % i * (3 + 4 * i)) + \
+                eng.tok.header("assistant")
+            eng.submit(sid, p, g, 6 + 3 * i, seed=11, on_done=lambda gen, st, i=i: res.__setitem__(i, gen))
+        eng.run_until_idle()
+        # a second run on the same threads reuses their (possibly speculative-trimmed) KV
+        for i, sid in enumerate(list(eng.seqs)):
+            s = eng.seqs[sid]
+            eng.submit(sid, s.tokens + eng.tok.message("user", "more %d" % i) + eng.tok.header("assistant"),
+                       None, 5, seed=12, on_done=lambda gen, st, i=i: res.__setitem__(100 + i, gen))
+        eng.run_until_idle()
+        assert len(res) == 12
+        outs.append(res)
+    assert outs[0] == outs[1]

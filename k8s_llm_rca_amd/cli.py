@@ -10,6 +10,9 @@
 * ``locate``     stage 1 only: srcKind + locator + metapaths (``test_find_metapath.py``)
 * ``query``      stage 2 only for one metapath string (``test_generate_query.py``)
 * ``state``      stage 3 only for one entity (``test_check_state.py``)
+* ``serve``      OpenAI-Assistants-shaped REST API over the engine (api/http.py);
+                 ``run --server URL`` drives a remote server instead of an
+                 in-process engine
 
 Backends: ``engine`` (MI355X LLM engine, default), ``opt-cpu`` (OPT-125m
 plumbing backend on CPU, BASELINE config 1) and ``oracle`` (scripted replies
@@ -119,7 +122,11 @@ def cmd_run(args) -> int:
         if torch.cuda.is_available():
             from .graph.device import to_device
             to_device(state, "cuda")
-    svc, eng = _service(args)
+    if args.server:
+        from .api.http import RemoteAssistantService
+        svc, eng = RemoteAssistantService(args.server), None
+    else:
+        svc, eng = _service(args)
     cfg = RCAConfig(model=args.model, hints=args.hints, budget=_budget(args))
     meta_qe, state_qe = GraphQueryExecutor(meta), GraphQueryExecutor(state)
     t0 = time.time()
@@ -131,7 +138,7 @@ def cmd_run(args) -> int:
     summary = {"analyses": len(st.results), "wall_s": round(wall, 2), "analyses_per_s": round(st.analyses_per_s, 3),
                "p50_latency_s": round(st.pct(0.5), 3), "p90_latency_s": round(st.pct(0.9), 3),
                "errors": len(st.errors), "output": args.output}
-    if args.state_out:
+    if args.state_out and hasattr(svc, "export_state"):
         with open(args.state_out, "w") as f:
             json.dump(svc.export_state(), f)
     print(json.dumps(summary))
@@ -204,6 +211,18 @@ def cmd_state(args) -> int:
     return 0
 
 
+def cmd_serve(args) -> int:
+    import uvicorn
+    from .api.http import create_app
+    svc, eng = _service(args)
+    try:
+        uvicorn.run(create_app(svc, eng), host=args.host, port=args.port, log_level="warning")
+    finally:
+        if eng is not None:
+            eng.stop()
+    return 0
+
+
 def main(argv: Optional[List[str]] = None) -> int:
     p = argparse.ArgumentParser(prog="k8s_llm_rca_amd", description=__doc__,
                                 formatter_class=argparse.RawDescriptionHelpFormatter)
@@ -234,6 +253,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     sp.add_argument("--concurrency", type=int, default=1)
     sp.add_argument("--device-graph", action="store_true", help="mirror the stategraph to HBM")
     sp.add_argument("--state-out", default=None, help="save assistants/threads JSON for resume")
+    sp.add_argument("--server", default=None, help="base URL of a `serve` instance (remote engine)")
     sp.set_defaults(fn=cmd_run)
     sp = sub.add_parser("locate")
     common(sp)
@@ -251,6 +271,11 @@ def main(argv: Optional[List[str]] = None) -> int:
     sp.add_argument("--timestamp", required=True)
     sp.add_argument("--message", default=None)
     sp.set_defaults(fn=cmd_state)
+    sp = sub.add_parser("serve")
+    common(sp)
+    sp.add_argument("--host", default="127.0.0.1")
+    sp.add_argument("--port", type=int, default=8000)
+    sp.set_defaults(fn=cmd_serve)
     args = p.parse_args(argv)
     logging.basicConfig(level=logging.INFO if args.verbose else logging.WARNING)
     return args.fn(args)

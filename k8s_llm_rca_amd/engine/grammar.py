@@ -120,3 +120,45 @@ def hinted_render(g: Grammar, fill: str = "ok") -> str:
         return int(h) if h is not None else r.min
 
     return render(g, choose, lambda f: fill, rep)
+
+
+# ---------------------------------------------------------------- JSON form
+# Grammars travel over the HTTP API as ``response_format = {"type":
+# "k8s_grammar", "grammar": grammar_to_json(g)}`` (api/http.py).
+
+def _seg_to_json(s: Seg) -> dict:
+    if isinstance(s, Lit):
+        return {"lit": s.text}
+    if isinstance(s, Choice):
+        return {"choice": list(s.options), "name": s.name}
+    if isinstance(s, Free):
+        return {"free": s.max_tokens, "forbid": s.forbid, "min": s.min_tokens, "name": s.name}
+    if isinstance(s, Repeat):
+        return {"repeat": [_seg_to_json(b) for b in s.body], "sep": s.sep, "close": s.close, "min": s.min,
+                "max": s.max, "name": s.name}
+    if isinstance(s, Ref):
+        return {"ref": s.name}
+    raise TypeError(f"not a grammar segment: {s!r}")
+
+
+def _seg_from_json(d: dict) -> Seg:
+    if "lit" in d:
+        return Lit(str(d["lit"]))
+    if "choice" in d:
+        return Choice([str(o) for o in d["choice"]], d.get("name"))
+    if "free" in d:
+        return Free(int(d["free"]), d.get("forbid", '"\n`\\{}'), int(d.get("min", 1)), d.get("name"))
+    if "repeat" in d:
+        return Repeat([_seg_from_json(b) for b in d["repeat"]], str(d["sep"]), str(d["close"]),
+                      int(d.get("min", 1)), int(d.get("max", 4)), d.get("name"))
+    if "ref" in d:
+        return Ref(str(d["ref"]))
+    raise ValueError(f"unknown grammar segment {d!r}")
+
+
+def grammar_to_json(g: Grammar) -> dict:
+    return {"segments": [_seg_to_json(s) for s in g.segments], "hints": dict(g.hints), "name": g.name}
+
+
+def grammar_from_json(d: dict) -> Grammar:
+    return Grammar([_seg_from_json(s) for s in d["segments"]], dict(d.get("hints") or {}), d.get("name", ""))

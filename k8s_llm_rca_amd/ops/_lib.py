@@ -75,7 +75,17 @@ def available() -> bool:
         return False
 
 
+_raw_stream = getattr(torch._C, "_cuda_getCurrentRawStream", None)
+
+
 def stream_ptr(t: torch.Tensor = None) -> int:
+    """Raw hipStream_t of the current stream on ``t``'s device.  The C fast
+    path skips the Stream object torch.cuda.current_stream() builds (~4 us a
+    call; an eager 8B forward issues ~350 kernels)."""
+    if _raw_stream is not None:
+        if t is not None and t.device.index is not None:
+            return _raw_stream(t.device.index)
+        return _raw_stream(torch.cuda.current_device())
     return torch.cuda.current_stream(t.device if t is not None else None).cuda_stream
 
 
@@ -90,7 +100,9 @@ def check(rc: int, name: str) -> None:
 
 def use_hip(*tensors) -> bool:
     """True when the op must run on the HIP kernels (device tensors)."""
-    dev = any(t is not None and t.is_cuda for t in tensors)
-    if dev:
-        lib()  # fail loudly when the native library is missing
-    return dev
+    for t in tensors:
+        if t is not None and t.is_cuda:
+            if _lib is None:
+                lib()  # fail loudly when the native library is missing
+            return True
+    return False

@@ -66,7 +66,8 @@ def _service(args):
     else:
         dev = "cuda" if torch.cuda.is_available() else "cpu"
         cfg = EngineConfig(model=args.model, device=dev, dtype=torch.bfloat16 if dev == "cuda" else torch.float32,
-                           kv_max_gb=args.kv_gb, num_blocks=None if dev == "cuda" else 1024)
+                           kv_max_gb=args.kv_gb, num_blocks=None if dev == "cuda" else 1024,
+                           weights=args.weights, tokenizer=args.tokenizer)
     eng = LLMEngine(cfg)
     eng.start()
     svc = AssistantService(EngineBackend(eng))
@@ -236,6 +237,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         sp.add_argument("--backend", choices=["engine", "opt-cpu", "oracle"], default="engine")
         sp.add_argument("--model", default="llama3-8b")
         sp.add_argument("--kv-gb", type=float, default=None)
+        sp.add_argument("--weights", default=None, help="HF checkpoint dir (config.json + *.safetensors)")
+        sp.add_argument("--tokenizer", default=None, help="tokenizer.json (default: the checkpoint's)")
         sp.add_argument("--hints", action=argparse.BooleanOptionalAction, default=True)
         sp.add_argument("--semantic-tokens", type=int, default=192)
         sp.add_argument("-v", "--verbose", action="store_true")

@@ -80,6 +80,8 @@ class EngineConfig:
     gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
+    weights: Optional[str] = None    # HF checkpoint dir (config.json + *.safetensors): real weights
+    tokenizer: Optional[str] = None  # tokenizer.json (default: the checkpoint's, else the built-in BPE)
     temperature: float = 0.7
     use_hints: bool = True
     model_overrides: dict = field(default_factory=dict)
@@ -135,12 +137,22 @@ class LLMEngine:
         self.cfg = cfg
         self.pc = pc or single()
         self.device = torch.device(cfg.device)
-        self.mc = get_config(cfg.model, **cfg.model_overrides)
-        self.max_context = cfg.max_context or self.mc.max_position
         t0 = time.perf_counter()
+        if cfg.weights and model is None:
+            from ..models.llama import LlamaModel
+            from ..models.weights import config_from_hf, load_safetensors
+            self.mc = config_from_hf(cfg.weights)
+            model = LlamaModel(self.mc, self.device, cfg.dtype, self.pc, init=False)
+            load_safetensors(model, cfg.weights)
+        else:
+            self.mc = get_config(cfg.model, **cfg.model_overrides)
+        self.max_context = cfg.max_context or self.mc.max_position
         self.model = model or _build_model(self.mc, self.device, cfg.dtype, self.pc, cfg.seed)
         self.t_model_init = time.perf_counter() - t0
-        self.tok = get_tokenizer()
+        tok_path = cfg.tokenizer
+        if tok_path is None and cfg.weights and os.path.exists(os.path.join(cfg.weights, "tokenizer.json")):
+            tok_path = os.path.join(cfg.weights, "tokenizer.json")
+        self.tok = get_tokenizer(tok_path) if tok_path else get_tokenizer()
         self.vocab = min(self.mc.vocab_size, max(self.tok.vocab_size, 1))
         self.grt = GrammarRuntime(self.tok, self.mc.vocab_size)
         self.eos_ids = [self.tok.eot_id, self.tok.eos_id]

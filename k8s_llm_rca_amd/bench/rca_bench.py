@@ -193,6 +193,7 @@ def run(args) -> Optional[Dict[str, Any]]:
 def parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description=__doc__)
     p.add_argument("--gpus", type=int, default=None, help="GPUs (= WORLD_SIZE under torchrun; default 1)")
+    p.add_argument("--preset", default=None, choices=sorted(PRESETS), help="a BASELINE.json config")
     p.add_argument("--steps", type=int, default=2)
     p.add_argument("--warmup", type=int, default=1)
     p.add_argument("--model", default="llama3-8b")
@@ -214,8 +215,29 @@ def parser() -> argparse.ArgumentParser:
     return p
 
 
+# One preset per BASELINE.json config; explicit flags override.
+PRESETS: Dict[str, Dict[str, Any]] = {
+    # "OPT-125m CPU backend, 10-node toy k8s dependency graph, single pod-crash RCA (plumbing, no GPU)"
+    "opt125m-cpu-toy": dict(model="opt-125m", device="cpu", graph_nodes=10, incidents=1),
+    # the headline: "RCA analyses/sec + p50 latency, Llama-3-8B backend, 10k-node graph"
+    "llama3-8b-10k": dict(model="llama3-8b", graph_nodes=10_000),
+    # "Llama-3-8B TP=1 bf16 on one MI355X, 1k-node synthetic k8s graph"
+    "llama3-8b-1k": dict(model="llama3-8b", graph_nodes=1_000),
+    # "Llama-3-8B TP=1, 100k-node synthetic graph (HIP CSR metapath BFS stress)"
+    "llama3-8b-100k": dict(model="llama3-8b", graph_nodes=100_000, graph_device=True),
+    # "Llama-3-70B TP=8 over xGMI, 10k-node graph, batched multi-incident RCA" (torchrun --nproc-per-node 8)
+    "llama3-70b-tp8-10k": dict(model="llama3-70b", tp=8, graph_nodes=10_000),
+    # "Mixtral 8x7B MoE backend (grouped GEMM + expert all-to-all over xGMI), 10k-node graph"
+    "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000),
+}
+
+
 def main(argv=None) -> int:
-    args = parser().parse_args(argv)
+    p = parser()
+    pre, _ = p.parse_known_args(argv)
+    if pre.preset:
+        p.set_defaults(**PRESETS[pre.preset])
+    args = p.parse_args(argv)
     res = run(args)
     if res is not None:
         print(json.dumps(res), flush=True)

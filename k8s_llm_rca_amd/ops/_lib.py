@@ -93,9 +93,20 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
+_SYNC_DEBUG = os.environ.get("K8S_RCA_SYNC_DEBUG") == "1"
+
+
 def check(rc: int, name: str) -> None:
+    """Raise on a launch error.  ``K8S_RCA_SYNC_DEBUG=1`` (SURVEY.md §5.2 debug
+    mode) also synchronises after every kernel so an asynchronous fault is
+    reported at the op that caused it, not at a later sync."""
     if rc != 0:
         raise RuntimeError(f"{name} failed with hipError {rc}")
+    if _SYNC_DEBUG and torch.cuda.is_available():
+        try:
+            torch.cuda.synchronize()
+        except RuntimeError as e:
+            raise RuntimeError(f"{name}: device fault surfaced at sync: {e}") from e
 
 
 def use_hip(*tensors) -> bool:

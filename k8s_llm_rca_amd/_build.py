@@ -46,8 +46,9 @@ def build_graphcore(force: bool = False) -> str:
     import pybind11
 
     src = os.path.join(CSRC, "graph", "graphcore.cpp")
+    hdr = os.path.join(CSRC, "graph", "graphcore_core.h")
     out = graphcore_path()
-    if force or _newer(out, [src]):
+    if force or _newer(out, [src, hdr]):
         inc = sysconfig.get_paths()["include"]
         tmp = out + ".tmp"
         _run(["g++", "-O3", "-std=c++17", "-shared", "-fPIC", "-fvisibility=hidden",
@@ -110,3 +111,13 @@ def build_all(force: bool = False) -> None:
 if __name__ == "__main__":
     build_all(force="--force" in sys.argv)
     print("built", graphcore_path(), hip_lib_path())
+
+
+def build_graphcore_sanitized(out_dir: str) -> str:
+    """Standalone test driver of the graph core under ASan + UBSan (host only;
+    SURVEY.md §5.2).  Returns the executable path."""
+    src = os.path.join(CSRC, "graph", "graphcore_test.cpp")
+    exe = os.path.join(out_dir, "graphcore_test_asan")
+    _run(["g++", "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+          "-fno-sanitize-recover=undefined", "-I", os.path.join(CSRC, "graph"), src, "-o", exe])
+    return exe

@@ -10,6 +10,7 @@
 * ``locate``     stage 1 only: srcKind + locator + metapaths (``test_find_metapath.py``)
 * ``query``      stage 2 only for one metapath string (``test_generate_query.py``)
 * ``state``      stage 3 only for one entity (``test_check_state.py``)
+* ``token-probe`` token accounting over two runs (``test_token.py``)
 * ``serve``      OpenAI-Assistants-shaped REST API over the engine (api/http.py);
                  ``run --server URL`` drives a remote server instead of an
                  in-process engine
@@ -212,6 +213,33 @@ def cmd_state(args) -> int:
     return 0
 
 
+def cmd_token_probe(args) -> int:
+    """The reference's token-accounting probe (test_token.py:1-49): a tutor
+    assistant, two messages with a run each, then get_token_usage over the
+    window.  The reference sleeps 60 s per run and uses int() second bounds;
+    here each run is awaited and the window is taken in float seconds, so the
+    usage of fast runs is not lost."""
+    from .api.assistant import GenericAssistant
+    svc, eng = _service(args)
+    tutor = GenericAssistant(svc)
+    tutor.create_assistant("You are a personal math tutor. When asked a question, write and run Python code to "
+                           "answer the question.", "math-tutor-2", args.model)
+    tutor.create_thread()
+    print(tutor.assistant.id)
+    print(tutor.thread.id)
+    start = time.time()
+    for m in ("what is the area of a circle with diameter 4", "what is the result for x in 'x + 3 = 15'?"):
+        tutor.add_message(m)
+        tutor.run_assistant(max_tokens=args.max_tokens)
+        print("run assistant ...")
+        tutor.wait_get_last_k_message(1)
+    usage = tutor.get_token_usage(start, time.time() + 1e-3, 5)
+    print(json.dumps(usage))
+    if eng is not None:
+        eng.stop()
+    return 0
+
+
 def cmd_serve(args) -> int:
     import uvicorn
     from .api.http import create_app
@@ -274,6 +302,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     sp.add_argument("--timestamp", required=True)
     sp.add_argument("--message", default=None)
     sp.set_defaults(fn=cmd_state)
+    sp = sub.add_parser("token-probe")
+    common(sp)
+    sp.add_argument("--max-tokens", type=int, default=32)
+    sp.set_defaults(fn=cmd_token_probe)
     sp = sub.add_parser("serve")
     common(sp)
     sp.add_argument("--host", default="127.0.0.1")

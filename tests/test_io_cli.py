@@ -49,3 +49,11 @@ def test_service_state_roundtrip():
     assert svc2.retrieve_assistant(a.id).instructions == "ins"
     msgs = svc2.list_messages(t.id, order="asc").data
     assert [m.role for m in msgs] == ["user", "assistant"] and msgs[1].text == "reply"
+
+
+def test_cli_token_probe(capsys):
+    import json as _json
+    from k8s_llm_rca_amd.cli import main
+    assert main(["token-probe", "--backend", "oracle", "--graph-nodes", "100"]) == 0
+    usage = _json.loads(capsys.readouterr().out.strip().splitlines()[-1])
+    assert usage["total_tokens"] == usage["prompt_tokens"] + usage["completion_tokens"] > 0

@@ -565,11 +565,16 @@ class LLMEngine:
         return out
 
     def _collect_timing(self) -> None:
-        """Fold finished step events into stats (called after the step's sync)."""
+        """Fold completed step events into stats (with overlapped steps the
+        newest forward may still be running: its events stay pending)."""
+        keep = []
         for kind, dt, (e0, e1) in self._pending_ev:
+            if not e1.query():
+                keep.append((kind, dt, (e0, e1)))
+                continue
             self.stats[kind + "_issue_s"] += dt
             self.stats[kind + "_gpu_s"] += e0.elapsed_time(e1) / 1e3
-        self._pending_ev = []
+        self._pending_ev = keep
 
     def _to_dev(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
         """One H2D copy for all int32 metadata arrays."""

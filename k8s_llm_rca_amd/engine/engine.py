@@ -185,7 +185,7 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
-        self._inflight: Optional[InFlight] = None
+        self._pending_sample = None  # (logits, seqs, rows): sampled at the start of the next step
         self._async = cfg.async_steps and self.pc.tp_size == 1
         # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
         self._dist_sample = (self.pc.tp_size > 1 and hasattr(self.model, "vocab_local")
@@ -313,6 +313,7 @@ class LLMEngine:
                 self._fail_all(repr(e))
 
     def _fail_all(self, err: str) -> None:
+        self._pending_sample = None
         for s in self._snapshot():
             r = s.req
             if r is not None:
@@ -423,17 +424,21 @@ class LLMEngine:
         self.stats["admit_s"] += time.perf_counter() - t_host0
         if self._releases:
             self._apply_releases()
-        infl = self._inflight
-        self._inflight = None
-        if infl is not None:
-            for s in infl.seqs:
+        # The previous forward's sampling is launched only now, AFTER this
+        # step is scheduled, so sample(k) and forward(k+1) reach the GPU back
+        # to back while it is still busy with forward(k): the host's
+        # scheduling never leaves the GPU idle.
+        ps = self._pending_sample
+        self._pending_sample = None
+        if ps is not None:
+            for s in ps[1]:
                 s.tokens.append(SPEC)
         active = [s for s in self._snapshot() if s.req is not None and s.pending > 0]
         if not active:
-            if infl is not None:  # nothing else to run: just finish the in-flight step
-                for s in infl.seqs:
+            if ps is not None:  # nothing else to run: just finish the pending sample
+                for s in ps[1]:
                     s.tokens.pop()
-                self._process_tokens(infl)
+                self._process_tokens(self._launch_sample(*ps))
                 return True
             return False
         BS = self.kv.block_size
@@ -470,6 +475,7 @@ class LLMEngine:
             off += q
             if s.n_cached + q == len(s.tokens):
                 sample_rows.append((off - 1, s))
+        infl = self._launch_sample(*ps) if ps is not None else None
         spec = None
         if infl is not None:
             pos_in = {s.id: j for j, s in enumerate(infl.seqs)}
@@ -500,13 +506,12 @@ class LLMEngine:
         keep = [(i, s) for i, (ri, s) in enumerate(sample_rows)
                 if s.req is not None and s.n_cached == len(s.tokens)]
         if keep:
-            if len(keep) != len(sample_rows):
-                logits = logits.index_select(0, torch.tensor([i for i, _ in keep], device=logits.device))
-            fl = self._launch_sample(logits, [s for _, s in keep])
+            rows_sel = [i for i, _ in keep] if len(keep) != len(sample_rows) else None
+            pend = (logits, [s for _, s in keep], rows_sel)
             if self._async:
-                self._inflight = fl
+                self._pending_sample = pend
             else:
-                self._process_tokens(fl)
+                self._process_tokens(self._launch_sample(*pend))
         return True
 
     # ------------------------------------------------------------- forward
@@ -929,13 +934,17 @@ class LLMEngine:
     def _mask_table(self) -> Optional[torch.Tensor]:
         if self._mask_ver != self.grt.masks.version:
             arr = self.grt.masks.array()
-            self._mask_dev = torch.from_numpy(arr).to(self.device)
+            host = torch.from_numpy(arr)
+            if self.device.type == "cuda":  # pinned + non-blocking: a pageable copy would wait for the GPU
+                host = host.pin_memory()
+            self._mask_dev = host.to(self.device, non_blocking=True)
             self._mask_ver = self.grt.masks.version
         return self._mask_dev
 
-    def _launch_sample(self, logits: torch.Tensor, seqs: List[Sequence]) -> InFlight:
-        """Launch masked sampling for ``seqs`` (rows of ``logits``) and an async
-        device -> host copy of the tokens; nothing waits here."""
+    def _launch_sample(self, logits: torch.Tensor, seqs: List[Sequence], rows: Optional[List[int]] = None) -> InFlight:
+        """Launch masked sampling for ``seqs`` (rows ``rows`` of ``logits``, all
+        rows when None) and an async device -> host copy of the tokens; nothing
+        waits here (every upload is pinned + non-blocking)."""
         t0 = time.perf_counter()
         B = len(seqs)
         mask_id = np.full(B, -1, dtype=np.int32)
@@ -960,12 +969,18 @@ class LLMEngine:
         if not lists:
             lists = [0]
         if self._dist_sample:
+            if rows is not None:
+                logits = logits.index_select(0, torch.tensor(rows, device=logits.device))
             tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
                                   seeds, steps, temps)
         else:
             table = self._mask_table()
-            ints = self._to_dev([mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps,
-                                 temps.view(np.int32)])
+            arrays = [mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps, temps.view(np.int32)]
+            if rows is not None:
+                arrays.append(np.asarray(rows, np.int32))
+            ints = self._to_dev(arrays)
+            if rows is not None:
+                logits = logits.index_select(0, ints[7])
             d_temps = ints[6].view(torch.float32)
             tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
                              vocab=self.vocab)

@@ -170,16 +170,14 @@ class LlamaModel:
             if inp.meta_prefill is not None and nd < T:
                 A.paged_attention(qkv[nd:], k_cache[li], v_cache[li], inp.meta_prefill, self.nq, self.nkv,
                                   self.scale, out=attn[nd:])
-            o = linear(attn, L["wo"])
-            self.pc.all_reduce(o)
+            o = self.pc.linear_all_reduce(attn, L["wo"], linear_fn=linear)
             N.rmsnorm(o, L["post_norm"], cfg.rms_eps, residual=residual, out=y)
             if self.moe is not None:
                 prev = self.moe.forward(li, y)
             else:
                 gu = linear(y, L["w_gu"])
                 act = N.silu_mul(gu)
-                prev = linear(act, L["w_down"])
-                self.pc.all_reduce(prev)
+                prev = self.pc.linear_all_reduce(act, L["w_down"], linear_fn=linear)
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
         logits = linear(sel, self.lm_head)

@@ -26,6 +26,8 @@ class ParallelContext:
     ep_group: Optional[object] = None
     comm_stream: Optional[object] = None  # HIP stream for overlapped collectives
     custom_ar: Optional[object] = None    # parallel.xgmi.XgmiAllReduce for small TP messages
+    ar_chunks: int = 4                    # GEMM / all-reduce pipeline depth (linear_all_reduce)
+    overlap_min_bytes: int = 256 << 10    # below this an all-reduce is latency-bound: no chunking
 
     @property
     def is_tp(self) -> bool:
@@ -38,6 +40,64 @@ class ParallelContext:
                 return car(t)
             dist.all_reduce(t, group=self.tp_group)
         return t
+
+    def _all_reduce_async(self, t: torch.Tensor):
+        """Start an all-reduce of ``t`` that overlaps later work on the compute
+        stream; returns a handle whose ``wait()`` orders the compute stream
+        after it."""
+        car = self.custom_ar
+        if car is not None and t.is_cuda and car.mode_for(t):
+            cur = torch.cuda.current_stream(t.device)
+            if self.comm_stream is None:
+                self.comm_stream = torch.cuda.Stream(t.device)
+            s = self.comm_stream
+            s.wait_stream(cur)
+            with torch.cuda.stream(s):
+                car(t)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            t.record_stream(s)
+
+            class _W:
+                def wait(self_inner):
+                    cur.wait_event(ev)
+            return _W()
+        return dist.all_reduce(t, group=self.tp_group, async_op=True)
+
+    def linear_all_reduce(self, x: torch.Tensor, w: torch.Tensor, linear_fn=None) -> torch.Tensor:
+        """Row-parallel projection ``all_reduce(x @ w^T)`` with the reduction of
+        chunk i overlapped with the GEMM of chunk i+1 (RCCL / the xGMI kernel
+        run on their own streams).  Decode-sized M splits the OUTPUT COLUMNS
+        (each chunk streams a disjoint weight slice: no weight byte is read
+        twice); prefill-sized M splits the rows (contiguous, no copies)."""
+        import torch.nn.functional as F
+        lin = linear_fn or F.linear
+        if self.tp_size == 1:
+            return lin(x, w)
+        M, N = x.shape[0], w.shape[0]
+        k = self.ar_chunks
+        if k <= 1 or M * N * x.element_size() < self.overlap_min_bytes * k:
+            return self.all_reduce(lin(x, w))
+        works, parts = [], []
+        if M <= 256:
+            step = -(-N // k)
+            step = -(-step // 8) * 8
+            for a in range(0, N, step):
+                y = lin(x, w[a:a + step]).contiguous()
+                works.append(self._all_reduce_async(y))
+                parts.append(y)
+            for h in works:
+                h.wait()
+            return torch.cat(parts, dim=1)
+        out = torch.empty(M, N, dtype=x.dtype, device=x.device)
+        step = -(-M // k)
+        for a in range(0, M, step):
+            y = out[a:a + step]
+            torch.matmul(x[a:a + step], w.t(), out=y)  # prefill-sized: library GEMM straight into the slice
+            works.append(self._all_reduce_async(y))
+        for h in works:
+            h.wait()
+        return out
 
     def all_gather_last(self, t: torch.Tensor) -> torch.Tensor:
         """[n, v_local] on every rank -> [n, v_local * tp] (rank-major)."""

@@ -145,3 +145,33 @@ def test_tp2_distributed_sampling_with_grammar_matches_tp1():
         a = torch.load(o2, weights_only=True)
         b = torch.load(o1, weights_only=True)
     assert a == b and len(a) == 3
+
+
+def _run_overlap(rank, world, port, out_path):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, ar_chunks=3, overlap_min_bytes=64)
+    g = torch.Generator().manual_seed(100 + rank)
+    res = {}
+    for M, N, K in ((7, 300, 64), (40, 64, 32), (600, 96, 48)):  # column path (M <= 256) and row path
+        x = torch.randn(M, K, generator=g)
+        w = torch.randn(N, K, generator=g)
+        got = pc.linear_all_reduce(x, w)
+        want = x @ w.t()
+        dist.all_reduce(want)
+        res[(M, N)] = (got - want).abs().max().item()
+    if rank == 0:
+        torch.save(res, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_linear_all_reduce_overlap_chunks_exact():
+    """Chunked GEMM + async all-reduce pipeline == GEMM then all-reduce."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_run_overlap, args=(2, _free_port(), out), nprocs=2, join=True)
+        res = torch.load(out, weights_only=True)
+    assert all(v < 1e-4 for v in res.values()), res

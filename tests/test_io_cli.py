@@ -1,4 +1,5 @@
 """Graph persistence, CLI drivers and assistant-service state round trips."""
+import pytest
 import json
 import os
 
@@ -57,3 +58,30 @@ def test_cli_token_probe(capsys):
     assert main(["token-probe", "--backend", "oracle", "--graph-nodes", "100"]) == 0
     usage = _json.loads(capsys.readouterr().out.strip().splitlines()[-1])
     assert usage["total_tokens"] == usage["prompt_tokens"] + usage["completion_tokens"] > 0
+
+
+@pytest.mark.slow
+def test_bench_dp2_torchrun_cpu_contract(tmp_path):
+    """The driver's multi-GPU contract on CPU: torchrun, 2 ranks (gloo), one
+    JSON line from rank 0 with the whole-job aggregate."""
+    import json as _json
+    import os
+    import socket
+    import subprocess
+    import sys
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
+           "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
+           "--warmup", "0", "--device", "cpu", "--model", "tiny-llama", "--incidents", "2", "--graph-nodes", "200"]
+    env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = _json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["steps"] == 1 and d["config"]["parallelism"] == "dp2"
+    assert d["config"]["global_batch"] == 4 and d["value"] > 0 and d["errors"] == 0

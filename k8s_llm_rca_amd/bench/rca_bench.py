@@ -127,6 +127,8 @@ def run(args) -> Optional[Dict[str, Any]]:
         errors += st.errors
     tracing.reset()
     stats0 = dict(eng.stats)
+    eng.kv.reset_peak()
+    t_wall0 = time.time()
     sync_world = 1 if tp_mode else world
     _barrier(sync_world, device)
     t0 = time.perf_counter()
@@ -147,6 +149,8 @@ def run(args) -> Optional[Dict[str, Any]]:
     total = n_done * sync_world
     value = total / max_elapsed
     d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    ttft = sorted(rs.metrics["ttft_s"] for rs in list(svc.runs.values())
+                  if rs.run.created_at >= t_wall0 and "ttft_s" in rs.metrics)
     p50 = statistics.median(all_lat) if all_lat else 0.0
     p90 = sorted(all_lat)[int(0.9 * (len(all_lat) - 1))] if all_lat else 0.0
     res = {
@@ -181,6 +185,14 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "post_s": round(d["post_s"], 3), "admit_s": round(d["admit_s"], 3),
                    "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
                    **{k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}},
+        "throughput": {  # rank 0's engine over the timed window
+            "prefill_tok_per_s": round(d["prefill_tokens"] / elapsed, 1),
+            "decode_tok_per_s": round(d["decode_tokens"] / elapsed, 1),
+            "forced_tok_per_s": round(d["forced_tokens"] / elapsed, 1),
+            "avg_decode_batch": round(d["decode_tokens"] / max(1, d["steps"]), 1),
+            "runs": len(ttft),
+            "ttft_p50_s": round(ttft[len(ttft) // 2], 4) if ttft else None,
+            "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         "setup_s": round(setup_s, 1),
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }

@@ -26,6 +26,7 @@ class KVPool:
         self.k = torch.zeros(n_layers, num_blocks, n_kv, block_size, head_dim, dtype=dtype, device=device)
         self.v = torch.zeros(n_layers, num_blocks, n_kv, head_dim, block_size, dtype=dtype, device=device)
         self._free: List[int] = list(range(num_blocks - 1, -1, -1))
+        self.peak_used = 0
         self._lock = threading.Lock()
 
     @staticmethod
@@ -41,6 +42,7 @@ class KVPool:
             if n > len(self._free):
                 raise MemoryError(f"KV pool exhausted: need {n}, have {len(self._free)}")
             out = [self._free.pop() for _ in range(n)]
+            self.peak_used = max(self.peak_used, self.num_blocks - len(self._free))
         return out
 
     def release(self, blocks: List[int]) -> None:
@@ -48,6 +50,9 @@ class KVPool:
             return
         with self._lock:
             self._free.extend(reversed(blocks))
+
+    def reset_peak(self) -> None:
+        self.peak_used = self.num_blocks - len(self._free)
 
     def utilization(self) -> float:
         return 1.0 - len(self._free) / max(1, self.num_blocks)

@@ -102,7 +102,8 @@ def run(args) -> Optional[Dict[str, Any]]:
     eng = LLMEngine(EngineConfig(model=args.model, device=str(device),
                                  dtype=torch.bfloat16 if cuda else torch.float32,
                                  kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,
-                                 use_graphs=cuda and not args.no_graphs, seed=args.seed + (0 if tp_mode else rank),
+                                 use_graphs=cuda and not args.no_graphs, prefix_sharing=not args.no_prefix_sharing,
+                                 seed=args.seed + (0 if tp_mode else rank),
                                  num_blocks=None if cuda else 512), pc)
     if tp_mode and rank > 0:
         eng.serve_worker()  # replays every step rank 0 schedules
@@ -183,6 +184,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "post_s": round(d["post_s"], 3), "admit_s": round(d["admit_s"], 3),
+                   "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,
                    "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
                    **{k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}},
         "throughput": {  # rank 0's engine over the timed window
@@ -224,6 +226,7 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--resolution-tokens", type=int, default=80)
     p.add_argument("--no-hints", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--no-prefix-sharing", action="store_true", help="do not share prompt KV pages across threads")
     return p
 
 

@@ -12,6 +12,10 @@ new messages are prefilled.  When a thread would overflow the model context,
 the oldest non-seed messages are dropped (the system prompt and the first
 ``keep_seed`` messages -- the reference's seeding messages -- are kept) and
 the engine's longest-common-prefix logic re-prefills from the first change.
+Truncation has hysteresis: an overflowing thread drops old turns down to
+``trunc_low`` of its window and that cut point is sticky, so the next runs
+append to a stable prefix (one re-prefill per ~half window of new history
+instead of one per run once a thread sits at the window edge).
 """
 from __future__ import annotations
 
@@ -26,7 +30,7 @@ log = logging.getLogger(__name__)
 
 
 class _ThreadTokens:
-    __slots__ = ("sid", "sys_text", "sys_ids", "segments", "lock")
+    __slots__ = ("sid", "sys_text", "sys_ids", "segments", "lock", "dropped")
 
     def __init__(self, sid: int):
         self.sid = sid
@@ -34,16 +38,18 @@ class _ThreadTokens:
         self.sys_ids: List[int] = []
         self.segments: Dict[str, List[int]] = {}  # message id -> token ids
         self.lock = threading.Lock()
+        self.dropped = 0  # non-seed messages cut from the front (sticky truncation point)
 
 
 class EngineBackend(Backend):
     def __init__(self, engine: LLMEngine, default_max_tokens: int = 512, keep_seed: int = 2,
-                 temperature: Optional[float] = None):
+                 temperature: Optional[float] = None, trunc_low: float = 0.5):
         self.engine = engine
         self.tok = engine.tok
         self.default_max_tokens = default_max_tokens
         self.keep_seed = keep_seed
         self.temperature = temperature
+        self.trunc_low = trunc_low
         self._gen_tokens: Dict[str, List[int]] = {}  # run id -> generated ids (for the reply segment)
         self._lock = threading.Lock()
 
@@ -72,20 +78,24 @@ class EngineBackend(Backend):
             st.sys_text = sys_text
             st.sys_ids = self.tok.system_prefix(sys_text)
         msgs = list(rs.thread.messages)
-        segs = [self._segment(st, m) for m in msgs]
         gen_prompt = self.tok.header("assistant")
         budget = self.engine.max_context - max_new - len(gen_prompt) - len(st.sys_ids)
-        total = sum(len(s) for s in segs)
+        n_seed = min(self.keep_seed, len(msgs))
+        seeds = [self._segment(st, m) for m in msgs[:n_seed]]
+        st.dropped = min(st.dropped, len(msgs) - n_seed)
+        rest = [self._segment(st, m) for m in msgs[n_seed + st.dropped:]]
+        n_seed_tok = sum(len(s) for s in seeds)
+        total = n_seed_tok + sum(len(s) for s in rest)
         if total > budget:
-            keep = list(range(min(self.keep_seed, len(segs))))
-            rest = list(range(len(keep), len(segs)))
-            while rest and total > budget:
-                total -= len(segs[rest.pop(0)])
-            idx = keep + rest
-            segs = [segs[i] for i in idx]
-            if total > budget:  # a single message larger than the window: keep its tail
-                flat = [t for s in segs for t in s]
-                segs = [flat[-budget:]] if budget > 0 else []
+            # cut down to the low-water mark (never the newest message) and remember the cut
+            low = max(n_seed_tok, int(budget * self.trunc_low))
+            while len(rest) > 1 and total > low:
+                total -= len(rest.pop(0))
+                st.dropped += 1
+        segs = seeds + rest
+        if total > budget:  # a single message larger than the window: keep its tail
+            flat = [t for s in segs for t in s]
+            segs = [flat[-budget:]] if budget > 0 else []
         out = list(st.sys_ids)
         for s in segs:
             out.extend(s)

@@ -15,7 +15,12 @@ Scheduling model (one step = one forward over a flattened token batch):
 * sampling is one masked kernel over the logits rows (grammar allow-lists /
   bitmaps), then each row's grammar state advances on the host;
 * when the KV pool runs dry, idle threads are evicted LRU (their tokens are
-  kept and re-prefilled on their next run).
+  kept and re-prefilled on their next run);
+* full KV blocks written by a prefill are published in the pool's prefix
+  table (``kv_cache.py``): a thread whose prompt starts with the same blocks
+  -- the three assistants' system prompts and seeding messages are identical
+  across every concurrent RCA pipeline -- attaches those pages instead of
+  prefilling its own copy.
 
 The engine runs in a background thread (:meth:`start`) or is stepped
 explicitly (:meth:`step`); :meth:`submit` is thread-safe.
@@ -39,7 +44,7 @@ from ..ops import attention as A
 from ..ops import sampling as SMP
 from ..parallel.groups import ParallelContext, single
 from ..utils import tracing
-from .kv_cache import KVPool
+from .kv_cache import KVPool, chain_key
 from .structured import GrammarRuntime, GrammarState
 from .tokenizer import get_tokenizer
 
@@ -77,6 +82,7 @@ class EngineConfig:
     # overlap the host's token processing of step n with the GPU's forward of
     # step n+1 (decode inputs taken from the device-side sampled tokens)
     async_steps: bool = True
+    prefix_sharing: bool = True  # attach other threads' published prompt pages (kv_cache.py)
     gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
@@ -109,13 +115,14 @@ class Request:
 
 
 class Sequence:
-    __slots__ = ("id", "tokens", "n_cached", "blocks", "req", "last_used")
+    __slots__ = ("id", "tokens", "n_cached", "blocks", "req", "last_used", "bh")
 
     def __init__(self, sid: int):
         self.id = sid
         self.tokens: List[int] = []
         self.n_cached = 0
         self.blocks: List[int] = []
+        self.bh: List[int] = []  # chain keys of the leading full blocks (prefix table)
         self.req: Optional[Request] = None
         self.last_used = 0.0
 
@@ -202,7 +209,8 @@ class LLMEngine:
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
-                      "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0}
+                      "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
+                      "prefix_hit_tokens": 0}
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -245,6 +253,7 @@ class LLMEngine:
                 if s is not None:
                     self.kv.release(s.blocks)
                     s.blocks = []
+                    s.bh = []
             self._releases = keep + self._releases
 
     def _snapshot(self) -> List[Sequence]:
@@ -321,6 +330,7 @@ class LLMEngine:
                 s.n_cached = 0
                 self.kv.release(s.blocks)
                 s.blocks = []
+                s.bh = []
                 if r.on_done:
                     r.on_done(None, {"error": err})
 
@@ -349,7 +359,13 @@ class LLMEngine:
                 lcp += 1
             s.tokens = toks
             s.n_cached = lcp
-            keep = (lcp + self.kv.block_size - 1) // self.kv.block_size
+            BS = self.kv.block_size
+            del s.bh[lcp // BS:]
+            keep = (lcp + BS - 1) // BS
+            if lcp % BS and keep <= len(s.blocks) and not self.kv.make_private(s.blocks[keep - 1]):
+                # the history diverges inside a page other threads share: recompute it privately
+                keep -= 1
+                s.n_cached = keep * BS
             if len(s.blocks) > keep:
                 self.kv.release(s.blocks[keep:])
                 s.blocks = s.blocks[:keep]
@@ -406,9 +422,9 @@ class LLMEngine:
                       key=lambda s: s.last_used)
         freed = 0
         for s in idle:
-            freed += len(s.blocks)
-            self.kv.release(s.blocks)
+            freed += self.kv.release(s.blocks)  # pages other threads still share stay resident
             s.blocks = []
+            s.bh = []
             s.n_cached = 0
             self.stats["evictions"] += 1
             if freed >= n_blocks:
@@ -458,6 +474,9 @@ class LLMEngine:
             q = min(s.pending, budget)
             if s.n_cached + q > self.kv.num_blocks * BS:
                 raise MemoryError("sequence longer than the whole KV pool")
+            if self.cfg.prefix_sharing and s.n_cached % BS == 0 and len(s.blocks) == s.n_cached // BS:
+                self._attach_prefix(s)
+                q = min(s.pending, budget)
             if not self._ensure_blocks(s, s.n_cached + q, protect):
                 continue
             chunks.append((s, q))
@@ -490,6 +509,9 @@ class LLMEngine:
                 spec_pos[s.id] = s.n_cached
             s.n_cached += q
             s.last_used = time.perf_counter()
+        if self.cfg.prefix_sharing:
+            for s, _ in chunks:  # publish the pages this prefill completed (their KV write is enqueued)
+                self._register_blocks(s)
         self.stats["steps"] += 1
         self.stats["prefill_tokens"] += sum(q for _, q in chunks)
         self.stats["decode_tokens"] += len(decode)
@@ -502,6 +524,7 @@ class LLMEngine:
                 p = spec_pos.get(s.id)
                 if p is not None and (len(s.tokens) <= p or s.tokens[p] != t):
                     s.n_cached = p  # the speculative KV at p is not this sequence's token (it finished)
+                    del s.bh[p // self.kv.block_size:]
         # rows still waiting for a sample (a finished or newly-forced sequence is not)
         keep = [(i, s) for i, (ri, s) in enumerate(sample_rows)
                 if s.req is not None and s.n_cached == len(s.tokens)]
@@ -513,6 +536,41 @@ class LLMEngine:
             else:
                 self._process_tokens(self._launch_sample(*pend))
         return True
+
+    def _attach_prefix(self, s: Sequence) -> None:
+        """Map the next full blocks of ``s``'s prompt onto published pages
+        (at least one token is left to prefill: it produces the logits)."""
+        BS = self.kv.block_size
+        toks = s.tokens
+        parent = s.bh[-1] if s.bh else 0
+        if len(s.bh) != len(s.blocks):  # chain keys of this thread's own leading pages first
+            for j in range(len(s.bh), len(s.blocks)):
+                parent = chain_key(parent, toks[j * BS:(j + 1) * BS])
+                s.bh.append(parent)
+        n = s.n_cached
+        hit = 0
+        while n + BS < len(toks):
+            k = chain_key(parent, toks[n:n + BS])
+            b = self.kv.lookup(k)
+            if b is None:
+                break
+            s.blocks.append(b)
+            s.bh.append(k)
+            parent = k
+            n += BS
+            hit += 1
+        if hit:
+            s.n_cached = n
+            self.stats["prefix_hit_tokens"] += hit * BS
+
+    def _register_blocks(self, s: Sequence) -> None:
+        BS = self.kv.block_size
+        toks = s.tokens
+        parent = s.bh[-1] if s.bh else 0
+        for j in range(len(s.bh), s.n_cached // BS):
+            parent = chain_key(parent, toks[j * BS:(j + 1) * BS])
+            s.bh.append(parent)
+            self.kv.register(s.blocks[j], parent)
 
     # ------------------------------------------------------------- forward
     def _meta_arrays(self, seqs_q: List[Tuple[Sequence, int]]):

@@ -141,6 +141,41 @@ def test_backend_truncates_long_threads():
         eng.stop()
 
 
+def test_backend_truncation_is_sticky():
+    """Once a thread hits the window, the cut point stays put until the thread
+    refills: most runs prefill only their new message (no re-prefill of the
+    whole window on every run)."""
+    from k8s_llm_rca_amd.api.assistant import GenericAssistant
+    from k8s_llm_rca_amd.api.service import AssistantService
+    from k8s_llm_rca_amd.engine.backend import EngineBackend
+    eng = _engine(max_context=600, num_blocks=128)
+    svc = AssistantService(EngineBackend(eng, default_max_tokens=8, keep_seed=1))
+    a = GenericAssistant(svc)
+    a.create_assistant("You are terse.", "t", "tiny-llama")
+    a.create_thread()
+    a.add_message("seed message that must survive")
+    eng.start()
+    per_run = []
+    try:
+        for i in range(24):
+            a.add_message(f"incident {i} " + "detail " * 30)
+            pre = eng.stats["prefill_tokens"]
+            a.run_assistant(max_tokens=8)
+            assert a.wait_get_last_k_message(1, timeout=120) is not None
+            per_run.append(eng.stats["prefill_tokens"] - pre)
+        st = a.service.threads[a.thread.id].backend_state
+        toks = eng.seqs[st.sid].tokens
+        assert len(toks) <= 600
+        seed = eng.tok.message("user", "seed message that must survive")
+        assert any(toks[i:i + len(seed)] == seed for i in range(0, 40))
+    finally:
+        eng.stop()
+    new_only = len(eng.tok.message("user", "incident 10 " + "detail " * 30)) + 24
+    big = [n for n in per_run[4:] if n > new_only]
+    assert st.dropped > 0
+    assert len(big) <= len(per_run[4:]) // 2, per_run  # dropping one turn per run would re-prefill every run
+
+
 def test_mixtral_and_opt_engines_generate():
     for model in ("tiny-mixtral", "tiny-opt"):
         eng = _engine(model)
@@ -228,3 +263,62 @@ def test_async_steps_match_sync(temperature):
         assert len(res) == 12
         outs.append(res)
     assert outs[0] == outs[1]
+
+
+def _greedy(eng, prompts, max_new=8):
+    outs = {}
+    for i, p in enumerate(prompts):
+        sid = eng.new_sequence()
+        eng.submit(sid, p, None, max_new, temperature=0.0, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+        eng.run_until_idle()
+    return [outs[i] for i in range(len(prompts))]
+
+
+def test_prefix_sharing_attaches_published_pages():
+    """Threads whose prompts start with the same full blocks share the pages:
+    the second thread prefills only its own suffix, generates exactly what an
+    engine without sharing generates, and the pool gets every page back."""
+    tok = get_tokenizer()
+    seed_text = "You are an expert in kubernetes root cause analysis. " * 12
+    prompts = [tok.system_prefix(seed_text) + tok.message("user", f"incident {i}: pod crash {i * 7}")
+               + tok.header("assistant") for i in range(3)]
+    shared = _engine(num_blocks=64, block_size=32, max_batch_tokens=512)
+    plain = _engine(num_blocks=64, block_size=32, max_batch_tokens=512, prefix_sharing=False)
+    free0 = shared.kv.free_blocks
+    a = _greedy(shared, prompts)
+    b = _greedy(plain, prompts)
+    assert a == b
+    common = next(i for i in range(len(prompts[0])) if prompts[0][i] != prompts[1][i])
+    assert shared.stats["prefix_hit_tokens"] == 2 * (common // 32) * 32
+    assert plain.stats["prefix_hit_tokens"] == 0
+    assert shared.stats["prefill_tokens"] == plain.stats["prefill_tokens"] - shared.stats["prefix_hit_tokens"]
+    assert shared.kv.shared_blocks == common // 32
+    for sid in list(shared.seqs):
+        shared.release_sequence(sid)
+    assert shared.kv.free_blocks == free0 and shared.kv.shared_blocks == 0
+
+
+def test_prefix_sharing_divergence_inside_shared_page():
+    """A thread whose history is rewritten inside a shared page (truncation)
+    recomputes that page privately; the other holder's pages are untouched."""
+    tok = get_tokenizer()
+    base = tok.system_prefix("shared system prompt " * 20)
+    eng = _engine(num_blocks=64, block_size=32, max_batch_tokens=512)
+    p1 = base + tok.message("user", "first") + tok.header("assistant")
+    s1, s2 = eng.new_sequence(), eng.new_sequence()
+    out = {}
+    for sid in (s1, s2):
+        eng.submit(sid, p1, None, 4, temperature=0.0, on_done=lambda g, st, sid=sid: out.__setitem__(sid, g))
+        eng.run_until_idle()
+    assert out[s1] == out[s2]
+    shared_pages = list(eng.seqs[s1].blocks[: len(base) // 32])
+    assert shared_pages == eng.seqs[s2].blocks[: len(base) // 32]
+    snap = eng.kv.k[:, shared_pages].clone()
+    # s2's history now diverges at token 40 (inside shared page 1)
+    p2 = base[:40] + tok.message("user", "other history") + tok.header("assistant")
+    eng.submit(s2, p2, None, 4, temperature=0.0, on_done=lambda g, st: out.__setitem__("b", g))
+    eng.run_until_idle()
+    assert eng.seqs[s2].blocks[0] == shared_pages[0] and eng.seqs[s2].blocks[1] != shared_pages[1]
+    assert torch.equal(eng.kv.k[:, shared_pages], snap)
+    fresh = _engine(num_blocks=64, block_size=32, max_batch_tokens=512, prefix_sharing=False)
+    assert _greedy(fresh, [p2], 4) == [out["b"]]

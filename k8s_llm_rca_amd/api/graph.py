@@ -5,12 +5,15 @@ user, password)``, ``run_query(query, parameters=None) -> list[Record]`` and
 ``close()`` -- but the graph lives in this process (host CSR + optional HBM
 mirror) instead of behind a Bolt connection.
 
-``uri`` may be a :class:`PropertyGraph` or a ``mem://<name>`` URI registered
+``uri`` may be a :class:`PropertyGraph`, a ``mem://<name>`` URI registered
 with :func:`register_graph` (so driver code keeps the reference's
-"two executors, two URIs" shape: metagraph + stategraph).
+"two executors, two URIs" shape: metagraph + stategraph), or a graph file
+written by ``gen-graph`` / :func:`..graph.io.save_graph` (``file:///x.jsonl``
+or a plain path; loaded once per process and cached under its path).
 """
 from __future__ import annotations
 
+import os
 import threading
 import time
 from typing import Any, Dict, List, Optional, Union
@@ -33,9 +36,15 @@ def register_graph(name: str, graph: PropertyGraph) -> str:
 def resolve_graph(uri: Union[str, PropertyGraph]) -> PropertyGraph:
     if isinstance(uri, PropertyGraph):
         return uri
-    name = uri.split("://", 1)[-1] if "://" in uri else uri
+    scheme, _, rest = uri.rpartition("://")
+    name = rest if scheme else uri
     with _LOCK:
         g = _REGISTRY.get(name)
+    if g is None and scheme in ("", "file") and os.path.isfile(name):
+        from ..graph.io import load_graph
+        g = load_graph(name, os.path.splitext(os.path.basename(name))[0])
+        with _LOCK:
+            g = _REGISTRY.setdefault(name, g)
     if g is None:
         raise ConnectionError(f"no in-process graph registered as {uri!r}")
     return g

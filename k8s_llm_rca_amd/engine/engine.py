@@ -155,6 +155,16 @@ class LLMEngine:
             self.mc = get_config(cfg.model, **cfg.model_overrides)
         self.max_context = cfg.max_context or self.mc.max_position
         self.model = model or _build_model(self.mc, self.device, cfg.dtype, self.pc, cfg.seed)
+        self.gemm_dispatch = False
+        if self.device.type == "cuda":
+            from ..ops import gemm_tuning
+            from ..ops import linear as LIN
+            gemm_tuning.load(self.mc.name, self.pc.tp_size)
+            self.gemm_dispatch = LIN.load_dispatch(LIN.dispatch_path(self.mc.name, self.pc.tp_size))
+            if self.gemm_dispatch:  # split-K scratch exists before any HIP-graph capture
+                LIN.reserve_mid_scratch(self.device, LIN.DISPATCH_MAX_M, max(n for n, _ in LIN.dispatch_table()))
+            else:
+                LIN.clear_dispatch()
         self.t_model_init = time.perf_counter() - t0
         tok_path = cfg.tokenizer
         if tok_path is None and cfg.weights and os.path.exists(os.path.join(cfg.weights, "tokenizer.json")):

@@ -32,6 +32,9 @@ _SIGS = {
     "k8s_attn_prefill": [P, I, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P, P, I, I, I, F, P, I, P],
     "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P],
     "k8s_gemm_skinny": [P, I, P, P, I, I, I, I, P],
+    "k8s_gemm_mid": [P, I, P, P, I, I, I, I, I, I, P, P],
+    "k8s_gemm_mid_num_cfgs": [],
+    "k8s_gemm_mid_cfg": [I, P],
     "k8s_moe_route": [P, I, I, I, P, P, P],
     "k8s_moe_align": [P, I, I, I, P, P, P, P],
     "k8s_moe_combine": [P, P, P, I, I, I, P, P],

@@ -1,7 +1,9 @@
 """Projection GEMMs: hand-written skinny MFMA GEMM for decode shapes, hipBLASLt otherwise."""
 from __future__ import annotations
 
+import json
 import os
+from typing import Dict, List, Tuple
 
 import torch
 import torch.nn.functional as F
@@ -25,6 +27,12 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
     """``x @ w.T`` for ``x`` [M, K] and ``w`` [N, K] (bf16)."""
     M, K = x.shape
     N = w.shape[0]
+    if _dispatch and x.is_cuda and M <= DISPATCH_MAX_M:
+        ent = _lookup(N, K, M)
+        if ent is not None and ent[0] == "mid" and _mid_ok(x, w, ent[1], ent[2]):
+            return gemm_mid(x, w, ent[1], ent[2], out)
+        if ent is not None and ent[0] == "lib":
+            return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
     if (_enabled and x.is_cuda and (M == 1 or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
             and x.dtype == torch.bfloat16 and K % 256 == 0
             and N % 16 == 0 and x.stride(1) == 1 and w.is_contiguous()):
@@ -36,3 +44,140 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
     if out is None:
         return F.linear(x, w)
     return torch.matmul(x, w.t(), out=out)
+
+
+# ------------------------------------------------------- measured dispatch
+# data/gemm_dispatch_<model>.json (tools/gemm_mid_sweep.py --emit): for each
+# (N, K) projection, per M bucket, the fastest of hipBLASLt / skinny / a
+# gemm_mid variant measured on MI355X with cold (per-layer) weights.  An M
+# between buckets uses the next bucket up (every listed kernel handles any M
+# up to its bucket).
+DISPATCH_MAX_M = 256
+_dispatch: Dict[Tuple[int, int], List[tuple]] = {}
+
+
+DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "data")
+
+
+def dispatch_path(model: str, tp: int = 1) -> str:
+    return os.path.join(DATA_DIR, f"gemm_dispatch_{model}" + (f"-tp{tp}" if tp > 1 else "") + ".json")
+
+
+def load_dispatch(path: str) -> bool:
+    global _dispatch
+    if not os.path.exists(path) or os.environ.get("K8SRCA_GEMM_DISPATCH", "1") != "1":
+        return False
+    with open(path) as f:
+        d = json.load(f)
+    tab = {}
+    for key, rows in d["shapes"].items():
+        n, k = (int(v) for v in key.split(","))
+        tab[(n, k)] = sorted((int(r["m"]), r["kind"], int(r.get("cfg", -1)), int(r.get("splits", 1))) for r in rows)
+    _dispatch = tab
+    return True
+
+
+def clear_dispatch() -> None:
+    _dispatch.clear()
+
+
+def dispatch_table() -> Dict[Tuple[int, int], List[tuple]]:
+    return _dispatch
+
+
+def _lookup(N: int, K: int, M: int):
+    rows = _dispatch.get((N, K))
+    if not rows:
+        return None
+    for m, kind, cfg, splits in rows:
+        if M <= m:
+            return kind, cfg, splits
+    return None
+
+
+def _mid_ok(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> bool:
+    mt, nt, nw, _ = mid_configs()[cfg]
+    M, K = x.shape
+    return (x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()
+            and M <= 16 * mt and w.shape[0] % (16 * nt * nw) == 0 and K % (64 * splits) == 0)
+
+# ------------------------------------------------------------ mid-M GEMM
+_mid_cfgs = None
+_mid_scratch = {}
+
+
+def mid_configs():
+    """[(mt, nt, nw, u)] of the compiled gemm_mid variants (index = cfg id)."""
+    global _mid_cfgs
+    if _mid_cfgs is None:
+        import ctypes
+        L = lib()
+        out = []
+        buf = (ctypes.c_int * 4)()
+        for i in range(L.k8s_gemm_mid_num_cfgs()):
+            check(L.k8s_gemm_mid_cfg(i, buf), "gemm_mid_cfg")
+            out.append(tuple(buf))
+        _mid_cfgs = out
+    return _mid_cfgs
+
+
+def _scratch(dev: torch.device, n: int) -> torch.Tensor:
+    t = _mid_scratch.get(dev)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
+        _mid_scratch[dev] = t
+    return t
+
+
+def reserve_mid_scratch(dev: torch.device, max_m: int, max_n: int, max_splits: int = 8) -> None:
+    """Allocate the split-K partial buffer up front (before HIP-graph capture)."""
+    _scratch(dev, max_m * max_n * max_splits)
+
+
+def gemm_mid(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, out: torch.Tensor = None) -> torch.Tensor:
+    """``x @ w.T`` on the mid-M kernel (csrc/kernels/gemm_mid.hip), variant
+    ``cfg``, K split over ``splits`` workgroups (fp32 partials + reduce)."""
+    M, K = x.shape
+    N = w.shape[0]
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    part = _scratch(x.device, splits * M * N) if splits > 1 else None
+    check(lib().k8s_gemm_mid(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, cfg, splits,
+                             ptr(part), stream_ptr(x)), "gemm_mid")
+    return out
+
+
+def mid_candidates(M: int, N: int, K: int):
+    """Every (cfg, splits) that applies to (M, N, K): grid of 128..1024 workgroups."""
+    out = []
+    for i, (mt, nt, nw, u) in enumerate(mid_configs()):
+        bn = 16 * nt * nw
+        if M > 16 * mt or M <= 16 * mt // 2 and mt > 2 or N % bn:
+            continue
+        for s in (1, 2, 4, 7, 8):
+            if K % (64 * s) or K // s < 64 * u:
+                continue
+            if 128 <= (N // bn) * s <= 1024:
+                out.append((i, s))
+    return out
+
+
+def candidate_kernels(M: int, N: int, K: int):
+    """Hand-written kernels applicable to an (M, N, K) bf16 projection, as
+    ``(name, fn(x, w) -> y)`` pairs (used by tools/gemm_mid_sweep.py)."""
+    out = []
+    if M <= 128 and N % 16 == 0 and K % 256 == 0:
+        def skinny(x, w):
+            y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+            check(lib().k8s_gemm_skinny(ptr(x), x.stride(0), ptr(w), ptr(y), y.stride(0), x.shape[0], w.shape[0],
+                                        x.shape[1], stream_ptr(x)), "gemm_skinny")
+            return y
+        out.append(("skinny", skinny))
+    if 16 < M <= 256 and x_ok(K):
+        for cfg, s in mid_candidates(M, N, K):
+            out.append((f"mid{cfg}:{mid_configs()[cfg]}x{s}", lambda x, w, cfg=cfg, s=s: gemm_mid(x, w, cfg, s)))
+    return out
+
+
+def x_ok(K: int) -> bool:
+    return K % 64 == 0

@@ -230,13 +230,15 @@ def test_sampling_vocab_parallel_matches_full(tp):
 
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (512, 14336), (1280, 8192)])
-def test_gemm_skinny(M, N, K):
+def test_gemm_skinny(M, N, K, monkeypatch):
     _need_gpu()
     from k8s_llm_rca_amd.ops import linear as LIN
     torch.manual_seed(3)
     x = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
-    LIN.SKINNY_MAX_M, LIN.SKINNY_MAX_NK = 128, 1 << 40
+    monkeypatch.setattr(LIN, "SKINNY_MAX_M", 128)
+    monkeypatch.setattr(LIN, "SKINNY_MAX_NK", 1 << 40)
+    monkeypatch.setattr(LIN, "_dispatch", {})
     y = LIN.linear(x, w)
     ref = (x.float() @ w.float().t())
     torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
@@ -247,6 +249,32 @@ def test_gemm_skinny(M, N, K):
     y2 = LIN.linear(e, w)
     exp = torch.stack([w[:, (i * 37) % K] for i in range(e.shape[0])])
     torch.testing.assert_close(y2.float(), exp.float(), atol=0, rtol=0)
+
+
+@pytest.mark.parametrize("M", [17, 40, 64, 127, 200, 256])
+@pytest.mark.parametrize("N,K", [(4096, 4096), (1024, 14336), (1536, 8192)])
+def test_gemm_mid_all_variants(M, N, K):
+    """Every compiled gemm_mid variant x split-K that applies, vs fp32, with a
+    row-strided X (a slice of a wider activation) and an exact column pick."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(5)
+    xw = torch.randn(M, K + 64, device=dev).bfloat16()
+    x = xw[:, 32:32 + K]
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    ref = x.float() @ w.float().t()
+    e = torch.zeros(M, K, device=dev).bfloat16()
+    cols = [(i * 37 + 5) % K for i in range(M)]
+    e[torch.arange(M), torch.tensor(cols)] = 1.0
+    exp = w[:, cols].t().float()
+    LIN.reserve_mid_scratch(torch.device(dev), 256, N)
+    n_checked = 0
+    for cfg, splits in LIN.mid_candidates(M, N, K):
+        y = LIN.gemm_mid(x, w, cfg, splits)
+        torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2, msg=f"cfg {cfg} x{splits}")
+        torch.testing.assert_close(LIN.gemm_mid(e, w, cfg, splits).float(), exp, atol=0, rtol=0)
+        n_checked += 1
+    assert n_checked > 0
 
 
 @pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])

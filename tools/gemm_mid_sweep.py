@@ -1,0 +1,120 @@
+"""Decode-regime GEMM sweep: hipBLASLt vs the hand-written kernels at M <= 256.
+
+    python tools/gemm_mid_sweep.py [--model llama3-8b] [--ms 24,32,...] [--emit]
+
+For every projection shape of the model and every M bucket, times hipBLASLt,
+the skinny kernel and every applicable gemm_mid variant (cfg x split-K) with
+COLD weights (several copies rotated, > 512 MB per shape, as consecutive
+layers are), checks each against an fp32 reference, and prints effective
+weight-streaming bandwidth.  ``--emit`` writes the engine's dispatch table
+(``data/gemm_dispatch_<model>.json``): a hand-written kernel is chosen only
+where it beats hipBLASLt by >= 3 %.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from k8s_llm_rca_amd.ops import linear as L  # noqa: E402
+from tools.tune_gemms import shapes_for  # noqa: E402
+
+BUCKETS = "1,2,4,8,16,24,32,48,64,96,128,160,192,224,256"
+
+
+def bench(fn, iters=40):
+    for _ in range(4):
+        fn()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    torch.cuda.synchronize()
+    s.record()
+    for _ in range(iters):
+        fn()
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) / iters * 1e3  # us
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--model", default="llama3-8b")
+    ap.add_argument("--tp", type=int, default=1)
+    ap.add_argument("--ms", default=BUCKETS)
+    ap.add_argument("--emit", action="store_true")
+    ap.add_argument("--margin", type=float, default=0.97)
+    a = ap.parse_args()
+    L.clear_dispatch()  # time the raw kernels
+    ms = [int(m) for m in a.ms.split(",")]
+    shapes = shapes_for(a.model, a.tp)
+    dev = torch.device("cuda")
+    ws = {}
+    for s in shapes:
+        ncopy = max(2, (512 << 20) // (s[0] * s[1] * 2) + 1)
+        ws[s] = [torch.randn(s, dtype=torch.bfloat16, device=dev) * 0.02 for _ in range(ncopy)]
+    L.reserve_mid_scratch(dev, 256, max(n for n, _ in shapes))
+    ctr = [0]
+
+    def rot(lst):
+        ctr[0] += 1
+        return lst[ctr[0] % len(lst)]
+
+    table = {f"{n},{k}": [] for n, k in shapes}
+    tot = {}
+    t0 = time.time()
+    for M in ms:
+        for (N, K) in shapes:
+            wl = ws[(N, K)]
+            w = wl[0]
+            x = torch.randn(M, K, dtype=torch.bfloat16, device=dev)
+            gb = N * K * 2 / 1e9
+            ref = x.float() @ w.float().t()
+            lib_t = bench(lambda: torch.matmul(x, rot(wl).t()))
+            res = {"hipblaslt": lib_t}
+            cands = []
+            for name, fn in L.candidate_kernels(M, N, K):
+                y = fn(x, w)
+                err = (y.float() - ref).abs().max().item() / (ref.abs().max().item() + 1e-6)
+                if err > 2e-2:
+                    print(f"  !! {name} M{M} N{N} K{K} rel err {err:.3e}", flush=True)
+                    continue
+                cands.append((bench(lambda: fn(x, rot(wl))), name))
+            cands.sort()
+            for t, n in cands:
+                k = "mid" if n.startswith("mid") else n
+                res.setdefault(k, t)
+            best = {"m": M, "kind": "lib", "t_us": round(lib_t, 2), "lib_us": round(lib_t, 2)}
+            if cands and cands[0][0] < a.margin * lib_t:
+                t, n = cands[0]
+                if n == "skinny":
+                    best.update(kind="skinny", t_us=round(t, 2))
+                else:
+                    cfg, sp = n[3:].split(":")[0], n.split("x")[-1]
+                    best.update(kind="mid", cfg=int(cfg), splits=int(sp), t_us=round(t, 2))
+            if best["kind"] == "skinny":
+                best["kind"] = "lib" if M > 16 else "skinny"  # skinny is the default path for M <= 16
+                if best["kind"] == "lib":
+                    best["t_us"] = round(lib_t, 2)
+            table[f"{N},{K}"].append(best)
+            line = "  ".join(f"{k} {v:7.1f}us {gb / (v * 1e-6) / 1e3:5.2f}TB/s" for k, v in res.items())
+            top = " | ".join(f"{n} {t:.1f}" for t, n in cands[:3])
+            print(f"M{M:4d} N{N:6d} K{K:6d}  {line}   [{top}] -> {best['kind']}", flush=True)
+            tot.setdefault(M, [0.0, 0.0])
+            tot[M][0] += lib_t
+            tot[M][1] += best["t_us"]
+    for M, (lt, bt) in tot.items():
+        print(f"M{M:4d} per-layer sum: hipblaslt {lt:8.1f}us  dispatch {bt:8.1f}us  ({lt / bt:.2f}x)")
+    print(f"sweep took {time.time() - t0:.0f}s")
+    if a.emit:
+        path = L.dispatch_path(a.model, a.tp)
+        with open(path, "w") as f:
+            json.dump({"model": a.model, "tp": a.tp, "device": torch.cuda.get_device_name(),
+                       "note": "per-M-bucket fastest kernel, cold weights (tools/gemm_mid_sweep.py)",
+                       "shapes": table}, f, indent=1)
+        print("wrote", path)
+
+
+if __name__ == "__main__":
+    main()

@@ -34,7 +34,7 @@ constexpr int kChunk = 64;  // k per LDS stage (2 MFMA k-steps)
 
 __device__ __forceinline__ int swz(int m, int j) { return j ^ ((m >> 1) & 7); }
 
-template <int MT, int NT, int NW, int U>
+template <int MT, int NT, int NW, int U, bool SILU>
 __global__ void __launch_bounds__(NW * 64) gemm_mid_kernel(const uint16_t* __restrict__ x, int ldx,
                                                            const uint16_t* __restrict__ w,
                                                            uint16_t* __restrict__ y, int ldy,
@@ -56,6 +56,8 @@ __global__ void __launch_bounds__(NW * 64) gemm_mid_kernel(const uint16_t* __res
   const uint16_t* wrow[NT];
 #pragma unroll
   for (int nt = 0; nt < NT; ++nt) wrow[nt] = w + (size_t)(n0 + 16 * nt + r) * K + kbeg + 8 * h;
+  // SILU: x is the gate_up activation [M][2K] (gate | up) and the operand
+  // silu(gate) * up is formed while staging (bit-identical to silu_mul_kernel)
   const uint16_t* xsrc[PPT];
   int xdst[PPT];
   bool xok[PPT];
@@ -86,15 +88,29 @@ __global__ void __launch_bounds__(NW * 64) gemm_mid_kernel(const uint16_t* __res
   // X: register double buffer, loaded two chunks ahead of its MFMAs (one
   // whole iteration of latency slack before the LDS write that needs it)
   u16x8 xr[2][PPT];
+  u16x8 xu[SILU ? 2 : 1][SILU ? PPT : 1];
   auto load_x = [&](int set, int c) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i)
-      if (xok[i]) xr[set][i] = *reinterpret_cast<const u16x8*>(xsrc[i] + c * kChunk);
+      if (xok[i]) {
+        xr[set][i] = *reinterpret_cast<const u16x8*>(xsrc[i] + c * kChunk);
+        if constexpr (SILU) xu[set][i] = *reinterpret_cast<const u16x8*>(xsrc[i] + K + c * kChunk);
+      }
   };
   auto store_x = [&](int set, int buf) {
 #pragma unroll
     for (int i = 0; i < PPT; ++i)
-      if (xok[i]) *reinterpret_cast<u16x8*>(&xs[buf][xdst[i]]) = xr[set][i];
+      if (xok[i]) {
+        u16x8 v = xr[set][i];
+        if constexpr (SILU) {
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float gv = bf2f(v[j]);
+            v[j] = f2bf(gv / (1.f + __expf(-gv)) * bf2f(xu[set][i][j]));
+          }
+        }
+        *reinterpret_cast<u16x8*>(&xs[buf][xdst[i]]) = v;
+      }
   };
   auto compute = [&](int slot, int buf) {
 #pragma unroll
@@ -183,18 +199,22 @@ __global__ void __launch_bounds__(256) gemm_mid_reduce_kernel(const float* __res
 }
 
 struct MidCfg {
-  int mt, nt, nw, u;
+  int mt, nt, nw, u, silu;
   const void* fn;
 };
 
-#define K8S_MID(MT, NT, NW, U) {MT, NT, NW, U, (const void*)gemm_mid_kernel<MT, NT, NW, U>}
+#define K8S_MID(MT, NT, NW, U) {MT, NT, NW, U, 0, (const void*)gemm_mid_kernel<MT, NT, NW, U, false>}
+#define K8S_MIDS(MT, NT, NW, U) {MT, NT, NW, U, 1, (const void*)gemm_mid_kernel<MT, NT, NW, U, true>}
 // variant table (index = the `cfg` argument of k8s_gemm_mid)
 static const MidCfg kMidCfgs[] = {
     K8S_MID(2, 1, 4, 4),  K8S_MID(2, 2, 4, 4),  K8S_MID(4, 1, 4, 4),  K8S_MID(4, 2, 4, 4),
     K8S_MID(8, 1, 4, 4),  K8S_MID(8, 2, 4, 4),  K8S_MID(16, 1, 4, 4), K8S_MID(16, 2, 4, 2),
     K8S_MID(8, 2, 4, 2),  K8S_MID(4, 2, 4, 8),  K8S_MID(8, 1, 8, 4),  K8S_MID(16, 1, 8, 4),
+    // SwiGLU-fused down projections (x = gate_up)
+    K8S_MIDS(2, 1, 4, 4), K8S_MIDS(4, 1, 4, 4), K8S_MIDS(8, 1, 4, 4), K8S_MIDS(8, 1, 8, 4), K8S_MIDS(16, 1, 8, 4),
 };
 #undef K8S_MID
+#undef K8S_MIDS
 constexpr int kNumMidCfgs = sizeof(kMidCfgs) / sizeof(kMidCfgs[0]);
 
 }  // namespace k8s
@@ -203,16 +223,18 @@ using namespace k8s;
 
 K8S_API int k8s_gemm_mid_num_cfgs() { return kNumMidCfgs; }
 
-K8S_API int k8s_gemm_mid_cfg(int cfg, int* out4) {
+K8S_API int k8s_gemm_mid_cfg(int cfg, int* out5) {
   if (cfg < 0 || cfg >= kNumMidCfgs) return (int)hipErrorInvalidValue;
-  out4[0] = kMidCfgs[cfg].mt;
-  out4[1] = kMidCfgs[cfg].nt;
-  out4[2] = kMidCfgs[cfg].nw;
-  out4[3] = kMidCfgs[cfg].u;
+  out5[0] = kMidCfgs[cfg].mt;
+  out5[1] = kMidCfgs[cfg].nt;
+  out5[2] = kMidCfgs[cfg].nw;
+  out5[3] = kMidCfgs[cfg].u;
+  out5[4] = kMidCfgs[cfg].silu;
   return 0;
 }
 
-// splits > 1 needs `part` = splits * M * N fp32 scratch.
+// splits > 1 needs `part` = splits * M * N fp32 scratch.  SwiGLU variants
+// read x as [M][2K] gate|up (ldx = row stride of that buffer).
 K8S_API int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, hipStream_t s) {
   if (cfg < 0 || cfg >= kNumMidCfgs || splits < 1) return (int)hipErrorInvalidValue;

@@ -27,7 +27,7 @@ import torch.nn.functional as F
 
 from ..ops import attention as A
 from ..ops import norm as N
-from ..ops.linear import linear
+from ..ops.linear import linear, linear_silu
 from ..parallel.groups import ParallelContext, single
 from .config import ModelConfig
 from . import moe as MOE
@@ -176,8 +176,10 @@ class LlamaModel:
                 prev = self.moe.forward(li, y)
             else:
                 gu = linear(y, L["w_gu"])
-                act = N.silu_mul(gu)
-                prev = self.pc.linear_all_reduce(act, L["w_down"], linear_fn=linear)
+                if self.pc.tp_size == 1:
+                    prev = linear_silu(gu, L["w_down"])  # SwiGLU fused into the down GEMM's operand staging
+                else:
+                    prev = self.pc.linear_all_reduce(N.silu_mul(gu), L["w_down"], linear_fn=linear)
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
         logits = linear(sel, self.lm_head)

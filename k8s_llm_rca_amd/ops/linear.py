@@ -33,7 +33,10 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
             return gemm_mid(x, w, ent[1], ent[2], out)
         if ent is not None and ent[0] == "lib":
             return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
-    if (_enabled and x.is_cuda and (M == 1 or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
+        forced_skinny = ent is not None and ent[0] == "skinny" and M <= 128
+    else:
+        forced_skinny = False
+    if (_enabled and x.is_cuda and (M == 1 or forced_skinny or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
             and x.dtype == torch.bfloat16 and K % 256 == 0
             and N % 16 == 0 and x.stride(1) == 1 and w.is_contiguous()):
         if out is None:
@@ -71,8 +74,9 @@ def load_dispatch(path: str) -> bool:
         d = json.load(f)
     tab = {}
     for key, rows in d["shapes"].items():
-        n, k = (int(v) for v in key.split(","))
-        tab[(n, k)] = sorted((int(r["m"]), r["kind"], int(r.get("cfg", -1)), int(r.get("splits", 1))) for r in rows)
+        fused = key.startswith("silu:")
+        n, k = (int(v) for v in key.split(":")[-1].split(","))
+        tab[("silu", n, k) if fused else (n, k)] = sorted((int(r["m"]), r["kind"], int(r.get("cfg", -1)), int(r.get("splits", 1))) for r in rows)
     _dispatch = tab
     return True
 
@@ -85,8 +89,8 @@ def dispatch_table() -> Dict[Tuple[int, int], List[tuple]]:
     return _dispatch
 
 
-def _lookup(N: int, K: int, M: int):
-    rows = _dispatch.get((N, K))
+def _lookup(N: int, K: int, M: int, silu: bool = False):
+    rows = _dispatch.get(("silu", N, K) if silu else (N, K))
     if not rows:
         return None
     for m, kind, cfg, splits in rows:
@@ -96,10 +100,26 @@ def _lookup(N: int, K: int, M: int):
 
 
 def _mid_ok(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> bool:
-    mt, nt, nw, _ = mid_configs()[cfg]
-    M, K = x.shape
+    mt, nt, nw, _, silu = mid_configs()[cfg]
+    M = x.shape[0]
+    N, K = w.shape
     return (x.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()
-            and M <= 16 * mt and w.shape[0] % (16 * nt * nw) == 0 and K % (64 * splits) == 0)
+            and x.shape[1] == (2 * K if silu else K) and M <= 16 * mt and N % (16 * nt * nw) == 0
+            and K % (64 * splits) == 0)
+
+
+def linear_silu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``silu_mul(gu) @ w.T`` (the SwiGLU down projection): one SwiGLU-fused
+    gemm_mid launch where the dispatch table measured it fastest, else the
+    activation kernel followed by :func:`linear`."""
+    M = gu.shape[0]
+    N, K = w.shape
+    if _dispatch and gu.is_cuda and M <= DISPATCH_MAX_M:
+        ent = _lookup(N, K, M, silu=True)
+        if ent is not None and ent[0] == "mid" and _mid_ok(gu, w, ent[1], ent[2]):
+            return gemm_mid(gu, w, ent[1], ent[2])
+    from .norm import silu_mul
+    return linear(silu_mul(gu), w)
 
 # ------------------------------------------------------------ mid-M GEMM
 _mid_cfgs = None
@@ -107,13 +127,13 @@ _mid_scratch = {}
 
 
 def mid_configs():
-    """[(mt, nt, nw, u)] of the compiled gemm_mid variants (index = cfg id)."""
+    """[(mt, nt, nw, u, silu)] of the compiled gemm_mid variants (index = cfg id)."""
     global _mid_cfgs
     if _mid_cfgs is None:
         import ctypes
         L = lib()
         out = []
-        buf = (ctypes.c_int * 4)()
+        buf = (ctypes.c_int * 5)()
         for i in range(L.k8s_gemm_mid_num_cfgs()):
             check(L.k8s_gemm_mid_cfg(i, buf), "gemm_mid_cfg")
             out.append(tuple(buf))
@@ -136,9 +156,11 @@ def reserve_mid_scratch(dev: torch.device, max_m: int, max_n: int, max_splits: i
 
 def gemm_mid(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, out: torch.Tensor = None) -> torch.Tensor:
     """``x @ w.T`` on the mid-M kernel (csrc/kernels/gemm_mid.hip), variant
-    ``cfg``, K split over ``splits`` workgroups (fp32 partials + reduce)."""
-    M, K = x.shape
-    N = w.shape[0]
+    ``cfg``, K split over ``splits`` workgroups (fp32 partials + reduce).  For
+    a SwiGLU variant ``x`` is the gate_up activation [M, 2K] and the product
+    is ``silu_mul(x) @ w.T``."""
+    M = x.shape[0]
+    N, K = w.shape
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     part = _scratch(x.device, splits * M * N) if splits > 1 else None
@@ -147,12 +169,12 @@ def gemm_mid(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, out: torch
     return out
 
 
-def mid_candidates(M: int, N: int, K: int):
+def mid_candidates(M: int, N: int, K: int, silu: bool = False):
     """Every (cfg, splits) that applies to (M, N, K): grid of 128..1024 workgroups."""
     out = []
-    for i, (mt, nt, nw, u) in enumerate(mid_configs()):
+    for i, (mt, nt, nw, u, fused) in enumerate(mid_configs()):
         bn = 16 * nt * nw
-        if M > 16 * mt or M <= 16 * mt // 2 and mt > 2 or N % bn:
+        if bool(fused) != silu or M > 16 * mt or M <= 16 * mt // 2 and mt > 2 or N % bn:
             continue
         for s in (1, 2, 4, 7, 8):
             if K % (64 * s) or K // s < 64 * u:
@@ -175,7 +197,16 @@ def candidate_kernels(M: int, N: int, K: int):
         out.append(("skinny", skinny))
     if 16 < M <= 256 and x_ok(K):
         for cfg, s in mid_candidates(M, N, K):
-            out.append((f"mid{cfg}:{mid_configs()[cfg]}x{s}", lambda x, w, cfg=cfg, s=s: gemm_mid(x, w, cfg, s)))
+            out.append((f"mid{cfg}:{mid_configs()[cfg][:4]}x{s}", lambda x, w, cfg=cfg, s=s: gemm_mid(x, w, cfg, s)))
+    return out
+
+
+def silu_candidates(M: int, N: int, K: int):
+    """SwiGLU-fused gemm_mid variants for ``silu_mul(gu) @ w.T`` (w [N, K], gu [M, 2K])."""
+    out = []
+    if 16 < M <= 256 and x_ok(K):
+        for cfg, s in mid_candidates(M, N, K, silu=True):
+            out.append((f"mid{cfg}:{mid_configs()[cfg][:4]}x{s}", lambda g, w, cfg=cfg, s=s: gemm_mid(g, w, cfg, s)))
     return out
 
 

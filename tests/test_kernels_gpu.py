@@ -6,6 +6,7 @@ import torch
 
 from k8s_llm_rca_amd.ops import attention as A
 from k8s_llm_rca_amd.ops import norm as N
+from k8s_llm_rca_amd.ops import norm as N_
 from k8s_llm_rca_amd.ops import sampling as SMP
 
 pytestmark = pytest.mark.gpu
@@ -275,6 +276,24 @@ def test_gemm_mid_all_variants(M, N, K):
         torch.testing.assert_close(LIN.gemm_mid(e, w, cfg, splits).float(), exp, atol=0, rtol=0)
         n_checked += 1
     assert n_checked > 0
+
+
+@pytest.mark.parametrize("M", [20, 64, 130, 256])
+def test_gemm_mid_silu_fused(M):
+    """SwiGLU-fused variants == silu_mul (same bf16 activation) then GEMM."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    N, K = 4096, 14336
+    torch.manual_seed(7)
+    gu = torch.randn(M, 2 * K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    act = N_.silu_mul(gu)
+    ref = act.float() @ w.float().t()
+    LIN.reserve_mid_scratch(torch.device(dev), 256, N)
+    cands = LIN.mid_candidates(M, N, K, silu=True)
+    assert cands
+    for cfg, splits in cands:
+        torch.testing.assert_close(LIN.gemm_mid(gu, w, cfg, splits).float(), ref, atol=2e-2, rtol=2e-2)
 
 
 @pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])

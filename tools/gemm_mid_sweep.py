@@ -62,6 +62,9 @@ def main():
         return lst[ctr[0] % len(lst)]
 
     table = {f"{n},{k}": [] for n, k in shapes}
+    from k8s_llm_rca_amd.models.config import get_config
+    mc = get_config(a.model)
+    down = (mc.hidden, mc.intermediate // a.tp) if not mc.n_experts else None
     tot = {}
     t0 = time.time()
     for M in ms:
@@ -98,6 +101,29 @@ def main():
                 if best["kind"] == "lib":
                     best["t_us"] = round(lib_t, 2)
             table[f"{N},{K}"].append(best)
+            if (N, K) == down:  # SwiGLU-fused down projection vs silu_mul + the best plain GEMM
+                from k8s_llm_rca_amd.ops.norm import silu_mul
+                gu = torch.randn(M, 2 * K, dtype=torch.bfloat16, device=dev)
+                base = bench(lambda: silu_mul(gu)) + best["t_us"]
+                ref2 = silu_mul(gu).float() @ w.float().t()
+                fc = []
+                for name, fn in L.silu_candidates(M, N, K):
+                    err = (fn(gu, w).float() - ref2).abs().max().item() / (ref2.abs().max().item() + 1e-6)
+                    if err > 2e-2:
+                        print(f"  !! silu {name} M{M} rel err {err:.3e}", flush=True)
+                        continue
+                    fc.append((bench(lambda: fn(gu, rot(wl))), name))
+                fc.sort()
+                ent = {"m": M, "kind": "unfused", "t_us": round(base, 2)}
+                if fc and fc[0][0] < a.margin * base:
+                    t, n = fc[0]
+                    ent.update(kind="mid", cfg=int(n[3:].split(":")[0]), splits=int(n.split("x")[-1]), t_us=round(t, 2))
+                table.setdefault(f"silu:{N},{K}", []).append(ent)
+                print(f"      silu+down: unfused {base:7.1f}us  fused best "
+                      + (f"{fc[0][1]} {fc[0][0]:.1f}us" if fc else "-") + f" -> {ent['kind']}", flush=True)
+                best_t_layer = min(base, fc[0][0] if fc else base)
+                tot.setdefault(M, [0.0, 0.0])
+                tot[M][1] += best_t_layer - best["t_us"]  # count the down projection as its fused cost
             line = "  ".join(f"{k} {v:7.1f}us {gb / (v * 1e-6) / 1e3:5.2f}TB/s" for k, v in res.items())
             top = " | ".join(f"{n} {t:.1f}" for t, n in cands[:3])
             print(f"M{M:4d} N{N:6d} K{K:6d}  {line}   [{top}] -> {best['kind']}", flush=True)

@@ -1,8 +1,11 @@
 """RCA benchmark: analyses/s and p50 end-to-end latency (BASELINE.json headline).
 
-One *step* = a batch of ``incidents`` RCA analyses (locate -> generate query
--> analyze, the full reference pipeline) run concurrently on this rank's
-engine against this rank's synthetic k8s graph.  Ranks are independent engine
+One *step* = ``incidents`` RCA analyses (locate -> generate query -> analyze,
+the full reference pipeline) on this rank's engine against this rank's
+synthetic k8s graph, by ``incidents`` concurrent pipelines.  The timed K steps'
+K x incidents analyses stream through those pipelines as one work queue (a
+pipeline takes its next incident as soon as it finishes one, like the CLI's
+``run --concurrency``); ``--sync-steps`` drains every step first instead.  Ranks are independent engine
 replicas (data parallel, one process per GPU, TP=1): per-GPU work is fixed as
 N grows (weak scaling).  Timing brackets exactly ``steps`` batches with a
 barrier + device synchronize on both sides and takes the max over ranks.
@@ -133,8 +136,15 @@ def run(args) -> Optional[Dict[str, Any]]:
     sync_world = 1 if tp_mode else world
     _barrier(sync_world, device)
     t0 = time.perf_counter()
-    for s in range(n_steps):
-        chunk = incidents[(n_warm + s) * per_step:(n_warm + s + 1) * per_step]
+    if args.sync_steps:  # batch-synchronous: every step drains before the next starts
+        for s in range(n_steps):
+            chunk = incidents[(n_warm + s) * per_step:(n_warm + s + 1) * per_step]
+            st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
+            lat += st.latencies
+            errors += st.errors
+            n_done += len(st.results)
+    else:  # streaming: the K steps' incidents feed one work queue of `incidents` concurrent pipelines
+        chunk = incidents[n_warm * per_step:(n_warm + n_steps) * per_step]
         st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
         lat += st.latencies
         errors += st.errors
@@ -172,7 +182,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "global_batch": per_step * sync_world, "seq_len": eng.max_context,
                    "parallelism": f"tp{world}" if tp_mode else f"dp{world}",
                    "graph_nodes": cluster.stategraph.num_nodes,
-                   "incidents_per_gpu_per_step": per_step, "grammar_hints": not args.no_hints},
+                   "incidents_per_gpu_per_step": per_step, "grammar_hints": not args.no_hints,
+                   "step_mode": "sync" if args.sync_steps else "stream"},
         "p50_latency_s": round(p50, 3),
         "p90_latency_s": round(p90, 3),
         "errors": len(errors),
@@ -226,6 +237,9 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--resolution-tokens", type=int, default=80)
     p.add_argument("--no-hints", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--sync-steps", action="store_true",
+                   help="drain each step's batch before starting the next (default: the K steps' incidents stream "
+                        "through the same concurrent pipelines, as `run --concurrency` processes a message file)")
     p.add_argument("--no-prefix-sharing", action="store_true", help="do not share prompt KV pages across threads")
     return p
 

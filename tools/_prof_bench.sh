@@ -8,5 +8,5 @@ cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats --output-format cs
 grep '^{"metric"' $O/bench.log | cut -c1-400
 f=$(find $O -name "*kernel_stats.csv" | head -1); t=$(find $O -name "*kernel_trace.csv" | head -1)
 python3 $R/tools/kernel_summary.py $f > $O/summary.txt && cat $O/summary.txt
-python3 $R/tools/trace_gaps.py $t > $O/gaps.json && head -c 600 $O/gaps.json
+python3 $R/tools/trace_gaps.py $t 0.55 > $O/gaps.json && head -c 1500 $O/gaps.json
 cp $f $O/kernel_stats.csv; rm -f $t

@@ -1,6 +1,9 @@
 """Summarise idle gaps between consecutive kernels of a rocprofv3 kernel trace.
 
-    python tools/trace_gaps.py run_kernel_trace.csv > gaps.json
+    python tools/trace_gaps.py run_kernel_trace.csv [FROM_FRAC] > gaps.json
+
+FROM_FRAC (0..1) drops the kernels that start in the first part of the trace
+(setup + warmup) so the busy/idle figures describe the timed region.
 
 Gaps are attributed to the (previous kernel -> next kernel) name pair, so host
 work between steps (after the sampling kernel) separates from launch gaps
@@ -21,12 +24,15 @@ def short(name: str) -> str:
     return n.split("::")[-1][:60]
 
 
-def main(path):
+def main(path, from_frac=0.0):
     ks = []
     with open(path) as f:
         for r in csv.DictReader(f):
             ks.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), short(r["Kernel_Name"])))
     ks.sort()
+    if from_frac > 0:  # e.g. the timed step of a warmup + timed run
+        t_cut = ks[0][0] + from_frac * (ks[-1][1] - ks[0][0])
+        ks = [k for k in ks if k[0] >= t_cut]
     busy_end = ks[0][1]
     total_gap = 0
     hist = defaultdict(lambda: [0, 0])
@@ -58,4 +64,4 @@ def main(path):
 
 
 if __name__ == "__main__":
-    main(sys.argv[1])
+    main(sys.argv[1], float(sys.argv[2]) if len(sys.argv) > 2 else 0.0)

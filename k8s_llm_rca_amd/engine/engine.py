@@ -54,6 +54,28 @@ PART_MIN = min(A.DECODE_PARTS)  # smallest decode partition: sizes the split-KV 
 SPEC = -1  # placeholder token: "the token sampled by the in-flight step" (device-side until processed)
 
 
+def _spec_tok(spec) -> torch.Tensor:
+    tok = spec[1]
+    return tok.tokens() if isinstance(tok, _LazySample) else tok
+
+
+class _LazySample:
+    """The previous step's sampling, launched on first use (inside the next
+    forward, before its first kernel) or at the latest right after it."""
+    __slots__ = ("eng", "ps", "infl")
+
+    def __init__(self, eng, ps):
+        self.eng, self.ps, self.infl = eng, ps, None
+
+    def launch(self) -> "InFlight":
+        if self.infl is None:
+            self.infl = self.eng._launch_sample(*self.ps)
+        return self.infl
+
+    def tokens(self) -> torch.Tensor:
+        return self.launch().tok
+
+
 class InFlight:
     """A sampled step whose tokens have not been processed on the host yet."""
     __slots__ = ("seqs", "tok", "tok_host", "event", "t0")
@@ -504,15 +526,20 @@ class LLMEngine:
             off += q
             if s.n_cached + q == len(s.tokens):
                 sample_rows.append((off - 1, s))
-        infl = self._launch_sample(*ps) if ps is not None else None
-        spec = None
-        if infl is not None:
-            pos_in = {s.id: j for j, s in enumerate(infl.seqs)}
+        spec = lazy = None
+        if ps is not None:
+            # the previous step's sampling is launched from inside the forward,
+            # after this step's inputs are packed and uploaded and right before
+            # its first kernel: the GPU goes sample(k) -> forward(k+1) with no
+            # host packing time between them
+            pos_in = {s.id: j for j, s in enumerate(ps[1])}
             src = np.array([pos_in.get(s.id, -1) if s.tokens[s.n_cached] == SPEC else -1 for s in decode],
                            dtype=np.int32)
-            spec = (src, infl.tok)
+            lazy = _LazySample(self, ps)
+            spec = (src, lazy)
         self.stats["host_s"] += time.perf_counter() - t_host0
         logits = self._forward(decode, chunks, [i for i, _ in sample_rows], spec)
+        infl = lazy.launch() if lazy is not None else None
         spec_pos = {}
         for s, q in rows:
             if q == 1 and s.tokens[s.n_cached] == SPEC:
@@ -721,7 +748,7 @@ class LLMEngine:
         d_ids, _ = take(T)
         if spec is not None:
             d_ids = d_ids.clone()
-            self._apply_spec(d_ids, spec[0], spec[1])
+            self._apply_spec(d_ids, spec[0], _spec_tok(spec))
         d_pos, _ = take(T)
         d_slots, _ = take(T)
         d_sidx, _ = take(ns)
@@ -902,7 +929,12 @@ class LLMEngine:
             "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
             "items": torch.zeros(Bmax * npmax, 4, dtype=torch.int32, device=dev),
             "n_items": torch.zeros(1, dtype=torch.int32, device=dev),
-            "host": torch.zeros(Bmax * (3 + mb + 2) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory(),
+            # two pinned staging buffers, alternated per graph step; each is
+            # reused only after the event recorded behind its last H2D copy
+            "host": [torch.zeros(Bmax * (3 + mb + 2) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory()
+                     for _ in range(2)],
+            "host_ev": [None, None],
+            "host_i": 0,
         }
         self._static = st
         return st
@@ -947,7 +979,7 @@ class LLMEngine:
         B = len(decode)
         Bb = self._bucket(B)
         if Bb > max(self.cfg.graph_batch_sizes):
-            return self._forward_eager(decode, [], list(range(B)))
+            return self._forward_eager(decode, [], list(range(B)), spec)
         BS = self.kv.block_size
         mb = self.max_blocks_per_seq
         ctx = np.ones(Bb, dtype=np.int32)
@@ -968,7 +1000,10 @@ class LLMEngine:
         items = A.build_decode_items(ctx, np.arange(Bb), part)
         n_items = items.shape[0]
         assert n_items <= self._max_items
-        host = st["host"]
+        hi = st["host_i"] = st["host_i"] ^ 1
+        if st["host_ev"][hi] is not None:
+            st["host_ev"][hi].synchronize()  # its previous upload has long completed in practice
+        host = st["host"][hi]
         hv = host.numpy()
         o = 0
         for arr in (ids, pos, slots, ctx):
@@ -985,6 +1020,8 @@ class LLMEngine:
             n += B
         dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
         dev_flat.copy_(host[:n], non_blocking=True)
+        ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event()
+        ev.record()
         st["ids"][:Bb].copy_(dev_flat[0:Bb])
         st["pos"][:Bb].copy_(dev_flat[Bb:2 * Bb])
         st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
@@ -992,8 +1029,8 @@ class LLMEngine:
         st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
         st["n_items"].copy_(dev_flat[o:o + 1])
         st["items"][:n_items].copy_(dev_flat[o + 1:o + 1 + n_items * 4].view(n_items, 4))
-        if spec is not None:
-            self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], spec[1])
+        if spec is not None:  # before a capture too: its warm-up forwards read these ids
+            self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], _spec_tok(spec))
         graph, out = self._capture(Bb, part)
         graph.replay()
         return out[:B]

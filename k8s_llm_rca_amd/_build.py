@@ -87,7 +87,10 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
     _drain(procs)
     if force or _newer(out, objs):
         tmp = out + ".tmp"
-        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-o", tmp])
+        # -lhipblaslt resolves (SONAME libhipblaslt.so.1) to the copy torch already
+        # mapped when the library is loaded after `import torch`: one hipBLASLt per process
+        _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lhipblaslt",
+              "-o", tmp])
         os.replace(tmp, out)
     return out
 

@@ -32,7 +32,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
         if ent is not None and ent[0] == "mid" and _mid_ok(x, w, ent[1], ent[2]):
             return gemm_mid(x, w, ent[1], ent[2], out)
         if ent is not None and ent[0] == "lib":
-            return F.linear(x, w) if out is None else torch.matmul(x, w.t(), out=out)
+            return lib_gemm(x, w, out)
         forced_skinny = ent is not None and ent[0] == "skinny" and M <= 128
     else:
         forced_skinny = False
@@ -44,9 +44,41 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
         check(lib().k8s_gemm_skinny(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K,
                                     stream_ptr(x)), "gemm_skinny")
         return out
+    return lib_gemm(x, w, out)
+
+
+# ------------------------------------------------------------ library GEMM
+# Native hipBLASLt front end (csrc/kernels/blaslt.hip): descriptors and the
+# heuristic's algorithm cached per shape, so a call costs a hash lookup plus
+# hipblasLtMatmul instead of F.linear's ~28 us of host time.
+BLASLT_WS_BYTES = 64 << 20
+_blaslt_ws = {}
+_native_lib_gemm = os.environ.get("K8SRCA_NATIVE_BLASLT", "1") == "1"
+
+
+def lib_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
+    """``x @ w.T`` on hipBLASLt (bf16, fp32 accumulate)."""
+    if (_native_lib_gemm and x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16
+            and x.stride(1) == 1 and w.is_contiguous() and (out is None or out.stride(1) == 1)):
+        M, K = x.shape
+        N = w.shape[0]
+        if out is None:
+            out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        ws = _blaslt_ws.get(x.device)
+        if ws is None:
+            ws = _blaslt_ws[x.device] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=x.device)
+        check(lib().k8s_blaslt_gemm(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, ptr(ws),
+                                    BLASLT_WS_BYTES, stream_ptr(x)), "blaslt_gemm")
+        return out
     if out is None:
         return F.linear(x, w)
     return torch.matmul(x, w.t(), out=out)
+
+
+def reserve_lib_workspace(dev: torch.device) -> None:
+    """Allocate the hipBLASLt workspace before any HIP-graph capture."""
+    if dev not in _blaslt_ws:
+        _blaslt_ws[dev] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=dev)
 
 
 # ------------------------------------------------------- measured dispatch

@@ -278,6 +278,48 @@ def test_gemm_mid_all_variants(M, N, K):
     assert n_checked > 0
 
 
+@pytest.mark.parametrize("M,N,K", [(1, 4096, 4096), (37, 6144, 4096), (300, 28672, 4096), (2048, 4096, 14336),
+                                   (5, 128256, 4096)])
+def test_native_blaslt_gemm(M, N, K):
+    """Native hipBLASLt front end == fp32 reference (strided X, output slice),
+    repeated calls reuse the cached plan, and it replays inside a HIP graph."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(11)
+    xw = torch.randn(M, K + 128, device=dev).bfloat16()
+    x = xw[:, 64:64 + K]
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    ref = x.float() @ w.float().t()
+    y = LIN.lib_gemm(x, w)
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    big = torch.zeros(M, N + 64, device=dev).bfloat16()
+    LIN.lib_gemm(x, w, out=big[:, :N])
+    torch.testing.assert_close(big[:, :N].float(), ref, atol=2e-2, rtol=2e-2)
+    assert big[:, N:].abs().max().item() == 0
+    n_plans = LIB_PLANS()
+    LIN.lib_gemm(x, w)
+    assert LIB_PLANS() == n_plans
+    LIN.reserve_lib_workspace(torch.device(dev))
+    out = torch.empty(M, N, device=dev).bfloat16()
+    g = torch.cuda.CUDAGraph()
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        LIN.lib_gemm(x, w, out=out)
+    torch.cuda.current_stream().wait_stream(s)
+    with torch.cuda.graph(g):
+        LIN.lib_gemm(x, w, out=out)
+    out.zero_()
+    g.replay()
+    torch.cuda.synchronize()
+    torch.testing.assert_close(out.float(), ref, atol=2e-2, rtol=2e-2)
+
+
+def LIB_PLANS():
+    from k8s_llm_rca_amd.ops._lib import lib
+    return lib().k8s_blaslt_num_plans()
+
+
 @pytest.mark.parametrize("M", [20, 64, 130, 256])
 def test_gemm_mid_silu_fused(M):
     """SwiGLU-fused variants == silu_mul (same bf16 activation) then GEMM."""

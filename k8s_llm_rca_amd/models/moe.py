@@ -6,7 +6,7 @@ histogram + prefix scan) and the weighted combine are HIP kernels
 (``csrc/kernels/moe.hip``); the expert GEMMs are one grouped-GEMM launch per
 projection (``csrc/kernels/grouped_gemm.hip``) driven by the device-side
 expert offsets -- no host sync, so MoE decode steps are graph-capturable --
-with SwiGLU fused into the down projection's operand load.  Under expert parallelism (EP) the whole experts live
+with the down projection split over K for decode-sized batches.  Under expert parallelism (EP) the whole experts live
 on ``E / ep`` ranks and tokens travel by all-to-all (:mod:`..parallel.ep`).
 """
 from __future__ import annotations
@@ -50,6 +50,8 @@ class MoELayerSet:
             w2.normal_(0.0, out_std, generator=g)
             self.w13.append(w13[sl].contiguous())
             self.w2.append(w2[sl].contiguous())
+        if torch.device(device).type == "cuda":  # split-K partials exist before any HIP-graph capture
+            M.reserve_split_scratch(torch.device(device), self.SPLIT_MAX_ROWS, H, self.DOWN_SPLITS)
 
     def weight_bytes(self) -> int:
         return sum(t.numel() * t.element_size() for lst in (self.router, self.w13, self.w2) for t in lst)
@@ -67,6 +69,11 @@ class MoELayerSet:
         return M.combine(out_perm, inv, topk_w, T, self.k)
 
     GROUPED_MAX_ROWS = 2048  # above: per-expert hipBLASLt (433 vs ~1100 TF at 8k rows, MI355X)
+    # split-K of the grouped down projection (tools/bench_kernels.py --what
+    # moe_split, Mixtral shapes): 237 -> 161-185 us (5.8 TB/s) at <= 512 rows,
+    # 264 -> 305 / 485 -> 442 us at 1024 / 2048 rows with 2 slices
+    DOWN_SPLITS = 2
+    SPLIT_MAX_ROWS = 2048
 
     def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
         """Grouped SwiGLU over contiguous expert slices offsets[e]..offsets[e+1]
@@ -84,4 +91,10 @@ class MoELayerSet:
                     out[a:b] = F.linear(N.silu_mul(gu), self.w2[li][e])
             return out
         gu = M.grouped_gemm(x_perm, self.w13[li], offsets)
-        return M.grouped_gemm(gu, self.w2[li], offsets, fuse_silu=True)
+        # measured (tools/bench_kernels.py --what moe_split): silu_mul + the
+        # un-fused down GEMM beats the SwiGLU-fused operand load (244 vs 287-305
+        # us per layer at decode sizes), and splitting K (only 32 column tiles
+        # per expert) fills the chip: 168-192 us
+        rows = x_perm.shape[0]
+        splits = self.DOWN_SPLITS if rows <= self.SPLIT_MAX_ROWS else 1
+        return M.grouped_gemm(N.silu_mul(gu), self.w2[li], offsets, splits=splits)

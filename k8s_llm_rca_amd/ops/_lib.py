@@ -40,7 +40,7 @@ _SIGS = {
     "k8s_moe_route": [P, I, I, I, P, P, P],
     "k8s_moe_align": [P, I, I, I, P, P, P, P],
     "k8s_moe_combine": [P, P, P, I, I, I, P, P],
-    "k8s_grouped_gemm": [P, I, P, P, I, P, I, I, I, I, I, P],
+    "k8s_grouped_gemm": [P, I, P, P, I, P, I, I, I, I, I, I, P, I, P],
     "k8s_substr_search": [P, P, P, I, P, I, P, P, P],
     "k8s_graph_expand2": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],

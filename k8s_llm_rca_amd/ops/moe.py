@@ -57,23 +57,26 @@ def combine(y_perm: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k:
 
 
 def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, fuse_silu: bool = False,
-                 out: Optional[torch.Tensor] = None) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, splits: int = 1) -> torch.Tensor:
     """B13: rows offsets[e]..offsets[e+1] of ``a`` times ``w[e]^T`` for every
     expert in one launch (``w`` [E, N, K]).  ``fuse_silu``: ``a`` is the
     gate_up output [rows, 2K] and the activation silu(gate) * up is formed on
-    the fly.  Offsets stay on the device (no host sync)."""
+    the fly.  ``splits`` > 1 splits K over workgroups (fp32 partials + a
+    reduce; see grouped_gemm.hip).  Offsets stay on the device (no host sync)."""
     E, N, K = w.shape
     rows = a.shape[0]
     if out is None:
         out = torch.empty(rows, N, dtype=a.dtype, device=a.device)
     if rows == 0:
         return out
-    if use_hip(a) and N % 128 == 0 and K % 64 == 0:
+    if use_hip(a) and N % 128 == 0 and K % (64 * splits) == 0:
         assert a.dtype == torch.bfloat16 and w.is_contiguous() and a.stride(1) == 1 and out.is_contiguous()
         assert a.shape[1] == (2 * K if fuse_silu else K)
         max_tiles = (rows + 63) // 64 + E
+        part = _split_scratch(a.device, splits * rows * N) if splits > 1 else None
         check(lib().k8s_grouped_gemm(ptr(a), a.stride(0), ptr(w), ptr(out), out.stride(0), ptr(offsets), E, N, K,
-                                     max_tiles, int(fuse_silu), stream_ptr(a)), "grouped_gemm")
+                                     max_tiles, int(fuse_silu), splits, ptr(part), rows, stream_ptr(a)),
+              "grouped_gemm")
         return out
     offs = offsets.tolist()
     for e in range(E):
@@ -85,3 +88,19 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, fuse_s
             x = torch.nn.functional.silu(x[:, :K]) * x[:, K:]
         out[lo:hi] = (x @ w[e].float().t()).to(out.dtype)
     return out
+
+
+_scratch = {}
+
+
+def _split_scratch(dev: torch.device, n: int) -> torch.Tensor:
+    t = _scratch.get(dev)
+    if t is None or t.numel() < n:
+        t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
+        _scratch[dev] = t
+    return t
+
+
+def reserve_split_scratch(dev: torch.device, max_rows: int, N: int, splits: int) -> None:
+    """Allocate the split-K partial buffer before any HIP-graph capture."""
+    _split_scratch(dev, max_rows * N * splits)

@@ -340,9 +340,11 @@ def test_gemm_mid_silu_fused(M):
 
 @pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])
 @pytest.mark.parametrize("fuse", [False, True])
-def test_grouped_gemm_matches_per_expert(E, N, K, fuse):
+@pytest.mark.parametrize("splits", [1, 2, 4])
+def test_grouped_gemm_matches_per_expert(E, N, K, fuse, splits):
     """B13: one launch over all experts (device offsets, empty experts, ragged
-    64-row tiles) == per-expert fp32 GEMMs; fused SwiGLU operand load."""
+    64-row tiles) == per-expert fp32 GEMMs; fused SwiGLU operand load; split-K
+    partials + reduce (rows past offsets[E] untouched)."""
     from k8s_llm_rca_amd.ops import moe as MO
     _need_gpu()
     torch.manual_seed(5)
@@ -352,6 +354,6 @@ def test_grouped_gemm_matches_per_expert(E, N, K, fuse):
     rows = int(offs[-1])
     a = (torch.randn(rows, 2 * K if fuse else K) * 0.5).bfloat16()
     w = (torch.randn(E, N, K) / K ** 0.5).bfloat16()
-    got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), fuse_silu=fuse).float().cpu()
+    got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), fuse_silu=fuse, splits=splits).float().cpu()
     ref = MO.grouped_gemm(a, w, offs, fuse_silu=fuse).float()
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)

@@ -186,6 +186,32 @@ def main():
             fl = 2 * rows * 3 * I * H
             res[f"moe rows{rows}"] = (f"grouped {us_g:.0f}us ({wbytes / us_g / 1e6:.2f} TB/s-w, "
                                       f"{fl / us_g / 1e6:.0f} TF) | hipBLASLt loop {us_l:.0f}us")
+    if args.what == "moe_split":  # each grouped projection alone; down fused vs silu_mul + unfused
+        from k8s_llm_rca_amd.ops import moe as MO
+        from k8s_llm_rca_amd.ops import norm as NO
+        E, H, I = 8, 4096, 14336
+        w13 = (torch.randn(E, 2 * I, H, device=dev) * 0.02).bfloat16()
+        w2 = (torch.randn(E, H, I, device=dev) * 0.02).bfloat16()
+        for rows in (16, 64, 128, 256, 512, 1024, 2048):
+            counts = torch.full((E,), rows // E)
+            counts[: rows % E] += 1
+            offs = torch.zeros(E + 1, dtype=torch.int32)
+            offs[1:] = torch.cumsum(counts, 0)
+            offs_d = offs.to(dev)
+            x = torch.randn(rows, H, device=dev).bfloat16()
+            gu = torch.randn(rows, 2 * I, device=dev).bfloat16()
+            act = NO.silu_mul(gu)
+            t13 = timeit(lambda: MO.grouped_gemm(x, w13, offs_d), iters=10)
+            t2f = timeit(lambda: MO.grouped_gemm(gu, w2, offs_d, fuse_silu=True), iters=10)
+            t2u = timeit(lambda: MO.grouped_gemm(act, w2, offs_d), iters=10)
+            tsl = timeit(lambda: NO.silu_mul(gu), iters=10)
+            sp = {z: timeit(lambda: MO.grouped_gemm(act, w2, offs_d, splits=z), iters=10) for z in (2, 4, 8)}
+            sp13 = {z: timeit(lambda: MO.grouped_gemm(x, w13, offs_d, splits=z), iters=10) for z in (2, 4)}
+            res[f"moe_split rows{rows}"] = (
+                f"w13 {t13:.0f}us ({w13.numel() * 2 / t13 / 1e6:.2f} TB/s) "
+                + " ".join(f"x{z} {t:.0f}" for z, t in sp13.items())
+                + f" | w2 fused {t2f:.0f}us | silu {tsl:.0f}us + w2 {t2u:.0f}us "
+                f"({w2.numel() * 2 / t2u / 1e6:.2f} TB/s) " + " ".join(f"x{z} {t:.0f}" for z, t in sp.items()))
     if args.what == "gemm_big":
         for M in (512, 1024, 2048, 4096, 8192):
             for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:

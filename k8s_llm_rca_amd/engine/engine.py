@@ -185,7 +185,7 @@ class LLMEngine:
             LIN.reserve_lib_workspace(self.device)
             self.gemm_dispatch = LIN.load_dispatch(LIN.dispatch_path(self.mc.name, self.pc.tp_size))
             if self.gemm_dispatch:  # split-K scratch exists before any HIP-graph capture
-                LIN.reserve_mid_scratch(self.device, LIN.DISPATCH_MAX_M, max(k[-2] for k in LIN.dispatch_table()))
+                LIN.reserve_dispatch_scratch(self.device)
             else:
                 LIN.clear_dispatch()
         self.t_model_init = time.perf_counter() - t0

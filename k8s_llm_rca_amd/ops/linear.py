@@ -31,6 +31,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
         ent = _lookup(N, K, M)
         if ent is not None and ent[0] == "mid" and _mid_ok(x, w, ent[1], ent[2]):
             return gemm_mid(x, w, ent[1], ent[2], out)
+        if ent is not None and ent[0] == "grp" and _grp_ok(x, w, ent[2]) and (out is None or out.is_contiguous()):
+            return gemm_grp(x, w, ent[2], out)
         if ent is not None and ent[0] == "lib":
             return lib_gemm(x, w, out)
         forced_skinny = ent is not None and ent[0] == "skinny" and M <= 128
@@ -140,6 +142,30 @@ def _mid_ok(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> bool:
             and K % (64 * splits) == 0)
 
 
+_offs_cache = {}
+
+
+def _grp_ok(x: torch.Tensor, w: torch.Tensor, splits: int) -> bool:
+    N, K = w.shape
+    return (x.dtype == torch.bfloat16 and x.stride(1) == 1 and w.is_contiguous() and x.shape[1] == K
+            and N % 128 == 0 and K % (64 * splits) == 0)
+
+
+def gemm_grp(x: torch.Tensor, w: torch.Tensor, splits: int, out: torch.Tensor = None) -> torch.Tensor:
+    """``x @ w.T`` on the grouped-GEMM kernel with a single expert (64 x 128
+    tiles through swizzled LDS, split-K partials + reduce): the structure that
+    streams the MoE down projection at 5.8 TB/s, applied to dense shapes."""
+    from . import moe as MO
+    M = x.shape[0]
+    key = (x.device, M)
+    offs = _offs_cache.get(key)
+    if offs is None:  # built by the warm-up forwards, before any HIP-graph capture of this M
+        offs = _offs_cache[key] = torch.tensor([0, M], dtype=torch.int32, device=x.device)
+    if out is None:
+        out = torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device)
+    return MO.grouped_gemm(x, w.view(1, *w.shape), offs, out=out, splits=splits)
+
+
 def linear_silu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``silu_mul(gu) @ w.T`` (the SwiGLU down projection): one SwiGLU-fused
     gemm_mid launch where the dispatch table measured it fastest, else the
@@ -186,6 +212,24 @@ def reserve_mid_scratch(dev: torch.device, max_m: int, max_n: int, max_splits: i
     _scratch(dev, max_m * max_n * max_splits)
 
 
+def reserve_dispatch_scratch(dev: torch.device) -> None:
+    """Size both split-K partial buffers (gemm_mid's and the grouped kernel's)
+    for the largest split entry of the loaded dispatch table."""
+    from . import moe as MO
+    need_mid = need_grp = 0
+    for key, rows in _dispatch.items():
+        n = key[-2]
+        for m, kind, _, splits in rows:
+            if kind == "mid" and splits > 1:
+                need_mid = max(need_mid, m * n * splits)
+            elif kind == "grp" and splits > 1:
+                need_grp = max(need_grp, m * n * splits)
+    if need_mid:
+        _scratch(dev, need_mid)
+    if need_grp:
+        MO.reserve_split_scratch(dev, need_grp, 1, 1)
+
+
 def gemm_mid(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, out: torch.Tensor = None) -> torch.Tensor:
     """``x @ w.T`` on the mid-M kernel (csrc/kernels/gemm_mid.hip), variant
     ``cfg``, K split over ``splits`` workgroups (fp32 partials + reduce).  For
@@ -230,6 +274,10 @@ def candidate_kernels(M: int, N: int, K: int):
     if 16 < M <= 256 and x_ok(K):
         for cfg, s in mid_candidates(M, N, K):
             out.append((f"mid{cfg}:{mid_configs()[cfg][:4]}x{s}", lambda x, w, cfg=cfg, s=s: gemm_mid(x, w, cfg, s)))
+    if M <= 256 and N % 128 == 0:
+        for s in (1, 2, 4, 8):
+            if K % (64 * s) == 0 and (N // 128) * ((M + 63) // 64) * s <= 2048:
+                out.append((f"grp:x{s}", lambda x, w, s=s: gemm_grp(x, w, s)))
     return out
 
 

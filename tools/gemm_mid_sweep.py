@@ -86,13 +86,15 @@ def main():
                 cands.append((bench(lambda: fn(x, rot(wl))), name))
             cands.sort()
             for t, n in cands:
-                k = "mid" if n.startswith("mid") else n
+                k = "mid" if n.startswith("mid") else "grp" if n.startswith("grp") else n
                 res.setdefault(k, t)
             best = {"m": M, "kind": "lib", "t_us": round(lib_t, 2), "lib_us": round(lib_t, 2)}
             if cands and cands[0][0] < a.margin * lib_t:
                 t, n = cands[0]
                 if n == "skinny":
                     best.update(kind="skinny", t_us=round(t, 2))
+                elif n.startswith("grp"):
+                    best.update(kind="grp", splits=int(n.split("x")[-1]), t_us=round(t, 2))
                 else:
                     cfg, sp = n[3:].split(":")[0], n.split("x")[-1]
                     best.update(kind="mid", cfg=int(cfg), splits=int(sp), t_us=round(t, 2))

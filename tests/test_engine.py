@@ -322,3 +322,35 @@ def test_prefix_sharing_divergence_inside_shared_page():
     assert torch.equal(eng.kv.k[:, shared_pages], snap)
     fresh = _engine(num_blocks=64, block_size=32, max_batch_tokens=512, prefix_sharing=False)
     assert _greedy(fresh, [p2], 4) == [out["b"]]
+
+
+def test_prefix_sharing_under_kv_pressure():
+    """Shared pages survive the eviction of some holders (refcounts, not
+    ownership), evicted threads re-attach them on their next run, and every
+    page comes back to the pool when the threads are released."""
+    tok = get_tokenizer()
+    base = tok.system_prefix("shared seed prompt for every thread " * 12)
+    eng = _engine(num_blocks=16, block_size=32, max_batch_tokens=256)
+    free0 = eng.kv.free_blocks
+    sids = [eng.new_sequence() for _ in range(6)]
+    outs = {}
+    for i, sid in enumerate(sids):
+        p = base + tok.message("user", f"incident {i} " + "details " * (10 + 5 * i)) + tok.header("assistant")
+        eng.submit(sid, p, None, 6, temperature=0.0, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+        eng.run_until_idle()
+    assert len(outs) == 6
+    assert eng.stats["evictions"] > 0 and eng.stats["prefix_hit_tokens"] > 0
+    # an evicted thread's next run re-attaches the published seed pages
+    ev = next(sid for sid in sids if not eng.seqs[sid].blocks)
+    hits = eng.stats["prefix_hit_tokens"]
+    p = eng.seqs[ev].tokens + tok.message("user", "again") + tok.header("assistant")
+    eng.submit(ev, p, None, 4, temperature=0.0, on_done=lambda g, st: outs.__setitem__("again", g))
+    eng.run_until_idle()
+    assert "again" in outs and eng.stats["prefix_hit_tokens"] > hits
+    refs = eng.kv._ref
+    assert (refs >= 0).all()
+    held = sum(len(eng.seqs[s].blocks) for s in sids)
+    assert eng.kv.num_blocks - eng.kv.free_blocks <= held
+    for sid in sids:
+        eng.release_sequence(sid)
+    assert eng.kv.free_blocks == free0 and eng.kv.shared_blocks == 0 and not eng.kv._by_key

@@ -126,21 +126,50 @@ class AttnMeta:
         return max(a + b for a, b in zip(s0, npp))
 
 
-DECODE_PARTS = (512, 768, 1024)         # candidate keys per decode work item
+DECODE_PARTS = tuple(range(256, 1537, 64))  # candidate keys per decode work item (64-key aligned)
+DECODE_PARTS_V1 = (512, 768, 1024)
 DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (<= 256 VGPRs)
 DECODE_ITEM_OVERHEAD = 256               # per-item start cost in key-equivalents (replay-calibrated)
+_DECODE_PLANNER = "makespan"
 
 
-def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=DECODE_PARTS) -> tuple:
+def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=None) -> tuple:
     """Keys per decode work item for one step -> (max items per sequence, part_size).
 
     The persistent decode kernel runs ``slots`` waves over a longest-first
-    work list, so a step costs about (total keys + per-item start overhead)
-    / slots + one item (the LPT tail): smaller items balance better until the
-    start latency and the partial rows to merge dominate.  Measured on
-    recorded RCA decode steps (``tools/bench_kernels.py --what replay``)."""
+    work list (unit u = item * nkv + kv head goes to wave u mod slots), so the
+    step takes as long as wave 0's share: the first unit of every round.
+    Sorted longest-first, the items are the full ``P``-key items followed by
+    each sequence's remainder, so that makespan is exact and cheap to compute
+    for every candidate ``P`` (one sort of S remainders each):
+    ``sum over rounds r of (size of unit r*slots + start overhead)``.
+    A coarse candidate set with a "total/slots + P" bound (round-1 planner,
+    ``DECODE_PARTS_V1``) left up to a whole item of LPT tail: e.g. 96
+    sequences x 3.4k keys ran 3 rounds of 512 keys (1536) where 448-key items
+    give 3 rounds of 448 (ideal 1275)."""
     import numpy as np
     c = np.asarray(ctx_lens, dtype=np.int64)
+    mx = int(c.max()) if c.size else 1
+    if _DECODE_PLANNER == "v1":
+        return _plan_decode_split_v1(c, nkv, slots, candidates or DECODE_PARTS_V1)
+    Ps = np.asarray(candidates or DECODE_PARTS, dtype=np.int64)[:, None]      # [nc, 1]
+    n = (c[None, :] + Ps - 1) // Ps                                            # [nc, S]
+    rem = c[None, :] - (n - 1) * Ps                                            # 1..P keys
+    n_full = (n - 1).sum(1) + (rem == Ps).sum(1)                               # [nc]
+    rems = np.sort(np.where(rem < Ps, rem, 0), axis=1)[:, ::-1]                 # partial items, longest first
+    n_items = n.sum(1)
+    rounds = -(-(n_items * nkv) // slots)
+    R = int(rounds.max())
+    first = np.arange(R, dtype=np.int64)[None, :] * slots // nkv               # [1, R] item index per round
+    live = np.arange(R)[None, :] < rounds[:, None]
+    ridx = np.clip(first - n_full[:, None], 0, c.size - 1)
+    sizes = np.where(first < n_full[:, None], Ps, np.take_along_axis(rems, ridx, axis=1))
+    cost = (np.where(live, sizes + DECODE_ITEM_OVERHEAD, 0)).sum(1)
+    P = int(Ps[int(np.argmin(cost)), 0])
+    return max(1, -(-mx // P)), P
+
+
+def _plan_decode_split_v1(c, nkv, slots, candidates):
     mx = int(c.max()) if c.size else 1
     total = nkv * int(c.sum())
     best = None
@@ -151,6 +180,13 @@ def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candid
             best = (cost, P)
     P = best[1]
     return max(1, -(-mx // P)), P
+
+
+def set_decode_planner(name: str) -> None:
+    """``"makespan"`` (default) or ``"v1"`` (A/B in tools/bench_kernels.py --what replay)."""
+    global _DECODE_PLANNER
+    assert name in ("makespan", "v1")
+    _DECODE_PLANNER = name
 
 
 def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size: int, device,

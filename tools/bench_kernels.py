@@ -117,7 +117,8 @@ def main():
         pre = [s["p"] for s in steps if s["p"]]
         idx = torch.randperm(len(dec), generator=rng)[: args.samples].tolist()
         tot_us = tot_bytes = 0.0
-        variants = {"fixed512": 512, "fixed768": 768, "fixed1024": 1024}
+        variants = {"plan_v1": "v1", "plan_makespan": "makespan", "makespan_o128": "makespan:128",
+                    "makespan_o512": "makespan:512", "makespan_o64": "makespan:64"}
 
         buckets = [(1, 16), (17, 48), (49, 96), (97, 256)]
         for name, fn in variants.items():
@@ -125,7 +126,15 @@ def main():
             for i in idx:
                 ctx = dec[i]
                 B = len(ctx)
-                meta, nb = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True, part_size=fn)
+                ovh0 = A.DECODE_ITEM_OVERHEAD
+                if isinstance(fn, str):
+                    A.set_decode_planner(fn.split(":")[0])
+                    if ":" in fn:
+                        A.DECODE_ITEM_OVERHEAD = int(fn.split(":")[1])
+                meta, nb = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True,
+                                     part_size=None if isinstance(fn, str) else fn)
+                A.set_decode_planner("makespan")
+                A.DECODE_ITEM_OVERHEAD = ovh0
                 kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
                 vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
                 q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()

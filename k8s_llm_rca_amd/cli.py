@@ -140,6 +140,14 @@ def cmd_run(args) -> int:
     summary = {"analyses": len(st.results), "wall_s": round(wall, 2), "analyses_per_s": round(st.analyses_per_s, 3),
                "p50_latency_s": round(st.pct(0.5), 3), "p90_latency_s": round(st.pct(0.9), 3),
                "errors": len(st.errors), "output": args.output}
+    if args.output:  # per-stage spans (and engine counters) next to the result file
+        from .utils import tracing
+        spans = {"stages": tracing.snapshot(), "summary": summary}
+        if eng is not None:
+            spans["engine"] = {k: (round(v, 4) if isinstance(v, float) else v) for k, v in eng.stats.items()}
+            spans["engine"]["kv_peak_util"] = round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)
+        with open(args.output + ".spans.json", "w") as f:
+            json.dump(spans, f, indent=1)
     if args.state_out and hasattr(svc, "export_state"):
         with open(args.state_out, "w") as f:
             json.dump(svc.export_state(), f)

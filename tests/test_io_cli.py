@@ -1,7 +1,8 @@
 """Graph persistence, CLI drivers and assistant-service state round trips."""
-import pytest
 import json
 import os
+
+import pytest
 
 from k8s_llm_rca_amd.api.service import AssistantService, ScriptedBackend
 from k8s_llm_rca_amd.graph import io as GIO
@@ -35,6 +36,8 @@ def test_cli_run_and_resume(tmp_path, capsys):
     from k8s_llm_rca_amd.pipeline.rca import read_results
     res = read_results(out)
     assert len(res) == 4 and len({r["error_message"] for r in res}) == 4
+    spans = json.load(open(out + ".spans.json"))
+    assert "rca.analyze" in spans["stages"] and spans["summary"]["analyses"] == 2
 
 
 def test_service_state_roundtrip():

@@ -14,10 +14,10 @@ from __future__ import annotations
 from typing import List, Optional
 
 import torch
-import torch.nn.functional as F
 
 from ..ops import moe as M
 from ..ops import norm as N
+from ..ops.linear import lib_gemm
 from ..parallel.groups import ParallelContext
 from .config import ModelConfig
 
@@ -58,7 +58,7 @@ class MoELayerSet:
 
     def forward(self, li: int, y: torch.Tensor) -> torch.Tensor:
         T, H = y.shape
-        logits = F.linear(y, self.router[li])                          # [T, E]
+        logits = lib_gemm(y, self.router[li])                          # [T, E]
         topk_w, topk_ids = M.route_topk(logits, self.k)                # [T,k] fp32, int32
         if self.pc.ep_size > 1:
             from ..parallel.ep import ep_moe_forward
@@ -87,8 +87,8 @@ class MoELayerSet:
             for e in range(self.E_local):
                 a, b = offs[e], offs[e + 1]
                 if b > a:
-                    gu = F.linear(x_perm[a:b], self.w13[li][e])
-                    out[a:b] = F.linear(N.silu_mul(gu), self.w2[li][e])
+                    gu = lib_gemm(x_perm[a:b], self.w13[li][e])
+                    lib_gemm(N.silu_mul(gu), self.w2[li][e], out=out[a:b])
             return out
         gu = M.grouped_gemm(x_perm, self.w13[li], offsets)
         # measured (tools/bench_kernels.py --what moe_split): silu_mul + the

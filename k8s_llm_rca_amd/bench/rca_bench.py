@@ -130,6 +130,14 @@ def run(args) -> Optional[Dict[str, Any]]:
         st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
         errors += st.errors
     tracing.reset()
+    if not args.no_gc_freeze:
+        # the graph store, model config, grammar tables and warm-up results are
+        # long-lived: move them out of the collector's generations so a gen-2
+        # pass in the timed region does not walk millions of objects while
+        # holding the GIL (the engine thread issues kernels under it)
+        import gc
+        gc.collect()
+        gc.freeze()
     stats0 = dict(eng.stats)
     eng.kv.reset_peak()
     t_wall0 = time.time()
@@ -240,6 +248,7 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--resolution-tokens", type=int, default=80)
     p.add_argument("--no-hints", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
+    p.add_argument("--no-gc-freeze", action="store_true", help="keep warm-up objects in the GC generations")
     p.add_argument("--sync-steps", action="store_true",
                    help="drain each step's batch before starting the next (default: the K steps' incidents stream "
                         "through the same concurrent pipelines, as `run --concurrency` processes a message file)")

@@ -1,0 +1,165 @@
+// Native layer executor for the dense Llama decoder (TP = 1).
+//
+// An eager engine step (prefill chunks mixed with decode rows: shapes change
+// every step, so it cannot replay a HIP graph) issues ~10 kernels per layer.
+// Issued op by op from Python each costs ~15-20 us of host time (wrapper
+// checks, ctypes marshalling, torch dispatch), ~6 ms for an 8B step: about
+// the GPU time of a small mixed step, so the host, not the GPU, set the pace
+// and the GPU idled between steps (tools/trace_gaps.py: "last GEMM ->
+// next step's upload" gaps).  Here the whole layer stack is issued by one
+// call from a per-step descriptor (pointers + sizes + the GEMM kernel chosen
+// for this step's M by the measured dispatch table), in exactly the order
+// and with exactly the kernels of the Python path (models/llama.py), so the
+// results are bit-identical; per-layer weight / KV pointers come from tables
+// built once at model init.
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+
+#include "common.h"
+
+// the kernels' C entry points (other translation units of this library)
+extern "C" {
+int k8s_rmsnorm(const void* x, void* res, const void* w, void* y, int T, int H, int x_stride, int y_stride, float eps,
+                hipStream_t s);
+int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
+int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc, int T,
+                int nq, int nkv, int BS, hipStream_t s);
+int k8s_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
+                    int bt_stride, const int* ctx_lens, const int* q_start, int S, int nq, int nkv, int BS,
+                    float scale, void* out, int out_stride, float* part_o, float* part_ml, int n_parts,
+                    int part_size, const int* items, int n_items, const int* d_n_items, int grid_waves,
+                    hipStream_t stream);
+int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
+                     int bt_stride, const int* ctx_lens, const int* q_start, const int* tile_seq,
+                     const int* tile_tok0, const int* tile_len, const int* tile_kv0, const int* tile_kv1,
+                     const int* tile_slot, int n_tiles, const int* m_tok0, const int* m_len, const int* m_slot0,
+                     const int* m_np, int n_merge, float* pf_o, float* pf_ml, int nq, int nkv, int BS, float scale,
+                     void* out, int out_stride, hipStream_t stream);
+int k8s_gemm_skinny(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, hipStream_t s);
+int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg, int splits,
+                 void* part, hipStream_t s);
+int k8s_grouped_gemm(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E, int N,
+                     int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows, hipStream_t s);
+int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
+                    size_t ws_bytes, hipStream_t s);
+}
+
+// kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits)
+struct K8sGemmSel {
+  int kind, cfg, splits, pad;
+};
+
+// Mirrors k8s_llm_rca_amd/ops/layer_exec.py:LlamaStep (ctypes, natural alignment).
+struct K8sLlamaStep {
+  int T, nd, H, nq, nkv, I, L, BS;
+  float eps, scale;
+  // per-layer tables (host arrays of L pointers)
+  const void* const* in_norm;
+  const void* const* post_norm;
+  const void* const* wqkv;
+  const void* const* wo;
+  const void* const* wgu;
+  const void* const* wdown;
+  void* const* kc;
+  void* const* vc;
+  // activations (row-major, contiguous)
+  void* residual;  // [T][H], updated in place
+  void* y;         // [T][H]
+  void* qkv;       // [T][(nq + 2 nkv) D]
+  void* attn;      // [T][nq D]
+  void* obuf;      // [T][H]
+  void* gu;        // [T][2 I]
+  void* act;       // [T][I]
+  void* prev;      // [T][H]  (down output of the last layer on return)
+  const int* pos;
+  const float* cos_sin;
+  const int* slots;
+  // decode meta (rows [0, nd))
+  const int* d_bt;
+  const int* d_ctx;
+  const int* d_qs;
+  float* d_part_o;
+  float* d_part_ml;
+  const int* d_items;
+  const int* d_n_items_dev;
+  int d_bt_stride, d_S, d_n_parts, d_part_size, d_n_items, d_grid;
+  // prefill meta (rows [nd, T))
+  const int* p_bt;
+  const int* p_ctx;
+  const int* p_qs;
+  const int* tile[6];
+  const int* merge[4];
+  float* pf_o;
+  float* pf_ml;
+  int p_bt_stride, p_S, n_tiles, n_merge;
+  // GEMM choices for this step's M = T: qkv, o, gate_up, down
+  K8sGemmSel sel[4];
+  void* blaslt_ws;
+  size_t blaslt_ws_bytes;
+  void* mid_part;
+  void* grp_part;
+  const int* grp_offs;  // device [0, T]
+};
+
+namespace {
+
+constexpr int kD = 128;
+
+int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, const void* w, void* y, int ldy, int M,
+         int N, int K, hipStream_t st) {
+  switch (g.kind) {
+    case 1:
+      return k8s_gemm_skinny(x, ldx, w, y, ldy, M, N, K, st);
+    case 2:
+      return k8s_gemm_mid(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part, st);
+    case 3:
+      return k8s_grouped_gemm(x, ldx, w, y, ldy, s.grp_offs, 1, N, K, (M + 63) / 64 + 1, 0, g.splits, s.grp_part, M,
+                              st);
+    default:
+      return k8s_blaslt_gemm(x, ldx, w, y, ldy, M, N, K, s.blaslt_ws, s.blaslt_ws_bytes, st);
+  }
+}
+
+}  // namespace
+
+#define K8S_TRY(call)          \
+  do {                         \
+    const int rc_ = (call);    \
+    if (rc_) return rc_;       \
+  } while (0)
+
+// Layers [0, L): on return `y` holds nothing useful and `prev` + `residual`
+// are the inputs of the final norm (exactly as after the Python loop).
+K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
+  const K8sLlamaStep& s = *sp;
+  const int T = s.T, H = s.H, nd = s.nd;
+  const int qd = s.nq * kD, ld_qkv = (s.nq + 2 * s.nkv) * kD;
+  uint16_t* qkv = (uint16_t*)s.qkv;
+  uint16_t* attn = (uint16_t*)s.attn;
+  for (int l = 0; l < s.L; ++l) {
+    if (l == 0)
+      K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    else
+      K8S_TRY(k8s_rmsnorm(s.prev, s.residual, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
+    K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    if (nd > 0 && s.d_bt)
+      K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
+                              s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,
+                              s.d_items, s.d_n_items, s.d_n_items_dev, s.d_grid, st));
+    if (nd < T && s.p_bt)
+      K8S_TRY(k8s_attn_prefill(qkv + (size_t)nd * ld_qkv, ld_qkv, s.kc[l], s.vc[l], s.p_bt, s.p_bt_stride, s.p_ctx,
+                               s.p_qs, s.tile[0], s.tile[1], s.tile[2], s.tile[3], s.tile[4], s.tile[5], s.n_tiles,
+                               s.merge[0], s.merge[1], s.merge[2], s.merge[3], s.n_merge, s.pf_o, s.pf_ml, s.nq,
+                               s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, st));
+    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st));
+    K8S_TRY(k8s_rmsnorm(s.obuf, s.residual, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
+    K8S_TRY(gemm(s, s.sel[2], s.y, H, s.wgu[l], s.gu, 2 * s.I, T, 2 * s.I, H, st));
+    K8S_TRY(k8s_silu_mul(s.gu, s.act, T, s.I, st));
+    K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st));
+  }
+  return (int)hipGetLastError();
+}
+
+K8S_API int k8s_llama_step_size() { return (int)sizeof(K8sLlamaStep); }

@@ -26,6 +26,7 @@ import torch
 import torch.nn.functional as F
 
 from ..ops import attention as A
+from ..ops import layer_exec as LX
 from ..ops import norm as N
 from ..ops.linear import linear, linear_silu
 from ..parallel.groups import ParallelContext, single
@@ -60,6 +61,7 @@ class LlamaModel:
         self.inter = cfg.intermediate // tp if cfg.n_experts == 0 else cfg.intermediate
         self.vocab_local = (cfg.vocab_size + tp - 1) // tp
         self.scale = 1.0 / math.sqrt(self.D)
+        self._exec = None  # native layer executor (ops/layer_exec.py), bound on first GPU forward
         self.cos_sin = A.rope_cos_sin(cfg.max_position, cfg.rope_theta, self.D, cfg.scaling_dict(), device=self.device)
         self.layers: List[Dict[str, torch.Tensor]] = []
         self.moe: Optional[MOE.MoELayerSet] = None
@@ -153,6 +155,16 @@ class LlamaModel:
         T = inp.input_ids.shape[0]
         H = cfg.hidden
         residual = F.embedding(inp.input_ids.long(), self.embed)     # [T, H]
+        if self._exec is None and LX.LlamaExecutor.eligible(self):
+            self._exec = LX.LlamaExecutor(self)
+        if self._exec is not None and LX.LlamaExecutor.eligible(self):
+            # the dense layer stack in one native call (ops/layer_exec.py): same kernels, same order
+            prev, residual = self._exec.run(inp, residual, k_cache, v_cache)
+            y = torch.empty_like(residual)
+            N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
+            sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
+            logits = linear(sel, self.lm_head)
+            return self.pc.all_gather_last(logits) if gather_logits else logits
         prev: Optional[torch.Tensor] = None
         y = torch.empty_like(residual)
         attn = torch.empty((T, self.nq * self.D), dtype=self.dtype, device=self.device)

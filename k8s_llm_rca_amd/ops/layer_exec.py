@@ -1,0 +1,184 @@
+"""Native layer executor binding (``csrc/kernels/llama_exec.hip``).
+
+:class:`LlamaExecutor` issues the whole dense layer stack of one forward with
+a single C call: per-layer weight / KV-page pointer tables are built once,
+and per step only the activation buffers, the attention metadata pointers and
+the GEMM kernel chosen for this step's M (:func:`..ops.linear.select_gemm`,
+the same choice the Python path makes) are filled in.  Same kernels in the
+same order as ``LlamaModel.forward``'s Python loop, hence bit-identical
+results (``tests/test_model_gpu.py::test_layer_executor_bit_identical``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import List
+
+import torch
+
+from . import attention as A
+from . import linear as LIN
+from ._lib import check, lib, ptr, stream_ptr
+
+P = ctypes.c_void_p
+I = ctypes.c_int
+
+
+class GemmSel(ctypes.Structure):
+    _fields_ = [("kind", I), ("cfg", I), ("splits", I), ("pad", I)]
+
+
+class LlamaStep(ctypes.Structure):
+    _fields_ = [
+        ("T", I), ("nd", I), ("H", I), ("nq", I), ("nkv", I), ("I", I), ("L", I), ("BS", I),
+        ("eps", ctypes.c_float), ("scale", ctypes.c_float),
+        ("in_norm", P), ("post_norm", P), ("wqkv", P), ("wo", P), ("wgu", P), ("wdown", P), ("kc", P), ("vc", P),
+        ("residual", P), ("y", P), ("qkv", P), ("attn", P), ("obuf", P), ("gu", P), ("act", P), ("prev", P),
+        ("pos", P), ("cos_sin", P), ("slots", P),
+        ("d_bt", P), ("d_ctx", P), ("d_qs", P), ("d_part_o", P), ("d_part_ml", P), ("d_items", P),
+        ("d_n_items_dev", P),
+        ("d_bt_stride", I), ("d_S", I), ("d_n_parts", I), ("d_part_size", I), ("d_n_items", I), ("d_grid", I),
+        ("p_bt", P), ("p_ctx", P), ("p_qs", P), ("tile", P * 6), ("merge", P * 4), ("pf_o", P), ("pf_ml", P),
+        ("p_bt_stride", I), ("p_S", I), ("n_tiles", I), ("n_merge", I),
+        ("sel", GemmSel * 4),
+        ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
+    ]
+
+
+_enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
+_checked = False
+
+
+def _check_abi() -> None:
+    global _checked
+    if not _checked:
+        L = lib()
+        L.k8s_llama_step_size.restype = I
+        L.k8s_llama_layers.argtypes = [ctypes.POINTER(LlamaStep), P]
+        L.k8s_llama_layers.restype = I
+        n = L.k8s_llama_step_size()
+        if n != ctypes.sizeof(LlamaStep):
+            raise RuntimeError(f"LlamaStep ABI mismatch: C {n} bytes, ctypes {ctypes.sizeof(LlamaStep)}")
+        _checked = True
+
+
+def set_enabled(on: bool) -> None:
+    global _enabled
+    _enabled = on
+
+
+class LlamaExecutor:
+    """Bound to one dense, TP=1, bf16 :class:`..models.llama.LlamaModel`."""
+
+    def __init__(self, model):
+        _check_abi()
+        self.m = model
+        Ls = model.layers
+        n = len(Ls)
+
+        def table(key):
+            arr = (P * n)(*[t[key].data_ptr() for t in Ls])
+            return arr
+
+        self._tabs = {k: table(k) for k in ("in_norm", "post_norm", "wqkv", "wo", "w_gu", "w_down")}
+        self._kv_key = None
+        self.st = LlamaStep()
+        st = self.st
+        cfg = model.cfg
+        st.H, st.nq, st.nkv, st.I, st.L = cfg.hidden, model.nq, model.nkv, model.inter, n
+        st.eps, st.scale = float(cfg.rms_eps), float(model.scale)
+        st.in_norm = ctypes.addressof(self._tabs["in_norm"])
+        st.post_norm = ctypes.addressof(self._tabs["post_norm"])
+        st.wqkv = ctypes.addressof(self._tabs["wqkv"])
+        st.wo = ctypes.addressof(self._tabs["wo"])
+        st.wgu = ctypes.addressof(self._tabs["w_gu"])
+        st.wdown = ctypes.addressof(self._tabs["w_down"])
+        st.cos_sin = model.cos_sin.data_ptr()
+
+    @staticmethod
+    def eligible(model) -> bool:
+        return (_enabled and model.device.type == "cuda" and model.pc.tp_size == 1 and model.moe is None
+                and model.dtype == torch.bfloat16 and model.D == A.HEAD_DIM and not _silu_fused_in_table(model))
+
+    def _bind_kv(self, k_cache: torch.Tensor, v_cache: torch.Tensor) -> None:
+        key = (k_cache.data_ptr(), v_cache.data_ptr(), k_cache.shape[1])
+        if key == self._kv_key:
+            return
+        n = self.st.L
+        self._kc = (P * n)(*[k_cache[li].data_ptr() for li in range(n)])
+        self._vc = (P * n)(*[v_cache[li].data_ptr() for li in range(n)])
+        self.st.kc = ctypes.addressof(self._kc)
+        self.st.vc = ctypes.addressof(self._vc)
+        self.st.BS = k_cache.shape[3]
+        self._kv_key = key
+
+    def run(self, inp, residual: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor) -> List[torch.Tensor]:
+        """All layers; returns ``(prev, residual)`` for the final norm."""
+        m, st = self.m, self.st
+        self._bind_kv(k_cache, v_cache)
+        T, H = residual.shape
+        dev, dt = residual.device, residual.dtype
+        ld_qkv = (m.nq + 2 * m.nkv) * m.D
+        y = torch.empty((T, H), dtype=dt, device=dev)
+        qkv = torch.empty((T, ld_qkv), dtype=dt, device=dev)
+        attn = torch.empty((T, m.nq * m.D), dtype=dt, device=dev)
+        obuf = torch.empty((T, H), dtype=dt, device=dev)
+        gu = torch.empty((T, 2 * m.inter), dtype=dt, device=dev)
+        act = torch.empty((T, m.inter), dtype=dt, device=dev)
+        prev = torch.empty((T, H), dtype=dt, device=dev)
+        st.T, st.nd = T, inp.n_decode
+        st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
+        st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
+        st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)
+        md = inp.meta_decode if inp.n_decode > 0 else None
+        if md is not None:
+            st.d_bt, st.d_ctx, st.d_qs = md.block_tables.data_ptr(), md.ctx_lens.data_ptr(), md.q_start.data_ptr()
+            st.d_part_o, st.d_part_ml = ptr(md.part_o), ptr(md.part_ml)
+            st.d_items, st.d_n_items_dev = ptr(md.items), ptr(md.d_n_items)
+            st.d_bt_stride, st.d_S = md.block_tables.stride(0), md.num_seqs
+            st.d_n_parts, st.d_part_size, st.d_n_items = md.n_parts, md.part_size, md.n_items
+            st.d_grid = md.grid_waves or min(A.DECODE_WAVE_SLOTS, md.n_items * m.nkv)
+        else:
+            st.d_bt = None
+        mp = inp.meta_prefill if inp.n_decode < T else None
+        if mp is not None:
+            if mp.n_merge and mp.pf_o is None:
+                mp.pf_o, mp.pf_ml = A.prefill_workspace(m.nkv, dev, max(mp.m_slot0_end(), 1))
+            st.p_bt, st.p_ctx, st.p_qs = mp.block_tables.data_ptr(), mp.ctx_lens.data_ptr(), mp.q_start.data_ptr()
+            for i, t in enumerate((mp.tile_seq, mp.tile_tok0, mp.tile_len, mp.tile_kv0, mp.tile_kv1, mp.tile_slot)):
+                st.tile[i] = t.data_ptr()
+            for i, t in enumerate((mp.m_tok0, mp.m_len, mp.m_slot0, mp.m_np)):
+                st.merge[i] = t.data_ptr()
+            st.pf_o, st.pf_ml = ptr(mp.pf_o), ptr(mp.pf_ml)
+            st.p_bt_stride, st.p_S, st.n_tiles, st.n_merge = mp.block_tables.stride(0), mp.num_seqs, mp.n_tiles, \
+                mp.n_merge
+        else:
+            st.p_bt = None
+        H_, I_ = m.cfg.hidden, m.inter
+        shapes = ((ld_qkv, H_), (H_, m.nq * m.D), (2 * I_, H_), (H_, I_))
+        need_mid = need_grp = 0
+        for i, (N, K) in enumerate(shapes):
+            kind, cfg, splits = LIN.select_gemm(T, N, K)
+            st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
+            if kind == LIN.KIND_MID and splits > 1:
+                need_mid = max(need_mid, splits * T * N)
+            elif kind == LIN.KIND_GRP:
+                need_grp = max(need_grp, splits * T * N if splits > 1 else 1)
+        LIN.reserve_lib_workspace(dev)
+        ws = LIN._blaslt_ws[dev]
+        st.blaslt_ws, st.blaslt_ws_bytes = ws.data_ptr(), LIN.BLASLT_WS_BYTES
+        # the same split-K buffers the Python path grows (reserved before any capture)
+        st.mid_part = LIN._scratch(dev, need_mid).data_ptr() if need_mid else None
+        if need_grp:
+            from . import moe as MO
+            st.grp_part = MO._split_scratch(dev, need_grp).data_ptr()
+            st.grp_offs = LIN.grp_offsets(dev, T).data_ptr()
+        check(lib().k8s_llama_layers(ctypes.byref(st), stream_ptr(residual)), "llama_layers")
+        return prev, residual
+
+
+def _silu_fused_in_table(model) -> bool:
+    """The executor issues silu_mul + down GEMM; a table that fuses SwiGLU into
+    the down GEMM for some M keeps the Python path (never the case today)."""
+    rows = LIN.dispatch_table().get(("silu", model.cfg.hidden, model.inter))
+    return bool(rows) and any(r[1] == "mid" for r in rows)

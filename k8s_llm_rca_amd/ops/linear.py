@@ -23,24 +23,45 @@ def set_skinny(enabled: bool) -> None:
     _enabled = enabled
 
 
+KIND_LIB, KIND_SKINNY, KIND_MID, KIND_GRP = 0, 1, 2, 3
+
+
+def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bool = True) -> Tuple[int, int, int]:
+    """(kind, cfg, splits) :func:`linear` runs for a contiguous bf16 ``x`` [M, K]
+    and ``w`` [N, K] on the GPU -- the measured dispatch table first, then the
+    skinny kernel's default range, else hipBLASLt.  Also used by the native
+    layer executor (ops/layer_exec.py) so both paths pick the same kernel."""
+    forced_skinny = False
+    if _dispatch and M <= DISPATCH_MAX_M:
+        ent = _lookup(N, K, M)
+        if ent is not None:
+            kind, cfg, splits = ent
+            if kind == "mid" and x_ok_layout and _mid_shape_ok(M, N, K, cfg, splits):
+                return KIND_MID, cfg, splits
+            if kind == "grp" and x_ok_layout and out_contig and N % 128 == 0 and K % (64 * splits) == 0:
+                return KIND_GRP, 0, splits
+            if kind == "lib":
+                return KIND_LIB, 0, 1
+            forced_skinny = kind == "skinny" and M <= 128
+    if (_enabled and (M == 1 or forced_skinny or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
+            and x_ok_layout and K % 256 == 0 and N % 16 == 0):
+        return KIND_SKINNY, 0, 1
+    return KIND_LIB, 0, 1
+
+
 def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
     """``x @ w.T`` for ``x`` [M, K] and ``w`` [N, K] (bf16)."""
     M, K = x.shape
     N = w.shape[0]
-    if _dispatch and x.is_cuda and M <= DISPATCH_MAX_M:
-        ent = _lookup(N, K, M)
-        if ent is not None and ent[0] == "mid" and _mid_ok(x, w, ent[1], ent[2]):
-            return gemm_mid(x, w, ent[1], ent[2], out)
-        if ent is not None and ent[0] == "grp" and _grp_ok(x, w, ent[2]) and (out is None or out.is_contiguous()):
-            return gemm_grp(x, w, ent[2], out)
-        if ent is not None and ent[0] == "lib":
-            return lib_gemm(x, w, out)
-        forced_skinny = ent is not None and ent[0] == "skinny" and M <= 128
-    else:
-        forced_skinny = False
-    if (_enabled and x.is_cuda and (M == 1 or forced_skinny or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
-            and x.dtype == torch.bfloat16 and K % 256 == 0
-            and N % 16 == 0 and x.stride(1) == 1 and w.is_contiguous()):
+    if not (x.is_cuda and x.dtype == torch.bfloat16):
+        return lib_gemm(x, w, out)
+    layout = x.stride(1) == 1 and x.stride(0) % 8 == 0 and w.is_contiguous()
+    kind, cfg, splits = select_gemm(M, N, K, layout, out is None or out.is_contiguous())
+    if kind == KIND_MID:
+        return gemm_mid(x, w, cfg, splits, out)
+    if kind == KIND_GRP:
+        return gemm_grp(x, w, splits, out)
+    if kind == KIND_SKINNY:
         if out is None:
             out = torch.empty((M, N), dtype=x.dtype, device=x.device)
         check(lib().k8s_gemm_skinny(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K,
@@ -133,6 +154,11 @@ def _lookup(N: int, K: int, M: int, silu: bool = False):
     return None
 
 
+def _mid_shape_ok(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
+    mt, nt, nw, _, silu = mid_configs()[cfg]
+    return not silu and M <= 16 * mt and N % (16 * nt * nw) == 0 and K % (64 * splits) == 0
+
+
 def _mid_ok(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int) -> bool:
     mt, nt, nw, _, silu = mid_configs()[cfg]
     M = x.shape[0]
@@ -151,16 +177,23 @@ def _grp_ok(x: torch.Tensor, w: torch.Tensor, splits: int) -> bool:
             and N % 128 == 0 and K % (64 * splits) == 0)
 
 
+def grp_offsets(dev: torch.device, M: int) -> torch.Tensor:
+    """Device [0, M] expert offsets of a single-expert grouped GEMM (built by
+    the warm-up forwards, before any HIP-graph capture of this M)."""
+    key = (dev, M)
+    offs = _offs_cache.get(key)
+    if offs is None:
+        offs = _offs_cache[key] = torch.tensor([0, M], dtype=torch.int32, device=dev)
+    return offs
+
+
 def gemm_grp(x: torch.Tensor, w: torch.Tensor, splits: int, out: torch.Tensor = None) -> torch.Tensor:
     """``x @ w.T`` on the grouped-GEMM kernel with a single expert (64 x 128
     tiles through swizzled LDS, split-K partials + reduce): the structure that
     streams the MoE down projection at 5.8 TB/s, applied to dense shapes."""
     from . import moe as MO
     M = x.shape[0]
-    key = (x.device, M)
-    offs = _offs_cache.get(key)
-    if offs is None:  # built by the warm-up forwards, before any HIP-graph capture of this M
-        offs = _offs_cache[key] = torch.tensor([0, M], dtype=torch.int32, device=x.device)
+    offs = grp_offsets(x.device, M)
     if out is None:
         out = torch.empty((M, w.shape[0]), dtype=x.dtype, device=x.device)
     return MO.grouped_gemm(x, w.view(1, *w.shape), offs, out=out, splits=splits)

@@ -104,3 +104,45 @@ def test_mixtral_engine_graphs_match_eager():
             assert eng.stats["graph_steps"] > 0
         outs.append(res)
     assert outs[0] == outs[1]
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_layer_executor_bit_identical(graphs):
+    """The native layer executor (one C call per forward) issues the same
+    kernels in the same order as the Python layer loop: every step's logits
+    are bit-identical, for mixed prefill+decode steps and graph decode steps."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.ops import layer_exec as LX
+    runs = []
+    try:
+        for on in (False, True):
+            LX.set_enabled(on)
+            eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=512, use_graphs=graphs,
+                                         temperature=0.0, max_batch_tokens=256, graph_batch_sizes=(1, 2, 4, 8)))
+            logs = []
+            fwd = eng.model.forward
+
+            def rec(*a, **k):
+                out = fwd(*a, **k)
+                if not torch.cuda.is_current_stream_capturing():  # graph steps: covered by the tokens
+                    logs.append(out.float().cpu())
+                return out
+            eng.model.forward = rec
+            res = {}
+            for i in range(6):
+                sid = eng.new_sequence()
+                p = eng.tok.system_prefix("s") + eng.tok.message("user", "w%d " % i * (20 + 40 * i)) + \
+                    eng.tok.header("assistant")
+                eng.submit(sid, p, None, 12, temperature=0.0, on_done=lambda g, st, i=i: res.__setitem__(i, g))
+            eng.run_until_idle()
+            assert (eng.model._exec is not None) == on
+            runs.append((res, logs))
+    finally:
+        LX.set_enabled(True)
+    (r0, l0), (r1, l1) = runs
+    assert r0 == r1
+    assert len(l0) == len(l1) and len(l0) > 2
+    for a, b in zip(l0, l1):
+        assert torch.equal(a, b)

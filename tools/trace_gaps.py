@@ -37,6 +37,7 @@ def main(path, from_frac=0.0):
     total_gap = 0
     hist = defaultdict(lambda: [0, 0])
     pairs = defaultdict(lambda: [0, 0])
+    big = defaultdict(lambda: [0, 0])  # >= 1 ms gaps only
     prev = ks[0][2]
     for s, e, n in ks[1:]:
         if s > busy_end:
@@ -47,6 +48,9 @@ def main(path, from_frac=0.0):
             hist[b][1] += g
             pairs[(prev, n)][0] += 1
             pairs[(prev, n)][1] += g
+            if g >= 1e6:
+                big[(prev, n)][0] += 1
+                big[(prev, n)][1] += g
         if e > busy_end:
             busy_end = e
             prev = n
@@ -54,7 +58,9 @@ def main(path, from_frac=0.0):
     top = sorted(pairs.items(), key=lambda kv: -kv[1][1])[:25]
     out = {"kernels": len(ks), "span_s": span / 1e9, "gap_s": total_gap / 1e9,
            "hist": {k: {"n": v[0], "s": v[1] / 1e9} for k, v in hist.items()},
-           "top_pairs": [{"prev": p[0], "next": p[1], "n": v[0], "s": round(v[1] / 1e9, 4)} for p, v in top]}
+           "top_pairs": [{"prev": p[0], "next": p[1], "n": v[0], "s": round(v[1] / 1e9, 4)} for p, v in top],
+           "big_gap_pairs": [{"prev": p[0], "next": p[1], "n": v[0], "s": round(v[1] / 1e9, 4)}
+                             for p, v in sorted(big.items(), key=lambda kv: -kv[1][1])[:10]]}
     mid = int(len(ks) * 0.7)
     win = []
     for s_, e_, n in ks[mid:mid + 400]:

@@ -88,3 +88,25 @@ def test_bench_dp2_torchrun_cpu_contract(tmp_path):
     d = _json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["steps"] == 1 and d["config"]["parallelism"] == "dp2"
     assert d["config"]["global_batch"] == 4 and d["value"] > 0 and d["errors"] == 0
+
+
+def test_cli_stage_drivers(tmp_path, capsys):
+    """The reference's per-stage drivers (test_find_metapath.py,
+    test_generate_query.py, test_check_state.py) as CLI subcommands."""
+    from k8s_llm_rca_amd.cli import main
+    from k8s_llm_rca_amd.graph.io import load_incidents_csv
+    d = str(tmp_path / "c")
+    assert main(["gen-graph", "--graph-nodes", "600", "--incidents", "12", "--out", d]) == 0
+    capsys.readouterr()
+    inc = next(i for i in load_incidents_csv(d + "/incidents.csv") if i.fault == "secret_missing")
+    base = ["--backend", "oracle", "--graph-dir", d, "--message", inc.message]
+    assert main(["locate", *base]) == 0
+    out = capsys.readouterr().out
+    j = json.loads(out[out.index("{"):])
+    assert j["srcKind"] == "Pod" and j["metapaths"]
+    mp = ("\n    HasEvent, Event, EVENT, metadata_uid;\n    ReferInternal, Event, Pod, involvedObject_uid;\n"
+          "    ReferInternal, Pod, Secret, spec_volumes_secret_secretName;\n")
+    assert main(["query", *base, "--metapath", mp]) == 0
+    assert "MATCH (evt:EVENT)" in capsys.readouterr().out
+    assert main(["state", *base, "--kind", "Pod", "--id", inc.involved_id, "--timestamp", inc.timestamp]) == 0
+    assert capsys.readouterr().out.strip()

@@ -15,7 +15,8 @@ CATS = [
     ("attn_prefill", r"attn_prefill"),
     ("gemm_hipblaslt", r"^(Custom_)?Cijk"),
     ("gemm_skinny", r"gemm_skinny|gemm_mid"),
-    ("moe", r"moe|grouped_gemm"),
+    ("gemm_grouped", r"grouped_gemm|grouped_reduce"),  # MoE experts, and split-K dense GEMMs (dispatch 'grp')
+    ("moe", r"moe"),
     ("norm_rope_act", r"rmsnorm|rope|silu|layernorm|relu"),
     ("sampling", r"sample|gumbel|argmax"),
     ("allreduce", r"allreduce|ncclDevKernel|rccl"),

@@ -56,6 +56,7 @@ def main():
     ap.add_argument("--what", default="all")
     ap.add_argument("--trace", default="profiles/r1_shape_trace_128.jsonl")
     ap.add_argument("--samples", type=int, default=80)
+    ap.add_argument("--variants", default="", help="replay: comma list of planner variants (default all)")
     args = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -119,6 +120,8 @@ def main():
         tot_us = tot_bytes = 0.0
         variants = {"plan_v1": "v1", "plan_makespan": "makespan", "makespan_o128": "makespan:128",
                     "makespan_o512": "makespan:512", "makespan_o64": "makespan:64"}
+        if args.variants:
+            variants = {k: v for k, v in variants.items() if k in args.variants.split(",")}
 
         buckets = [(1, 16), (17, 48), (49, 96), (97, 256)]
         for name, fn in variants.items():

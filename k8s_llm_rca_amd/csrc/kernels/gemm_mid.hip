@@ -235,8 +235,8 @@ K8S_API int k8s_gemm_mid_cfg(int cfg, int* out5) {
 
 // splits > 1 needs `part` = splits * M * N fp32 scratch.  SwiGLU variants
 // read x as [M][2K] gate|up (ldx = row stride of that buffer).
-K8S_API int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
-                         int splits, void* part, hipStream_t s) {
+static int launch_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                      int splits, void* part, bool reduce, hipStream_t s) {
   if (cfg < 0 || cfg >= kNumMidCfgs || splits < 1) return (int)hipErrorInvalidValue;
   const MidCfg& c = kMidCfgs[cfg];
   const int bn = 16 * c.nt * c.nw;
@@ -250,10 +250,22 @@ K8S_API int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy
   // the kernel parameters above are all 4- or 8-byte scalars/pointers, in order
   hipError_t e = hipLaunchKernel(c.fn, g, dim3(c.nw * 64), args, 0, s);
   if (e != hipSuccess) return (int)e;
-  if (splits > 1) {
+  if (splits > 1 && reduce) {
     const int blocks = (M * N / 8 + 255) / 256;
     hipLaunchKernelGGL(gemm_mid_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, splits,
                        (uint16_t*)y, ldy, M, N);
   }
   return (int)hipGetLastError();
+}
+
+K8S_API int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                         int splits, void* part, hipStream_t s) {
+  return launch_mid(x, ldx, w, y, ldy, M, N, K, cfg, splits, part, true, s);
+}
+
+// splits > 1: leaves the fp32 partials [splits][M][N] in `part` for a fused
+// consumer (k8s_splitk_addnorm) instead of launching the reduce kernel.
+K8S_API int k8s_gemm_mid_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                              int splits, void* part, hipStream_t s) {
+  return launch_mid(x, ldx, w, y, ldy, M, N, K, cfg, splits, part, false, s);
 }

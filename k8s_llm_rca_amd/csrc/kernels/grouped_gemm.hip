@@ -194,9 +194,9 @@ using namespace k8s;
 // max_tiles >= sum_e ceil(rows_e / 64); ceil(total_rows / 64) + E always is.
 // splits > 1: part = splits * total_rows * N fp32 scratch (total_rows = rows
 // of `a`, >= offsets[E]); K % (64 * splits) == 0.
-K8S_API int k8s_grouped_gemm(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E,
-                             int N, int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows,
-                             hipStream_t s) {
+static int launch_grouped(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E, int N,
+                          int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows, bool reduce,
+                          hipStream_t s) {
   if (N % GG_BN || K % (GG_BK * splits) || E <= 0 || max_tiles <= 0 || splits < 1 || (splits > 1 && !part) ||
       N % 8 || ldy % 8)
     return (int)hipErrorInvalidValue;
@@ -208,10 +208,24 @@ K8S_API int k8s_grouped_gemm(const void* a, int lda, const void* w, void* y, int
   else
     hipLaunchKernelGGL(grouped_gemm_kernel<false>, grid, dim3(256), 0, s, (const uint16_t*)a, lda,
                        (const uint16_t*)w, (uint16_t*)y, ldy, offsets, E, N, K, pp, total_rows);
-  if (splits > 1) {
+  if (splits > 1 && reduce) {
     const int blocks = min(2048, (int)(((size_t)total_rows * N / 8 + 255) / 256));
     hipLaunchKernelGGL(grouped_reduce_kernel, dim3(max(blocks, 1)), dim3(256), 0, s, (const float*)pp, splits,
                        (uint16_t*)y, ldy, offsets, E, N, total_rows);
   }
   return (int)hipGetLastError();
+}
+
+K8S_API int k8s_grouped_gemm(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E,
+                             int N, int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows,
+                             hipStream_t s) {
+  return launch_grouped(a, lda, w, y, ldy, offsets, E, N, K, max_tiles, fuse_silu, splits, part, total_rows, true, s);
+}
+
+// splits > 1: partials [splits][total_rows][N] stay in `part` for a fused consumer
+K8S_API int k8s_grouped_gemm_part(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E,
+                                  int N, int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows,
+                                  hipStream_t s) {
+  return launch_grouped(a, lda, w, y, ldy, offsets, E, N, K, max_tiles, fuse_silu, splits, part, total_rows, false,
+                        s);
 }

@@ -22,6 +22,8 @@
 extern "C" {
 int k8s_rmsnorm(const void* x, void* res, const void* w, void* y, int T, int H, int x_stride, int y_stride, float eps,
                 hipStream_t s);
+int k8s_splitk_addnorm(const void* part, int splits, void* res, const void* w, void* y, int T, int H, int y_stride,
+                       float eps, hipStream_t s);
 int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc, int T,
                 int nq, int nkv, int BS, hipStream_t s);
@@ -39,15 +41,20 @@ int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc
 int k8s_gemm_skinny(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, hipStream_t s);
 int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg, int splits,
                  void* part, hipStream_t s);
+int k8s_gemm_mid_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                      int splits, void* part, hipStream_t s);
 int k8s_grouped_gemm(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E, int N,
                      int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows, hipStream_t s);
+int k8s_grouped_gemm_part(const void* a, int lda, const void* w, void* y, int ldy, const int* offsets, int E, int N,
+                          int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows, hipStream_t s);
 int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
                     size_t ws_bytes, hipStream_t s);
 }
 
-// kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits)
+// kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits);
+// fuse: a split-K o / down projection may leave its partials to the next norm
 struct K8sGemmSel {
-  int kind, cfg, splits, pad;
+  int kind, cfg, splits, fuse;
 };
 
 // Mirrors k8s_llm_rca_amd/ops/layer_exec.py:LlamaStep (ctypes, natural alignment).
@@ -106,16 +113,26 @@ namespace {
 
 constexpr int kD = 128;
 
+// A split-K choice (kinds 2 and 3, splits > 1) with `defer` leaves its fp32
+// partials in the kind's scratch for the following norm to reduce
+// (k8s_splitk_addnorm); deferred() tells the caller where they are.
+bool deferred(const K8sGemmSel& g, bool defer) {
+  return defer && g.fuse && g.splits > 1 && (g.kind == 2 || g.kind == 3);
+}
+
+const void* part_of(const K8sLlamaStep& s, const K8sGemmSel& g) { return g.kind == 2 ? s.mid_part : s.grp_part; }
+
 int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, const void* w, void* y, int ldy, int M,
-         int N, int K, hipStream_t st) {
+         int N, int K, hipStream_t st, bool defer = false) {
+  const bool d = deferred(g, defer);
   switch (g.kind) {
     case 1:
       return k8s_gemm_skinny(x, ldx, w, y, ldy, M, N, K, st);
     case 2:
-      return k8s_gemm_mid(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part, st);
+      return (d ? k8s_gemm_mid_part : k8s_gemm_mid)(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part, st);
     case 3:
-      return k8s_grouped_gemm(x, ldx, w, y, ldy, s.grp_offs, 1, N, K, (M + 63) / 64 + 1, 0, g.splits, s.grp_part, M,
-                              st);
+      return (d ? k8s_grouped_gemm_part : k8s_grouped_gemm)(x, ldx, w, y, ldy, s.grp_offs, 1, N, K,
+                                                            (M + 63) / 64 + 1, 0, g.splits, s.grp_part, M, st);
     default:
       return k8s_blaslt_gemm(x, ldx, w, y, ldy, M, N, K, s.blaslt_ws, s.blaslt_ws_bytes, st);
   }
@@ -131,15 +148,22 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
 
 // Layers [0, L): on return `y` holds nothing useful and `prev` + `residual`
 // are the inputs of the final norm (exactly as after the Python loop).
+// Where the step's dispatch picked a split-K kernel for the o or down
+// projection, its partials are reduced inside the following residual-add +
+// RMSNorm (k8s_splitk_addnorm): bit-identical, one launch fewer per GEMM.
 K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   const K8sLlamaStep& s = *sp;
   const int T = s.T, H = s.H, nd = s.nd;
   const int qd = s.nq * kD, ld_qkv = (s.nq + 2 * s.nkv) * kD;
   uint16_t* qkv = (uint16_t*)s.qkv;
   uint16_t* attn = (uint16_t*)s.attn;
+  bool pend = false;  // the previous layer's down projection is still split-K partials
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    else if (pend)
+      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[3]), s.sel[3].splits, s.residual, s.in_norm[l], s.y, T, H, H,
+                                 s.eps, st));
     else
       K8S_TRY(k8s_rmsnorm(s.prev, s.residual, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
     K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
@@ -153,11 +177,17 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                                s.p_qs, s.tile[0], s.tile[1], s.tile[2], s.tile[3], s.tile[4], s.tile[5], s.n_tiles,
                                s.merge[0], s.merge[1], s.merge[2], s.merge[3], s.n_merge, s.pf_o, s.pf_ml, s.nq,
                                s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, st));
-    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st));
-    K8S_TRY(k8s_rmsnorm(s.obuf, s.residual, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
+    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, true));
+    if (deferred(s.sel[1], true))
+      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[1]), s.sel[1].splits, s.residual, s.post_norm[l], s.y, T, H, H,
+                                 s.eps, st));
+    else
+      K8S_TRY(k8s_rmsnorm(s.obuf, s.residual, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
     K8S_TRY(gemm(s, s.sel[2], s.y, H, s.wgu[l], s.gu, 2 * s.I, T, 2 * s.I, H, st));
     K8S_TRY(k8s_silu_mul(s.gu, s.act, T, s.I, st));
-    K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st));
+    // the last layer's down output is returned (`prev`) for the final norm
+    pend = deferred(s.sel[3], l + 1 < s.L);
+    K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, l + 1 < s.L));
   }
   return (int)hipGetLastError();
 }

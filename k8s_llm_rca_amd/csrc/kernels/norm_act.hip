@@ -7,22 +7,56 @@ namespace k8s {
 // ------------------------------------------------------------ RMSNorm (+add)
 // y = rmsnorm(x [+ res]) * w ; when res != nullptr, res <- x + res (bf16).
 // One workgroup per row; each thread keeps NC 8-element chunks in registers.
-template <int NC>
+//
+// PART: x is the still-unreduced output of a split-K projection GEMM
+// (fp32 partials part[s][row][:], s < splits; gemm_mid / grouped layout):
+// the row is summed here in the reduce kernels' order and rounded to bf16
+// before the residual add, so the result is bit-identical to reduce kernel +
+// rmsnorm kernel, one launch (and one [T][H] round trip) fewer.  Every
+// decode-step launch costs ~5 us however small (tools/trace_by_grid.py), so
+// the launch, not the bytes, is what this saves.
+template <int NC, bool PART = false>
 __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict__ x, uint16_t* __restrict__ res,
                                                       const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                      int H, int x_stride, int y_stride, float eps) {
+                                                      int H, int x_stride, int y_stride, float eps,
+                                                      const float* __restrict__ part = nullptr, int splits = 0,
+                                                      int T = 0) {
   __shared__ float scratch[16];
   const int row = blockIdx.x;
   const int nv = H >> 3;
   const uint16_t* xr = x + (size_t)row * x_stride;
   uint16_t* rr = res ? res + (size_t)row * H : nullptr;
+  // the weight row does not depend on the reduction: issue its loads first
+  u16x8 wv[NC];
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int i = threadIdx.x + c * 256;
+    if (i < nv) wv[c] = *reinterpret_cast<const u16x8*>(w + i * 8);
+  }
   float v[NC][8];
   float ss = 0.f;
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int i = threadIdx.x + c * 256;
     if (i < nv) {
-      u16x8 a = *reinterpret_cast<const u16x8*>(xr + i * 8);
+      u16x8 a;
+      if constexpr (PART) {
+        const float* pr = part + (size_t)row * H + i * 8;
+        const size_t TH = (size_t)T * H;
+        f32x4 a0 = *reinterpret_cast<const f32x4*>(pr);
+        f32x4 a1 = *reinterpret_cast<const f32x4*>(pr + 4);
+        for (int sp = 1; sp < splits; ++sp) {
+          a0 += *reinterpret_cast<const f32x4*>(pr + sp * TH);
+          a1 += *reinterpret_cast<const f32x4*>(pr + sp * TH + 4);
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          a[j] = f2bf(a0[j]);
+          a[j + 4] = f2bf(a1[j]);
+        }
+      } else {
+        a = *reinterpret_cast<const u16x8*>(xr + i * 8);
+      }
       if (rr) {
         u16x8 b = *reinterpret_cast<const u16x8*>(rr + i * 8);
         u16x8 s;
@@ -48,10 +82,9 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
   for (int c = 0; c < NC; ++c) {
     const int i = threadIdx.x + c * 256;
     if (i < nv) {
-      u16x8 wv = *reinterpret_cast<const u16x8*>(w + i * 8);
       u16x8 o;
 #pragma unroll
-      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[j]));
+      for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[c][j]));
       *reinterpret_cast<u16x8*>(yr + i * 8) = o;
     }
   }
@@ -141,14 +174,38 @@ K8S_API int k8s_rmsnorm(const void* x, void* res, const void* w, void* y, int T,
   uint16_t* yy = (uint16_t*)y;
   if (T <= 0) return 0;
   switch (nc) {
-    case 1: hipLaunchKernelGGL(rmsnorm_kernel<1>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
-    case 2: hipLaunchKernelGGL(rmsnorm_kernel<2>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
+    case 1: hipLaunchKernelGGL((rmsnorm_kernel<1, false>), dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps, nullptr, 0, 0); break;
+    case 2: hipLaunchKernelGGL((rmsnorm_kernel<2, false>), dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps, nullptr, 0, 0); break;
     case 3:
-    case 4: hipLaunchKernelGGL(rmsnorm_kernel<4>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps); break;
+    case 4: hipLaunchKernelGGL((rmsnorm_kernel<4, false>), dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps, nullptr, 0, 0); break;
     default:
       if (nc > 8) return (int)hipErrorInvalidValue;
-      hipLaunchKernelGGL(rmsnorm_kernel<8>, dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps);
+      hipLaunchKernelGGL((rmsnorm_kernel<8, false>), dim3(T), dim3(256), 0, s, xx, rr, ww, yy, H, x_stride, y_stride, eps, nullptr, 0, 0);
   }
+  return (int)hipGetLastError();
+}
+
+// y = rmsnorm(bf16(sum_s part[s]) + res) * w, res <- bf16(sum_s part[s]) + res;
+// part = [splits][T][H] fp32 partials of a split-K GEMM (see rmsnorm_kernel).
+K8S_API int k8s_splitk_addnorm(const void* part, int splits, void* res, const void* w, void* y, int T, int H,
+                               int y_stride, float eps, hipStream_t s) {
+  if (H % 8 || splits < 1 || !part || !res || H / 8 > 1024) return (int)hipErrorInvalidValue;
+  if (T <= 0) return 0;
+  const int nc = (H / 8 + 255) / 256;
+  const float* pp = (const float*)part;
+  uint16_t* rr = (uint16_t*)res;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  const uint16_t* nx = nullptr;
+  if (nc == 1)
+    hipLaunchKernelGGL((rmsnorm_kernel<1, true>), dim3(T), dim3(256), 0, s, nx, rr, ww, yy, H, H, y_stride, eps, pp,
+                       splits, T);
+  else if (nc == 2)
+    hipLaunchKernelGGL((rmsnorm_kernel<2, true>), dim3(T), dim3(256), 0, s, nx, rr, ww, yy, H, H, y_stride, eps, pp,
+                       splits, T);
+  else
+    hipLaunchKernelGGL((rmsnorm_kernel<4, true>), dim3(T), dim3(256), 0, s, nx, rr, ww, yy, H, H, y_stride, eps, pp,
+                       splits, T);
   return (int)hipGetLastError();
 }
 

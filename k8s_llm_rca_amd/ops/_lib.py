@@ -33,6 +33,8 @@ _SIGS = {
     "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P],
     "k8s_gemm_skinny": [P, I, P, P, I, I, I, I, P],
     "k8s_gemm_mid": [P, I, P, P, I, I, I, I, I, I, P, P],
+    "k8s_gemm_mid_part": [P, I, P, P, I, I, I, I, I, I, P, P],
+    "k8s_splitk_addnorm": [P, I, P, P, P, I, I, I, F, P],
     "k8s_gemm_mid_num_cfgs": [],
     "k8s_blaslt_gemm": [P, I, P, P, I, I, I, I, P, ctypes.c_size_t, P],
     "k8s_blaslt_num_plans": [],
@@ -41,6 +43,7 @@ _SIGS = {
     "k8s_moe_align": [P, I, I, I, P, P, P, P],
     "k8s_moe_combine": [P, P, P, I, I, I, P, P],
     "k8s_grouped_gemm": [P, I, P, P, I, P, I, I, I, I, I, I, P, I, P],
+    "k8s_grouped_gemm_part": [P, I, P, P, I, P, I, I, I, I, I, I, P, I, P],
     "k8s_substr_search": [P, P, P, I, P, I, P, P, P],
     "k8s_graph_expand2": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],

@@ -25,7 +25,7 @@ I = ctypes.c_int
 
 
 class GemmSel(ctypes.Structure):
-    _fields_ = [("kind", I), ("cfg", I), ("splits", I), ("pad", I)]
+    _fields_ = [("kind", I), ("cfg", I), ("splits", I), ("fuse", I)]
 
 
 class LlamaStep(ctypes.Structure):
@@ -46,6 +46,8 @@ class LlamaStep(ctypes.Structure):
 
 
 _enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
+# split-K o / down projections reduced inside the following residual add + RMSNorm
+_fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
 _checked = False
 
 
@@ -160,6 +162,7 @@ class LlamaExecutor:
         for i, (N, K) in enumerate(shapes):
             kind, cfg, splits = LIN.select_gemm(T, N, K)
             st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
+            st.sel[i].fuse = int(_fuse_splitk)
             if kind == LIN.KIND_MID and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:

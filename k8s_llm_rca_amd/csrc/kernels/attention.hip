@@ -68,7 +68,7 @@ struct AttnArgs {
   // decode work list (persistent kernel): int4 (seq, part | -1 = whole row, k1, qrow)
   const int4* items;
   int n_items;
-  const int* d_n_items;   // device count (HIP graphs: the grid stays fixed), or null
+  const int* d_n_items;   // device {item count, part_size} (HIP graphs: the grid stays fixed), or null
 };
 
 struct RowState {
@@ -399,7 +399,10 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
 __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
   const int lane = threadIdx.x;
   const int r = lane & 15;
-  const int n_items = a.d_n_items ? __builtin_amdgcn_readfirstlane(*a.d_n_items) : a.n_items;
+  // graphs: {item count, keys per partition} are read on the device, so one
+  // captured graph serves every step's plan
+  const int n_items = a.d_n_items ? __builtin_amdgcn_readfirstlane(a.d_n_items[0]) : a.n_items;
+  const int part_size = a.d_n_items ? __builtin_amdgcn_readfirstlane(a.d_n_items[1]) : a.part_size;
   const int total = n_items * a.nkv;
   const bool valid = r < a.G;
   for (int w = blockIdx.x; w < total; w += gridDim.x) {
@@ -408,7 +411,7 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
     const int seq = item.x, k1 = item.z, qrow = item.w;
     const bool whole = item.y < 0;
     const int part = whole ? 0 : item.y;
-    const int k0 = part * a.part_size;
+    const int k0 = part * part_size;
     const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
     const int pg0 = k0 / a.BS, npg = (k1 - 1) / a.BS - pg0 + 1;
     const int blkv = lane < npg ? bt[pg0 + lane] : 0;
@@ -423,7 +426,8 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   const int qh = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
   const int ctx = a.ctx_lens[seq];
-  const int np = min(a.n_parts, (ctx + a.part_size - 1) / a.part_size);
+  const int part_size = a.d_n_items ? a.d_n_items[1] : a.part_size;
+  const int np = min(a.n_parts, (ctx + part_size - 1) / part_size);
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
   float M = -INFINITY;

@@ -929,10 +929,10 @@ class LLMEngine:
             "part_o": torch.empty(Bmax * self.model.nq * npmax * self.model.D, dtype=torch.float32, device=dev),
             "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
             "items": torch.zeros(Bmax * npmax, 4, dtype=torch.int32, device=dev),
-            "n_items": torch.zeros(1, dtype=torch.int32, device=dev),
+            "n_items": torch.zeros(2, dtype=torch.int32, device=dev),  # {item count, keys per item}
             # two pinned staging buffers, alternated per graph step; each is
             # reused only after the event recorded behind its last H2D copy
-            "host": [torch.zeros(Bmax * (3 + mb + 2) + 1 + Bmax * npmax * 4, dtype=torch.int32).pin_memory()
+            "host": [torch.zeros(Bmax * (3 + mb + 2) + 2 + Bmax * npmax * 4, dtype=torch.int32).pin_memory()
                      for _ in range(2)],
             "host_ev": [None, None],
             "host_i": 0,
@@ -953,7 +953,9 @@ class LLMEngine:
         return StepInputs(st["ids"][:B], st["pos"][:B], st["slots"][:B], B, meta, None, st["sidx"][:B])
 
     def _capture(self, B: int, part: int):
-        key = (B, part)
+        """Graph of a ``B``-row decode step.  ``part`` only seeds the capture:
+        the decode kernels read each replay's keys-per-item from the device."""
+        key = B
         g = self._graphs.get(key)
         if g is not None:
             return g
@@ -1013,8 +1015,9 @@ class LLMEngine:
         hv[o:o + Bb * mb] = bt.reshape(-1)
         o += Bb * mb
         hv[o] = n_items
-        hv[o + 1:o + 1 + n_items * 4] = items.reshape(-1)
-        n = o + 1 + n_items * 4
+        hv[o + 1] = part
+        hv[o + 2:o + 2 + n_items * 4] = items.reshape(-1)
+        n = o + 2 + n_items * 4
         if spec is not None:
             hv[n:n + B] = spec[0]
             n_src = n
@@ -1028,11 +1031,11 @@ class LLMEngine:
         st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
         st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
         st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
-        st["n_items"].copy_(dev_flat[o:o + 1])
-        st["items"][:n_items].copy_(dev_flat[o + 1:o + 1 + n_items * 4].view(n_items, 4))
+        st["n_items"].copy_(dev_flat[o:o + 2])
+        st["items"][:n_items].copy_(dev_flat[o + 2:o + 2 + n_items * 4].view(n_items, 4))
         if spec is not None:  # before a capture too: its warm-up forwards read these ids
             self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], _spec_tok(spec))
-        graph, out = self._capture(Bb, part)
+        graph, out = self._capture(Bb, part)  # one graph per bucket: the plan's part size is read on the device
         graph.replay()
         return out[:B]
 

@@ -112,7 +112,7 @@ class AttnMeta:
     # decode work list (persistent kernel, BS % 64 == 0): see build_decode_items
     items: Optional[torch.Tensor] = None      # [n_items, 4] int32
     n_items: int = 0
-    d_n_items: Optional[torch.Tensor] = None  # [1] int32 device count (HIP graphs)
+    d_n_items: Optional[torch.Tensor] = None  # [2] int32 device {item count, part_size} (HIP graphs)
     grid_waves: int = 0
     # host copies for the reference path
     ctx_lens_host: Optional[list] = None

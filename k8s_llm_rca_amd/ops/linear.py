@@ -178,8 +178,17 @@ def _grp_ok(x: torch.Tensor, w: torch.Tensor, splits: int) -> bool:
 
 
 def grp_offsets(dev: torch.device, M: int) -> torch.Tensor:
-    """Device [0, M] expert offsets of a single-expert grouped GEMM (built by
-    the warm-up forwards, before any HIP-graph capture of this M)."""
+    """Device [0, M] expert offsets of a single-expert grouped GEMM: a row of
+    one table uploaded once per device (a per-M ``torch.tensor`` upload is a
+    pageable copy that waits for every queued kernel -- a GPU bubble each
+    time a new M shows up mid-run)."""
+    tab = _offs_cache.get(dev)
+    if tab is None:
+        rows = torch.arange(DISPATCH_MAX_M + 1, dtype=torch.int32)
+        tab = torch.stack([torch.zeros_like(rows), rows], 1)
+        tab = _offs_cache[dev] = tab.to(dev)
+    if M <= DISPATCH_MAX_M:
+        return tab[M]
     key = (dev, M)
     offs = _offs_cache.get(key)
     if offs is None:
@@ -261,6 +270,8 @@ def reserve_dispatch_scratch(dev: torch.device) -> None:
         _scratch(dev, need_mid)
     if need_grp:
         MO.reserve_split_scratch(dev, need_grp, 1, 1)
+    if dev.type == "cuda":
+        grp_offsets(dev, 0)  # the offsets table, before any timed step or capture
 
 
 def gemm_mid(x: torch.Tensor, w: torch.Tensor, cfg: int, splits: int, out: torch.Tensor = None) -> torch.Tensor:

@@ -107,7 +107,7 @@ def test_mixtral_engine_graphs_match_eager():
 
 
 @pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True)])
-def test_layer_executor_bit_identical(graphs, splitk, monkeypatch):
+def test_layer_executor_bit_identical(graphs, splitk):
     """The native layer executor (one C call per forward) issues the same
     kernels in the same order as the Python layer loop: every step's logits
     are bit-identical, for mixed prefill+decode steps and graph decode steps.
@@ -119,14 +119,17 @@ def test_layer_executor_bit_identical(graphs, splitk, monkeypatch):
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
     from k8s_llm_rca_amd.ops import layer_exec as LX
     from k8s_llm_rca_amd.ops import linear as LIN
-    if splitk:  # tiny-llama: o and down are both [512, 1024]
-        monkeypatch.setitem(LIN._dispatch, (512, 1024), [(32, "mid", 0, 2), (64, "mid", 2, 4), (256, "grp", -1, 2)])
+    split_rows = [(32, "mid", 0, 2), (64, "mid", 2, 4), (256, "grp", -1, 2)]  # tiny-llama o and down: [512, 1024]
     runs = []
     try:
         for on in (False, True):
             LX.set_enabled(on)
             eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=512, use_graphs=graphs,
                                          temperature=0.0, max_batch_tokens=256, graph_batch_sizes=(1, 2, 4, 8)))
+            if splitk:  # after the engine's own (absent) dispatch table was loaded
+                LIN._dispatch[(512, 1024)] = split_rows
+                assert LIN.select_gemm(6, 512, 1024)[0] == LIN.KIND_MID
+                assert LIN.select_gemm(100, 512, 1024)[0] == LIN.KIND_GRP
             logs = []
             fwd = eng.model.forward
 
@@ -147,6 +150,7 @@ def test_layer_executor_bit_identical(graphs, splitk, monkeypatch):
             runs.append((res, logs))
     finally:
         LX.set_enabled(True)
+        LIN._dispatch.pop((512, 1024), None)
     (r0, l0), (r1, l1) = runs
     assert r0 == r1
     assert len(l0) == len(l1) and len(l0) > 2

@@ -212,6 +212,14 @@ static const MidCfg kMidCfgs[] = {
     K8S_MID(8, 2, 4, 2),  K8S_MID(4, 2, 4, 8),  K8S_MID(8, 1, 8, 4),  K8S_MID(16, 1, 8, 4),
     // SwiGLU-fused down projections (x = gate_up)
     K8S_MIDS(2, 1, 4, 4), K8S_MIDS(4, 1, 4, 4), K8S_MIDS(8, 1, 4, 4), K8S_MIDS(8, 1, 8, 4), K8S_MIDS(16, 1, 8, 4),
+    // M tiles matched to the decode batch buckets 48 / 96 / 160 / 192 / 224:
+    // every wave reads all 16*MT staged X rows from LDS per chunk (the LDS
+    // reads, not HBM, bound this kernel -- profiles/README.md), so padding
+    // M = 96 to 128 rows or 192 to 256 costs 25-33 % of that traffic and of the
+    // MFMAs.  Appended so the indices above (dispatch tables) stay valid.
+    K8S_MID(3, 1, 4, 4),  K8S_MID(3, 2, 4, 4),  K8S_MID(6, 1, 4, 4),  K8S_MID(6, 1, 8, 4),
+    K8S_MID(6, 2, 4, 4),  K8S_MID(10, 1, 8, 4), K8S_MID(12, 1, 4, 4), K8S_MID(12, 1, 8, 4),
+    K8S_MID(14, 1, 8, 4),
 };
 #undef K8S_MID
 #undef K8S_MIDS

@@ -118,6 +118,9 @@ DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 
 
 def dispatch_path(model: str, tp: int = 1) -> str:
+    override = os.environ.get("K8SRCA_GEMM_DISPATCH_FILE")  # A/B of two measured tables
+    if override:
+        return override
     return os.path.join(DATA_DIR, f"gemm_dispatch_{model}" + (f"-tp{tp}" if tp > 1 else "") + ".json")
 
 

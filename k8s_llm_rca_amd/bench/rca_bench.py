@@ -218,6 +218,10 @@ def run(args) -> Optional[Dict[str, Any]]:
             "ttft_p50_s": round(ttft[len(ttft) // 2], 4) if ttft else None,
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         "setup_s": round(setup_s, 1),
+        "blaslt_tune": ({"s": round(eng.t_gemm_tune, 2), "points": len(eng.gemm_tuning),
+                         "heuristic_us": round(sum(t[3] for t in eng.gemm_tuning), 1),
+                         "tuned_us": round(sum(t[4] for t in eng.gemm_tuning), 1)}
+                        if getattr(eng, "gemm_tuning", None) else None),
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }
     if world > 1 and not tp_mode:

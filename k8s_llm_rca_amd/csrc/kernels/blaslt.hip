@@ -17,11 +17,22 @@
 // Layout: hipBLASLt is column-major.  Row-major Y[M][N] is column-major
 // Y^T[N][M] (ld = ldy) = W . X^T: A = the column-major K x N image of W
 // (lda = K) transposed, B = the column-major K x M image of X (ldb = ldx).
+//
+// Measured algorithm choice (k8s_blaslt_tune): at prefill-sized M (256..8192)
+// the heuristic's first solution is not always the fastest one it lists, so
+// the engine times the top candidates once per (N, K) at a ladder of M at
+// init; a later plan for any M takes the candidate tuned at the largest
+// ladder M <= M, if hipBLASLt confirms it supports the problem; below the
+// ladder (decode sizes: data/gemm_dispatch_*.json) and otherwise, the heuristic's.
 #include <hip/hip_runtime.h>
 #include <hipblaslt/hipblaslt.h>
+#include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <iterator>
+#include <map>
 #include <mutex>
 #include <unordered_map>
+#include <vector>
 
 #include "common.h"
 
@@ -55,29 +66,57 @@ struct Plan {
 std::mutex g_mu;
 hipblasLtHandle_t g_handle = nullptr;
 std::unordered_map<Key, Plan, KeyHash> g_plans;
+// (N, K) -> ladder M -> tuned algorithm
+std::map<std::pair<int, int>, std::map<int, hipblasLtMatmulAlgo_t>> g_tuned;
 
-int build_plan(const Key& k, size_t ws_limit, Plan* out) {
-  Plan p;
-  hipblasStatus_t st;
-  st = hipblasLtMatmulDescCreate(&p.desc, HIPBLAS_COMPUTE_32F, HIP_R_32F);
+int make_desc(const Key& k, Plan* p) {
+  hipblasStatus_t st = hipblasLtMatmulDescCreate(&p->desc, HIPBLAS_COMPUTE_32F, HIP_R_32F);
   if (st != HIPBLAS_STATUS_SUCCESS) return 1000 + (int)st;
   hipblasOperation_t ta = HIPBLAS_OP_T, tb = HIPBLAS_OP_N;
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
-  hipblasLtMatmulDescSetAttribute(p.desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
+  hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSA, &ta, sizeof(ta));
+  hipblasLtMatmulDescSetAttribute(p->desc, HIPBLASLT_MATMUL_DESC_TRANSB, &tb, sizeof(tb));
   // A: K x N (lda = K), B: K x M (ldb = ldx), C/D: N x M (ldc = ldy)
-  if (hipblasLtMatrixLayoutCreate(&p.a, HIP_R_16BF, k.K, k.N, k.K) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.b, HIP_R_16BF, k.K, k.M, k.ldx) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p.c, HIP_R_16BF, k.N, k.M, k.ldy) != HIPBLAS_STATUS_SUCCESS)
+  if (hipblasLtMatrixLayoutCreate(&p->a, HIP_R_16BF, k.K, k.N, k.K) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p->b, HIP_R_16BF, k.K, k.M, k.ldx) != HIPBLAS_STATUS_SUCCESS ||
+      hipblasLtMatrixLayoutCreate(&p->c, HIP_R_16BF, k.N, k.M, k.ldy) != HIPBLAS_STATUS_SUCCESS)
     return 1100;
+  return 0;
+}
+
+int heuristic(const Plan& p, size_t ws_limit, int want, hipblasLtMatmulHeuristicResult_t* res, int* n) {
   hipblasLtMatmulPreference_t pref;
   hipblasLtMatmulPreferenceCreate(&pref);
   uint64_t wsl = ws_limit;
   hipblasLtMatmulPreferenceSetAttribute(pref, HIPBLASLT_MATMUL_PREF_MAX_WORKSPACE_BYTES, &wsl, sizeof(wsl));
+  hipblasStatus_t st = hipblasLtMatmulAlgoGetHeuristic(g_handle, p.desc, p.a, p.b, p.c, p.c, pref, want, res, n);
+  hipblasLtMatmulPreferenceDestroy(pref);
+  return (st != HIPBLAS_STATUS_SUCCESS || *n < 1) ? 1200 + (int)st : 0;
+}
+
+int build_plan(const Key& k, size_t ws_limit, Plan* out) {
+  Plan p;
+  int rc = make_desc(k, &p);
+  if (rc) return rc;
+  auto t = g_tuned.find({k.N, k.K});
+  if (t != g_tuned.end() && !t->second.empty()) {
+    auto it = t->second.upper_bound(k.M);  // first ladder M > M
+    hipblasLtMatmulAlgo_t algo;
+    size_t wsz = 0;
+    const float alpha = 1.f, beta = 0.f;
+    if (it != t->second.begin() && (algo = std::prev(it)->second, true) &&
+        hipblaslt_ext::matmulIsAlgoSupported(g_handle, p.desc, &alpha, p.a, p.b, &beta, p.c, p.c, algo, wsz) ==
+            HIPBLAS_STATUS_SUCCESS &&
+        wsz <= ws_limit) {
+      p.algo = algo;
+      p.ws = wsz;
+      *out = p;
+      return 0;
+    }
+  }
   hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
-  st = hipblasLtMatmulAlgoGetHeuristic(g_handle, p.desc, p.a, p.b, p.c, p.c, pref, 1, res, &n);
-  hipblasLtMatmulPreferenceDestroy(pref);
-  if (st != HIPBLAS_STATUS_SUCCESS || n < 1) return 1200 + (int)st;
+  rc = heuristic(p, ws_limit, 1, res, &n);
+  if (rc) return rc;
   p.algo = res[0].algo;
   p.ws = res[0].workspaceSize;
   *out = p;
@@ -115,4 +154,75 @@ K8S_API int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int 
 K8S_API int k8s_blaslt_num_plans() {
   std::lock_guard<std::mutex> g(g_mu);
   return (int)g_plans.size();
+}
+
+// Time the heuristic's top `max_algos` solutions for this problem (`iters`
+// launches each on stream s, after 2 warm-up launches) and keep the fastest
+// for (N, K) at ladder point M.  Plans already built for (N, K) are dropped so
+// later calls re-plan against the tuned table (their descriptors are kept
+// alive: a concurrent caller may still hold one).  Not capturable (events +
+// synchronisation): call at init, before any HIP-graph capture.
+// times[0] = heuristic first choice (us), times[1] = chosen (us).
+// Returns the chosen candidate's rank in the heuristic list, or < 0 on error.
+K8S_API int k8s_blaslt_tune(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
+                            size_t ws_bytes, int max_algos, int iters, hipStream_t s, float* times) {
+  if (M <= 0 || N <= 0 || K <= 0 || ldx < K || ldy < N || max_algos < 1 || iters < 1) return -(int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return -900;
+  const Key key{M, N, K, ldx, ldy};
+  Plan p;
+  int rc = make_desc(key, &p);
+  if (rc) return -rc;
+  std::vector<hipblasLtMatmulHeuristicResult_t> res(max_algos);
+  int n = 0;
+  rc = heuristic(p, ws_bytes, max_algos, res.data(), &n);
+  if (rc) return -rc;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -901;
+  const float alpha = 1.f, beta = 0.f;
+  int best = -1;
+  float best_us = 0.f, first_us = -1.f;
+  for (int i = 0; i < n; ++i) {
+    if (res[i].workspaceSize > ws_bytes) continue;
+    bool ok = true;
+    for (int r = 0; r < 2 && ok; ++r)
+      ok = hipblasLtMatmul(g_handle, p.desc, &alpha, w, p.a, x, p.b, &beta, y, p.c, y, p.c, &res[i].algo, ws,
+                           res[i].workspaceSize, s) == HIPBLAS_STATUS_SUCCESS;
+    if (!ok || hipStreamSynchronize(s) != hipSuccess) continue;
+    hipEventRecord(e0, s);
+    for (int r = 0; r < iters; ++r)
+      hipblasLtMatmul(g_handle, p.desc, &alpha, w, p.a, x, p.b, &beta, y, p.c, y, p.c, &res[i].algo, ws,
+                      res[i].workspaceSize, s);
+    hipEventRecord(e1, s);
+    if (hipEventSynchronize(e1) != hipSuccess) continue;
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    const float us = 1000.f * ms / iters;
+    if (i == 0) first_us = us;
+    if (best < 0 || us < best_us) {
+      best = i;
+      best_us = us;
+    }
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  if (best < 0) return -1500;
+  g_tuned[{N, K}][M] = res[best].algo;
+  for (auto it = g_plans.begin(); it != g_plans.end();) {
+    if (it->first.N == N && it->first.K == K)
+      it = g_plans.erase(it);  // descriptors intentionally not destroyed (see above)
+    else
+      ++it;
+  }
+  if (times) {
+    times[0] = first_us;
+    times[1] = best_us;
+  }
+  return best;
+}
+
+K8S_API void k8s_blaslt_clear_tuning() {
+  std::lock_guard<std::mutex> g(g_mu);
+  g_tuned.clear();
+  g_plans.clear();
 }

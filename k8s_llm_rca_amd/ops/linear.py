@@ -104,6 +104,72 @@ def reserve_lib_workspace(dev: torch.device) -> None:
         _blaslt_ws[dev] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=dev)
 
 
+# ------------------------------------------------ hipBLASLt solution tuning
+# Prefill-sized projections (M >= 256) always run on hipBLASLt (the hand-written
+# kernels lose there: profiles/r1_prefill_gemm_sweep.txt).  The heuristic's
+# first solution is not always the fastest it lists at these M, so at engine
+# init each projection (N, K) is timed at a ladder of M over the heuristic's top
+# candidates and the fastest is kept natively (csrc/kernels/blaslt.hip); any
+# later M uses the solution tuned at the largest ladder M <= M.  Off by default
+# (EngineConfig.tune_lib_gemms): end to end it lost 4 % on the headline config.
+TUNE_LADDER = (256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)
+_tuned_report: List[tuple] = []
+_tuned_done: set = set()
+
+
+def projection_shapes(mc, tp: int = 1) -> List[Tuple[int, int]]:
+    """(N, K) of the dense projections hipBLASLt runs at prefill M (per TP rank)."""
+    H, I = mc.hidden, mc.intermediate
+    qkv = (mc.n_heads + 2 * mc.n_kv_heads) * mc.head_dim // tp
+    out = [(qkv, H), (H, mc.n_heads * mc.head_dim // tp)]
+    if not getattr(mc, "n_experts", 0):
+        out += [(2 * I // tp, H), (H, I // tp)]
+    return out
+
+
+def tune_lib_gemms(dev: torch.device, shapes, max_m: int = 8192, max_algos: int = 24, iters: int = 5) -> List[tuple]:
+    """Time hipBLASLt's top ``max_algos`` solutions for every (N, K) in
+    ``shapes`` at each ladder M <= ``max_m`` and keep the fastest (native
+    table).  Call before any HIP-graph capture.  Returns
+    ``[(M, N, K, heuristic_us, tuned_us, rank)]``."""
+    import ctypes
+    if not (_native_lib_gemm and dev.type == "cuda"):
+        return []
+    reserve_lib_workspace(dev)
+    ws = _blaslt_ws[dev]
+    out = []
+    times = (ctypes.c_float * 2)()
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(0)
+    for N, K in shapes:
+        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=gen) * 0.02
+        for M in TUNE_LADDER:
+            if M > max_m:
+                break
+            if (dev, M, N, K) in _tuned_done:  # an earlier engine in this process
+                continue
+            _tuned_done.add((dev, M, N, K))
+            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=gen)
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            torch.cuda.synchronize(dev)
+            rank = lib().k8s_blaslt_tune(ptr(x), K, ptr(w), ptr(y), N, M, N, K, ptr(ws), BLASLT_WS_BYTES, max_algos,
+                                         iters, stream_ptr(x), times)
+            if rank < 0:
+                raise RuntimeError(f"k8s_blaslt_tune({M}, {N}, {K}) failed: {rank}")
+            out.append((M, N, K, round(times[0], 2), round(times[1], 2), rank))
+            del x, y
+        del w
+    torch.cuda.synchronize(dev)
+    _tuned_report[:] = out
+    return out
+
+
+def clear_lib_tuning() -> None:
+    lib().k8s_blaslt_clear_tuning()
+    _tuned_report.clear()
+    _tuned_done.clear()
+
+
 # ------------------------------------------------------- measured dispatch
 # data/gemm_dispatch_<model>.json (tools/gemm_mid_sweep.py --emit): for each
 # (N, K) projection, per M bucket, the fastest of hipBLASLt / skinny / a

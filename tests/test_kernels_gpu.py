@@ -379,3 +379,24 @@ def test_grouped_gemm_matches_per_expert(E, N, K, fuse, splits):
     got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), fuse_silu=fuse, splits=splits).float().cpu()
     ref = MO.grouped_gemm(a, w, offs, fuse_silu=fuse).float()
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
+
+
+def test_blaslt_tuned_solutions():
+    """Measured hipBLASLt solutions (k8s_blaslt_tune): the tuned table serves
+    M on and between ladder points, results match fp32, and below the ladder
+    (decode sizes) the heuristic's plan is used."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(11)
+    N, K = 1536, 2048
+    rep = LIN.tune_lib_gemms(torch.device(dev), [(N, K)], max_m=512, max_algos=8, iters=2)
+    assert [r[0] for r in rep] == [256, 384, 512]
+    assert all(r[4] <= r[3] + 1e-3 and r[5] >= 0 for r in rep)
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    try:
+        for M in (64, 256, 300, 512, 777):
+            x = torch.randn(M, K, device=dev).bfloat16()
+            y = LIN.lib_gemm(x, w)
+            torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    finally:
+        LIN.clear_lib_tuning()

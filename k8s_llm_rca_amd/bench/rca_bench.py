@@ -286,4 +286,11 @@ def main(argv=None) -> int:
     res = run(args)
     if res is not None:
         print(json.dumps(res), flush=True)
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized():
+        # Orderly teardown: no rank exits while a peer's gloo/RCCL background
+        # threads still reference it (an abort at exit fails the torchrun job).
+        dist.barrier()
+        dist.destroy_process_group()
     return 0

@@ -9,6 +9,9 @@ import os
 import sys
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+# Kernel arguments in device memory: with it explicitly off the headline drops
+# 6.03 -> 5.91 analyses/s (profiles/README.md); pin it on unless the caller says otherwise.
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 
 from k8s_llm_rca_amd.bench.rca_bench import main  # noqa: E402
 

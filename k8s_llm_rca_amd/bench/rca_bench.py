@@ -1,14 +1,20 @@
 """RCA benchmark: analyses/s and p50 end-to-end latency (BASELINE.json headline).
 
-One *step* = ``incidents`` RCA analyses (locate -> generate query -> analyze,
-the full reference pipeline) on this rank's engine against this rank's
-synthetic k8s graph, by ``incidents`` concurrent pipelines.  The timed K steps'
-K x incidents analyses stream through those pipelines as one work queue (a
-pipeline takes its next incident as soon as it finishes one, like the CLI's
-``run --concurrency``); ``--sync-steps`` drains every step first instead.  Ranks are independent engine
-replicas (data parallel, one process per GPU, TP=1): per-GPU work is fixed as
-N grows (weak scaling).  Timing brackets exactly ``steps`` batches with a
-barrier + device synchronize on both sides and takes the max over ranks.
+Each rank runs ``--incidents`` (128) concurrent RCA pipelines (locate ->
+generate query -> analyze, the full reference pipeline,
+``test_with_file.py:64-204``) on its own engine against its own synthetic k8s
+graph, as a steady stream: a pipeline takes its next incident the moment it
+finishes one.  One *step* is a fixed quantum (``--quantum``, 16) of completed
+analyses per rank: ``--warmup`` steps stream untimed, then exactly ``--steps``
+quanta are timed with a barrier + device synchronize on both sides and the max
+over ranks is taken.  Ranks are independent engine replicas (data parallel,
+one process per GPU, TP=1: weak scaling), or one tensor-parallel engine over
+all ranks (``--tp``: strong scaling).  ``bench.py --gpus N`` spawns the N
+ranks itself when no launcher did.  A wall-clock budget stops the run and
+still prints the JSON line (flagged).  After the timed window the same stream
+is optionally measured with the oracle hints off (``no_hints`` in the line).
+The graph is built at ``--graph-nodes`` including the injected faults; the
+stream cycles the distinct incidents.
 """
 from __future__ import annotations
 
@@ -71,8 +77,8 @@ def _allgather_list(xs: List[float], world: int, device) -> List[float]:
 def run(args) -> Optional[Dict[str, Any]]:
     logging.basicConfig(level=logging.WARNING)
     world, rank = _dist_init()
-    if args.gpus and world > 1 and args.gpus != world:
-        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (bench.py spawns the ranks itself)")
     cuda = torch.cuda.is_available() and args.device != "cpu"
     device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}" if cuda else "cpu")
     if cuda:
@@ -82,14 +88,20 @@ def run(args) -> Optional[Dict[str, Any]]:
     from ..api.service import AssistantService
     from ..engine.backend import EngineBackend
     from ..engine.engine import EngineConfig, LLMEngine
-    from ..graph.synth import generate_cluster
+    from ..graph.synth import NODES_PER_INCIDENT, generate_cluster
     from ..pipeline.formats import GenerationBudget
-    from ..pipeline.rca import RCAConfig, RCAPipeline, run_batch
+    from ..pipeline.rca import IncidentStream, RCAConfig, RCAPipeline
     from ..utils import tracing
 
-    n_steps, n_warm, per_step = args.steps, args.warmup, args.incidents
-    t_setup = time.perf_counter()
-    cluster = generate_cluster(args.graph_nodes, per_step * (n_steps + n_warm), seed=args.seed + 7919 * rank)
+    t_start = time.perf_counter()
+    deadline = t_start + args.time_budget if args.time_budget else None
+    n_steps, n_warm, quantum, conc = args.steps, args.warmup, args.quantum, args.incidents
+    nh_steps = 0 if args.no_hints else args.no_hints_steps
+    # distinct incidents: enough that no two concurrent pipelines share one, capped
+    # so the injected faults stay within the graph-size target (the stream cycles them)
+    need = (n_warm + n_steps + nh_steps) * quantum + 2 * conc
+    n_inc = max(1, min(need, int(0.3 * args.graph_nodes / NODES_PER_INCIDENT)))
+    cluster = generate_cluster(args.graph_nodes, n_inc, seed=args.seed + 7919 * rank)
     if cuda and args.graph_device:
         from ..graph.device import to_device
         to_device(cluster.stategraph, device)
@@ -118,17 +130,24 @@ def run(args) -> Optional[Dict[str, Any]]:
     cfg = RCAConfig(model=args.model, hints=not args.no_hints, budget=budget)
     meta_qe = GraphQueryExecutor(cluster.metagraph)
     state_qe = GraphQueryExecutor(cluster.stategraph)
-    pipelines = [RCAPipeline(svc, meta_qe, state_qe, cfg) for _ in range(per_step)]
-    setup_s = time.perf_counter() - t_setup
+    pipelines = [RCAPipeline(svc, meta_qe, state_qe, cfg) for _ in range(conc)]
+    setup_s = time.perf_counter() - t_start
 
-    incidents = cluster.incidents
-    lat: List[float] = []
-    errors: List[str] = []
-    n_done = 0
-    for w in range(n_warm):
-        chunk = incidents[w * per_step:(w + 1) * per_step]
-        st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
-        errors += st.errors
+    last = [time.perf_counter()]
+
+    def _poll():
+        if eng.error is not None:
+            raise RuntimeError(f"engine fault: {eng.error!r}")
+        now = time.perf_counter()
+        if now - last[0] >= 20.0 and rank == 0:  # progress on stderr (a silent run looks hung)
+            last[0] = now
+            print(f"[bench] t={now - t_start:.0f}s completed={stream.n_ok} errors={stream.n_err} "
+                  f"engine_steps={eng.stats['steps']}", file=sys.stderr, flush=True)
+
+    # ---- warm-up: W quanta of completed analyses from the running stream
+    stream = IncidentStream(pipelines, cluster.incidents, hints=not args.no_hints)
+    stream.start()
+    truncated = not stream.wait_ok(n_warm * quantum, deadline, _poll)
     tracing.reset()
     if not args.no_gc_freeze:
         # the graph store, model config, grammar tables and warm-up results are
@@ -138,27 +157,38 @@ def run(args) -> Optional[Dict[str, Any]]:
         import gc
         gc.collect()
         gc.freeze()
+    sync_world = 1 if tp_mode else world
+    # ---- timed: exactly K quanta of completed analyses, barrier + sync on both sides
+    _barrier(sync_world, device)
     stats0 = dict(eng.stats)
     eng.kv.reset_peak()
     t_wall0 = time.time()
-    sync_world = 1 if tp_mode else world
-    _barrier(sync_world, device)
     t0 = time.perf_counter()
-    if args.sync_steps:  # batch-synchronous: every step drains before the next starts
-        for s in range(n_steps):
-            chunk = incidents[(n_warm + s) * per_step:(n_warm + s + 1) * per_step]
-            st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
-            lat += st.latencies
-            errors += st.errors
-            n_done += len(st.results)
-    else:  # streaming: the K steps' incidents feed one work queue of `incidents` concurrent pipelines
-        chunk = incidents[n_warm * per_step:(n_warm + n_steps) * per_step]
-        st = run_batch(None, [i.message for i in chunk], truths=chunk, pipelines=pipelines)
-        lat += st.latencies
-        errors += st.errors
-        n_done += len(st.results)
+    base = stream.n_ok
+    done_all = stream.wait_ok(base + n_steps * quantum, deadline, _poll)
+    t_end = time.perf_counter()
+    n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
+    truncated = truncated or not done_all
+    d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    lat = stream.window(t0, t_end + 1e-9)
+    err_timed = sum(1 for t, _, ok in list(stream.done) if not ok and t0 <= t <= t_end)
+    # ---- optional no-hints window (disclosure): the same engine and stream with the
+    # oracle hints off, timed after one full turnover of the in-flight analyses
+    nh = None
+    if nh_steps and not truncated:
+        cfg.hints = False
+        stream.hints = False
+        n_switch = stream.n_ok + conc
+        if stream.wait_ok(n_switch, deadline, _poll):
+            t_nh0 = time.perf_counter()
+            if stream.wait_ok(n_switch + nh_steps * quantum, deadline, _poll):
+                dt = time.perf_counter() - t_nh0
+                nh_lat = stream.window(t_nh0, time.perf_counter())
+                nh = {"value": round(nh_steps * quantum * sync_world / dt, 4), "steps": nh_steps,
+                      "p50_latency_s": round(statistics.median(nh_lat), 3) if nh_lat else None}
+    stream.stop()
     eng.stop()
     eng.stop_workers()
     if eng.error is not None:
@@ -166,8 +196,7 @@ def run(args) -> Optional[Dict[str, Any]]:
     max_elapsed = _allreduce_max(elapsed, sync_world, device)
     all_lat = _allgather_list(lat, sync_world, device)
     total = n_done * sync_world
-    value = total / max_elapsed
-    d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    value = total / max_elapsed if max_elapsed > 0 else 0.0
     ttft = sorted(rs.metrics["ttft_s"] for rs in list(svc.runs.values())
                   if rs.run.created_at >= t_wall0 and "ttft_s" in rs.metrics)
     p50 = statistics.median(all_lat) if all_lat else 0.0
@@ -190,38 +219,40 @@ def run(args) -> Optional[Dict[str, Any]]:
         "dtype": "bf16" if cuda else "fp32",
         "data": "synthetic k8s stategraph (seeded generator, fault injection) + random-init weights",
         "config": {"model": model_name,
-                   "global_batch": per_step * sync_world, "seq_len": eng.max_context,
+                   "global_batch": conc * sync_world, "seq_len": eng.max_context,
                    "parallelism": f"tp{world}" if tp_mode else f"dp{world}",
-                   "graph_nodes": cluster.stategraph.num_nodes,
-                   "incidents_per_gpu_per_step": per_step, "grammar_hints": not args.no_hints,
-                   "step_mode": "sync" if args.sync_steps else "stream"},
+                   "graph_nodes": cluster.stategraph.num_nodes, "graph_nodes_target": args.graph_nodes,
+                   "distinct_incidents": len(cluster.incidents),
+                   "concurrent_analyses_per_gpu": conc, "analyses_per_step": quantum * sync_world,
+                   "grammar_hints": not args.no_hints, "step_mode": "stream"},
         "p50_latency_s": round(p50, 3),
         "p90_latency_s": round(p90, 3),
-        "errors": len(errors),
-        "engine": {"steps": d["steps"], "graph_steps": d["graph_steps"], "prefill_tokens": d["prefill_tokens"],
-                   "decode_tokens": d["decode_tokens"], "sampled_tokens": d["sampled_tokens"],
-                   "forced_tokens": d["forced_tokens"], "forward_s": round(d["forward_s"], 3),
-                   "sample_s": round(d["sample_s"], 3), "host_s": round(d["host_s"], 3),
-                   "evictions": d["evictions"], "requests": d["requests"],
+        "analyses_timed": total,
+        "errors": err_timed,
+        "errors_total": stream.n_err,
+        "truncated_by_time_budget": truncated,
+        "tokens": {"sampled": d["sampled_tokens"], "forced": d["forced_tokens"], "prefill": d["prefill_tokens"],
+                   "decode_rows": d["decode_tokens"]},
+        "no_hints": nh,
+        "engine": {"steps": d["steps"], "graph_steps": d["graph_steps"],
+                   "forward_s": round(d["forward_s"], 3), "sample_s": round(d["sample_s"], 3),
+                   "host_s": round(d["host_s"], 3), "evictions": d["evictions"],
+                   "preemptions": d.get("preemptions", 0), "requests": d["requests"],
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
-                   "post_s": round(d["post_s"], 3), "admit_s": round(d["admit_s"], 3),
                    "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,
-                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
-                   **{k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}},
+                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3)},
         "throughput": {  # rank 0's engine over the timed window
             "prefill_tok_per_s": round(d["prefill_tokens"] / elapsed, 1),
             "decode_tok_per_s": round(d["decode_tokens"] / elapsed, 1),
+            "sampled_tok_per_s": round(d["sampled_tokens"] / elapsed, 1),
             "forced_tok_per_s": round(d["forced_tokens"] / elapsed, 1),
             "avg_decode_batch": round(d["decode_tokens"] / max(1, d["steps"]), 1),
             "runs": len(ttft),
             "ttft_p50_s": round(ttft[len(ttft) // 2], 4) if ttft else None,
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         "setup_s": round(setup_s, 1),
-        "blaslt_tune": ({"s": round(eng.t_gemm_tune, 2), "points": len(eng.gemm_tuning),
-                         "heuristic_us": round(sum(t[3] for t in eng.gemm_tuning), 1),
-                         "tuned_us": round(sum(t[4] for t in eng.gemm_tuning), 1)}
-                        if getattr(eng, "gemm_tuning", None) else None),
+        "wall_s": round(time.perf_counter() - t_start, 1),
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }
     if world > 1 and not tp_mode:
@@ -232,14 +263,21 @@ def run(args) -> Optional[Dict[str, Any]]:
 
 def parser() -> argparse.ArgumentParser:
     p = argparse.ArgumentParser(description=__doc__)
-    p.add_argument("--gpus", type=int, default=None, help="GPUs (= WORLD_SIZE under torchrun; default 1)")
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs = ranks; without torchrun's WORLD_SIZE, bench.py spawns this many rank processes")
     p.add_argument("--preset", default=None, choices=sorted(PRESETS), help="a BASELINE.json config")
-    p.add_argument("--steps", type=int, default=2)
-    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10, help="timed steps; one step = --quantum completed analyses per GPU")
+    p.add_argument("--warmup", type=int, default=3, help="untimed steps streamed before the timer starts")
+    p.add_argument("--quantum", type=int, default=16, help="completed analyses per GPU per step")
+    p.add_argument("--time-budget", type=float, default=360.0,
+                   help="seconds after start at which the stream stops waiting and the JSON is printed anyway "
+                        "(flagged truncated_by_time_budget); 0 = none")
+    p.add_argument("--no-hints-steps", type=int, default=3,
+                   help="after the timed window, steps measured with the oracle hints off (0 = skip)")
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (one engine over all ranks)")
     p.add_argument("--device", default="cuda")
-    p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses per GPU per step")
+    p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses (pipelines) per GPU")
     p.add_argument("--graph-nodes", type=int, default=10_000)
     p.add_argument("--graph-device", action="store_true", help="mirror the stategraph to HBM (HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
@@ -253,9 +291,6 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--no-hints", action="store_true")
     p.add_argument("--no-graphs", action="store_true")
     p.add_argument("--no-gc-freeze", action="store_true", help="keep warm-up objects in the GC generations")
-    p.add_argument("--sync-steps", action="store_true",
-                   help="drain each step's batch before starting the next (default: the K steps' incidents stream "
-                        "through the same concurrent pipelines, as `run --concurrency` processes a message file)")
     p.add_argument("--no-prefix-sharing", action="store_true", help="do not share prompt KV pages across threads")
     return p
 
@@ -263,7 +298,8 @@ def parser() -> argparse.ArgumentParser:
 # One preset per BASELINE.json config; explicit flags override.
 PRESETS: Dict[str, Dict[str, Any]] = {
     # "OPT-125m CPU backend, 10-node toy k8s dependency graph, single pod-crash RCA (plumbing, no GPU)"
-    "opt125m-cpu-toy": dict(model="opt-125m", device="cpu", graph_nodes=10, incidents=1),
+    "opt125m-cpu-toy": dict(model="opt-125m", device="cpu", graph_nodes=10, incidents=1, quantum=1, steps=1,
+                            warmup=0, no_hints_steps=0, time_budget=0),
     # the headline: "RCA analyses/sec + p50 latency, Llama-3-8B backend, 10k-node graph"
     "llama3-8b-10k": dict(model="llama3-8b", graph_nodes=10_000),
     # "Llama-3-8B TP=1 bf16 on one MI355X, 1k-node synthetic k8s graph"
@@ -277,12 +313,61 @@ PRESETS: Dict[str, Dict[str, Any]] = {
 }
 
 
+def _free_port() -> int:
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def spawn_ranks(n: int, argv: List[str]) -> int:
+    """``bench.py --gpus N`` without a launcher: start N rank processes (one per
+    GPU, torchrun's env contract, rendezvous on 127.0.0.1) and wait for them.
+    Runs before anything in this process touches the GPU; the ranks are
+    children, never an exec of this process.  Rank 0 prints the JSON line."""
+    import subprocess
+    port = _free_port()
+    script = os.path.abspath(sys.argv[0]) if sys.argv and sys.argv[0].endswith(".py") else None
+    cmd = [sys.executable, script] if script else [sys.executable, "-m", "k8s_llm_rca_amd.bench.rca_bench"]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   GROUP_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        procs.append(subprocess.Popen(cmd + list(argv), env=env))
+    rc = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for pr in list(pending):
+                code = pr.poll()
+                if code is None:
+                    continue
+                pending.remove(pr)
+                if code != 0:
+                    rc = rc or code
+                    for other in pending:  # one rank died: the collective would hang the rest
+                        other.terminate()
+            time.sleep(0.2)
+    finally:
+        for pr in procs:
+            if pr.poll() is None:
+                pr.kill()
+    return rc
+
+
 def main(argv=None) -> int:
+    argv = list(sys.argv[1:] if argv is None else argv)
     p = parser()
     pre, _ = p.parse_known_args(argv)
     if pre.preset:
         p.set_defaults(**PRESETS[pre.preset])
     args = p.parse_args(argv)
+    if args.gpus and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        return spawn_ranks(args.gpus, argv)
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    if args.tp > world:
+        logging.warning("--tp %d > %d ranks: running TP=%d", args.tp, world, world)
+        args.tp = world
     res = run(args)
     if res is not None:
         print(json.dumps(res), flush=True)
@@ -294,3 +379,16 @@ def main(argv=None) -> int:
         dist.barrier()
         dist.destroy_process_group()
     return 0
+
+
+def exit_now(rc: int) -> None:
+    """Leave without interpreter teardown: the stream's pipeline threads are
+    still parked on runs the stopped engine will never finish, and tearing the
+    runtime down under them aborts the process (exit 134) after the JSON line."""
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(rc)
+
+
+if __name__ == "__main__":
+    exit_now(main())

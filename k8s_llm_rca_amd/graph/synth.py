@@ -36,6 +36,7 @@ from .store import PropertyGraph, ms_to_ts, ts_to_ms
 T0 = ts_to_ms("2020-12-10 00:00:00.000")
 WINDOW_MS = 4 * 24 * 3600 * 1000
 FOREVER = "9999-12-31 23:59:59.999"
+NODES_PER_INCIDENT = 2.85  # measured mean over FAULT_TYPES (Event + EVENT + re-stated / dangling object)
 
 FAULT_TYPES = [
     "quota_pods", "nfs_missing", "secret_missing", "configmap_missing", "cni_failure",
@@ -167,7 +168,9 @@ class _Gen:
 
 def generate_cluster(target_nodes: int = 10_000, n_incidents: int = 64, seed: int = 0,
                      fault_mix: Optional[List[str]] = None) -> SynthCluster:
-    """Build a stategraph of roughly ``target_nodes`` nodes with ``n_incidents`` faults."""
+    """Build a stategraph of ``target_nodes`` nodes (+- half a tenant, faults included) with
+    ``n_incidents`` faults; at most ~30 % of the target is spent on fault nodes, beyond that the
+    graph grows past the target (callers cycle a smaller incident set instead)."""
     from .schema import build_metagraph
 
     G = _Gen(seed)
@@ -189,132 +192,153 @@ def generate_cluster(target_nodes: int = 10_000, n_incidents: int = 64, seed: in
                      spec={"provisioner": "cluster.local/nfs-client-provisioner"})
     nfs_server = "172.16.112.63"
 
-    # per-namespace tenants until the node budget is used
-    tenants = []
-    while g.num_nodes < target_nodes * 0.92:
-        user = f"{_USERS[int(rng.integers(len(_USERS)))]}{int(rng.integers(1, 99))}"
-        ns_name = G.unique(user)
-        t_ns = T0 - WINDOW_MS + int(rng.integers(0, WINDOW_MS // 2))
-        ns, _ = G.entity("Namespace", ns_name, None, t_ns, status={"phase": "Active"})
-        quota_name = f"compute-resources-{ns_name}"
-        quota, _ = G.entity("ResourceQuota", quota_name, ns_name, t_ns,
-                            spec={"hard": {"pods": "50", "limits.memory": "1800Gi"}},
-                            status={"hard": {"pods": "50", "limits.memory": "1800Gi"},
-                                    "used": {"pods": str(int(rng.integers(5, 40))),
-                                             "limits.memory": f"{int(rng.integers(100, 900))}Gi"}})
-        G.ref(quota, ns, "metadata_namespace")
-        tok = f"default-token-{G.suffix(5)}"
-        sa_secret, _ = G.entity("Secret", tok, ns_name, t_ns, spec=None,
-                                status=None, extra_meta={"type": "kubernetes.io/service-account-token"})
-        G.ref(sa_secret, ns, "metadata_namespace")
-        sa, _ = G.entity("ServiceAccount", "default", ns_name, t_ns)
-        G.ref(sa, ns, "metadata_namespace")
-        G.ref(sa, sa_secret, "secrets_name")
-        tenant = {"ns": ns, "ns_name": ns_name, "quota": quota, "quota_name": quota_name, "sa": sa,
-                  "sa_secret": sa_secret, "tok": tok, "pods": [], "jobs": [], "sts": [], "pvc_pods": []}
-        n_apps = int(rng.integers(2, 7))
-        for _ in range(n_apps):
-            kind = rng.choice(["deploy", "deploy", "sts", "cron"])
-            app = G.unique(f"{G.word()}-{G.word()}-{ns_name}" if rng.random() < 0.3 else f"{G.word()}-{G.word()}")
-            t_app = t_ns + int(rng.integers(0, WINDOW_MS // 4))
-            cm, _ = G.entity("ConfigMap", f"{app}-configmap", ns_name, t_app,
-                             extra_meta={"labels": {"app": app}})
-            G.ref(cm, ns, "metadata_namespace")
-            sec, _ = G.entity("Secret", f"{app}-secret", ns_name, t_app)
-            G.ref(sec, ns, "metadata_namespace")
-            svc, _ = G.entity("Service", app, ns_name, t_app, spec={"ports": [{"port": 8080}], "selector": {"app": app}})
-            G.ref(svc, ns, "metadata_namespace")
-            ep, _ = G.entity("Endpoints", app, ns_name, t_app)
-            G.ref(ep, svc, "metadata_name")
-            image_v = f"registry.local/{app}:v{int(rng.integers(1, 9))}.{int(rng.integers(0, 20))}"
-            img, _ = G.external("image", image_v, t_app, state_props={"imageName": image_v})
-            if kind == "deploy":
-                dep, _ = G.entity("Deployment", app, ns_name, t_app, spec={"replicas": 2})
-                G.ref(dep, ns, "metadata_namespace")
-                rs_name = f"{app}-{G.suffix(10)}"
-                owner, _ = G.entity("ReplicaSet", rs_name, ns_name, t_app, spec={"replicas": 2})
-                G.ref(owner, dep, "metadata_ownerReferences_uid")
-                G.ref(owner, ns, "metadata_namespace")
-                pod_names = [f"{rs_name}-{G.suffix(5)}" for _ in range(2)]
-            elif kind == "sts":
-                owner, _ = G.entity("StatefulSet", app, ns_name, t_app, spec={"replicas": 2, "serviceName": app})
-                G.ref(owner, ns, "metadata_namespace")
-                G.ref(owner, svc, "spec_serviceName")
-                tenant["sts"].append((owner, app))
-                pod_names = [f"{app}-{i}" for i in range(2)]
-            else:
-                cj, _ = G.entity("CronJob", f"{app}-cronjob", ns_name, t_app, spec={"schedule": "*/5 * * * *"})
-                G.ref(cj, ns, "metadata_namespace")
-                stamp = 1607600000 + int(rng.integers(0, 300000))
-                owner, _ = G.entity("Job", f"{app}-cronjob-{stamp}", ns_name, t_app, spec={"completions": 1})
-                G.ref(owner, cj, "metadata_ownerReferences_uid")
-                G.ref(owner, ns, "metadata_namespace")
-                tenant["jobs"].append((owner, f"{app}-cronjob-{stamp}"))
-                pod_names = [f"{app}-cronjob-{stamp}-{G.suffix(5)}"]
-            for pn in pod_names:
-                node = k8s_nodes[int(rng.integers(len(k8s_nodes)))]
-                vol_cfg = f"{app}-conf"
-                spec = {"nodeName": g.node_props(node)["name2"], "serviceAccountName": "default",
-                        "containers": [{"name": app, "image": image_v}],
-                        "volumes": [{"name": vol_cfg, "configMap": {"name": f"{app}-configmap"}},
-                                    {"name": f"{app}-secret", "secret": {"secretName": f"{app}-secret"}},
-                                    {"name": tok, "secret": {"secretName": tok}}]}
-                pvc = pv = nfs = None
-                if kind == "sts":
-                    pvc_name = f"pvc-{app}-{pn}"
-                    pvc, pvc_uid = G.entity("PersistentVolumeClaim", pvc_name, ns_name, t_app,
-                                            spec={"storageClassName": "nfs-client"},
-                                            status={"phase": "Bound"})
-                    pv_name = f"pvc-{pvc_uid}"
-                    path = f"/mnt/k8s_nfs_pv/{ns_name}-{pvc_name}-{pv_name}"
-                    pv, _ = G.entity("PersistentVolume", pv_name, None, t_app,
-                                     spec={"nfs": {"server": nfs_server, "path": path},
-                                           "claimRef": {"uid": pvc_uid, "name": pvc_name}},
-                                     status={"phase": "Bound"})
-                    nfs, _ = G.external("nfs", path, t_app, state_props={"path": path, "server": nfs_server})
-                    G.ref(pvc, pv, "spec_volumeName")
-                    G.ref(pvc, sc, "spec_storageClassName")
-                    G.ref(pvc, ns, "metadata_namespace")
-                    G.ref(pv, pvc, "spec_claimRef_uid")
-                    G.ref(pv, sc, "spec_storageClassName")
-                    G.ref(pv, nfs, "spec_nfs_path", rel="UseExternal")
-                    spec["volumes"].append({"name": pv_name, "persistentVolumeClaim": {"claimName": pvc_name}})
-                pod, pod_uid = G.entity("Pod", pn, ns_name, t_app + 1000, spec=spec,
-                                        status={"phase": "Running", "hostIP": "172.16.0.1"})
-                G.ref(pod, node, "spec_nodeName")
-                G.ref(pod, ns, "metadata_namespace")
-                G.ref(pod, cm, "spec_volumes_configMap_name")
-                G.ref(pod, sec, "spec_volumes_secret_secretName")
-                G.ref(pod, sa_secret, "spec_volumes_secret_secretName")
-                G.ref(pod, sa, "spec_serviceAccountName")
-                G.ref(pod, owner, "metadata_ownerReferences_uid")
-                if pvc is not None:
-                    G.ref(pod, pvc, "spec_volumes_persistentVolumeClaim_claimName")
-                ctr, _ = G.external("container", app, t_app + 1000, state_props={"containerName": app})
-                G.ref(pod, ctr, "spec_containers_name", rel="UseExternal")
-                G.ref(pod, img, "spec_containers_image", rel="UseExternal")
-                G.ref(ep, pod, "subsets_addresses_targetRef_uid")
-                rec = {"pod": pod, "pod_uid": pod_uid, "name": pn, "node": node, "cm": cm, "sec": sec,
-                       "pvc": pvc, "pv": pv, "nfs": nfs, "app": app, "owner": owner}
-                tenant["pods"].append(rec)
-                if pvc is not None:
-                    tenant["pvc_pods"].append(rec)
-                # a normal lifecycle event per pod
-                G.event(pod, f"Successfully assigned {ns_name}/{pn} to {g.node_props(node)['name2']}",
-                        G.ts(t_app + 1000, t_app + 5000), "Scheduled", "Normal")
-        tenants.append(tenant)
+    # per-namespace tenants.  Every injected incident adds ~2.85 nodes (its Event
+    # entity + EVENT, plus a re-stated or dangling object), so the base is built
+    # to the target minus that reserve, the faults are injected, and tenants are
+    # added again until the final count lands on the target (+- half a tenant).
+    reserve = min(int(target_nodes * 0.3), int(NODES_PER_INCIDENT * n_incidents))
+    n0 = g.num_nodes
+    tenants = [_add_tenant(G, k8s_nodes, sc, nfs_server)]
+    while g.num_nodes + (g.num_nodes - n0) / len(tenants) < target_nodes - reserve:  # undershoot; topped up below
+        tenants.append(_add_tenant(G, k8s_nodes, sc, nfs_server))
+    tenant_size = (g.num_nodes - n0) / len(tenants)
+    app_size = max(1.0, (tenant_size - 8) / 4.0)  # a tenant = ~8 fixed nodes + 2..6 apps
 
     # ------------------------------------------------------------ incidents
     incidents: List[Incident] = []
-    tries = 0
+    tries = miss = 0
     while len(incidents) < n_incidents and tries < n_incidents * 20:
         tries += 1
-        fault = faults[len(incidents) % len(faults)]
+        # the scheduled type (uniform mix) on up to 5 random tenants, then the next
+        # type: a graph with no tenant able to host one fault type still fills up
+        fault = faults[(len(incidents) + miss // 5) % len(faults)]
         t = tenants[int(rng.integers(len(tenants)))]
         inc = _inject(G, t, fault, nfs_server)
-        if inc is not None:
+        if inc is None:
+            miss += 1
+        else:
             incidents.append(inc)
+            miss = 0
+    while g.num_nodes + 8 + app_size / 2 < target_nodes:  # top up with tenants sized to the remainder
+        n_apps = int(min(6, max(1, round((target_nodes - g.num_nodes - 8) / app_size))))
+        _add_tenant(G, k8s_nodes, sc, nfs_server, n_apps)
     return SynthCluster(stategraph=g.finalize(), metagraph=build_metagraph(), incidents=incidents, seed=seed)
+
+
+def _add_tenant(G: _Gen, k8s_nodes: List[int], sc: int, nfs_server: str, n_apps: Optional[int] = None) -> dict:
+    """One namespace: quota, service-account token, 2-6 apps (deploy / sts / cron) with their pods."""
+    g, rng = G.g, G.rng
+    user = f"{_USERS[int(rng.integers(len(_USERS)))]}{int(rng.integers(1, 99))}"
+    ns_name = G.unique(user)
+    t_ns = T0 - WINDOW_MS + int(rng.integers(0, WINDOW_MS // 2))
+    ns, _ = G.entity("Namespace", ns_name, None, t_ns, status={"phase": "Active"})
+    quota_name = f"compute-resources-{ns_name}"
+    quota, _ = G.entity("ResourceQuota", quota_name, ns_name, t_ns,
+                        spec={"hard": {"pods": "50", "limits.memory": "1800Gi"}},
+                        status={"hard": {"pods": "50", "limits.memory": "1800Gi"},
+                                "used": {"pods": str(int(rng.integers(5, 40))),
+                                         "limits.memory": f"{int(rng.integers(100, 900))}Gi"}})
+    G.ref(quota, ns, "metadata_namespace")
+    tok = f"default-token-{G.suffix(5)}"
+    sa_secret, _ = G.entity("Secret", tok, ns_name, t_ns, spec=None,
+                            status=None, extra_meta={"type": "kubernetes.io/service-account-token"})
+    G.ref(sa_secret, ns, "metadata_namespace")
+    sa, _ = G.entity("ServiceAccount", "default", ns_name, t_ns)
+    G.ref(sa, ns, "metadata_namespace")
+    G.ref(sa, sa_secret, "secrets_name")
+    tenant = {"ns": ns, "ns_name": ns_name, "quota": quota, "quota_name": quota_name, "sa": sa,
+              "sa_secret": sa_secret, "tok": tok, "pods": [], "jobs": [], "sts": [], "pvc_pods": []}
+    n_draw = int(rng.integers(2, 7))
+    for _ in range(n_apps or n_draw):
+        kind = rng.choice(["deploy", "deploy", "sts", "cron"])
+        app = G.unique(f"{G.word()}-{G.word()}-{ns_name}" if rng.random() < 0.3 else f"{G.word()}-{G.word()}")
+        t_app = t_ns + int(rng.integers(0, WINDOW_MS // 4))
+        cm, _ = G.entity("ConfigMap", f"{app}-configmap", ns_name, t_app,
+                         extra_meta={"labels": {"app": app}})
+        G.ref(cm, ns, "metadata_namespace")
+        sec, _ = G.entity("Secret", f"{app}-secret", ns_name, t_app)
+        G.ref(sec, ns, "metadata_namespace")
+        svc, _ = G.entity("Service", app, ns_name, t_app, spec={"ports": [{"port": 8080}], "selector": {"app": app}})
+        G.ref(svc, ns, "metadata_namespace")
+        ep, _ = G.entity("Endpoints", app, ns_name, t_app)
+        G.ref(ep, svc, "metadata_name")
+        image_v = f"registry.local/{app}:v{int(rng.integers(1, 9))}.{int(rng.integers(0, 20))}"
+        img, _ = G.external("image", image_v, t_app, state_props={"imageName": image_v})
+        if kind == "deploy":
+            dep, _ = G.entity("Deployment", app, ns_name, t_app, spec={"replicas": 2})
+            G.ref(dep, ns, "metadata_namespace")
+            rs_name = f"{app}-{G.suffix(10)}"
+            owner, _ = G.entity("ReplicaSet", rs_name, ns_name, t_app, spec={"replicas": 2})
+            G.ref(owner, dep, "metadata_ownerReferences_uid")
+            G.ref(owner, ns, "metadata_namespace")
+            pod_names = [f"{rs_name}-{G.suffix(5)}" for _ in range(2)]
+        elif kind == "sts":
+            owner, _ = G.entity("StatefulSet", app, ns_name, t_app, spec={"replicas": 2, "serviceName": app})
+            G.ref(owner, ns, "metadata_namespace")
+            G.ref(owner, svc, "spec_serviceName")
+            tenant["sts"].append((owner, app))
+            pod_names = [f"{app}-{i}" for i in range(2)]
+        else:
+            cj, _ = G.entity("CronJob", f"{app}-cronjob", ns_name, t_app, spec={"schedule": "*/5 * * * *"})
+            G.ref(cj, ns, "metadata_namespace")
+            stamp = 1607600000 + int(rng.integers(0, 300000))
+            owner, _ = G.entity("Job", f"{app}-cronjob-{stamp}", ns_name, t_app, spec={"completions": 1})
+            G.ref(owner, cj, "metadata_ownerReferences_uid")
+            G.ref(owner, ns, "metadata_namespace")
+            tenant["jobs"].append((owner, f"{app}-cronjob-{stamp}"))
+            pod_names = [f"{app}-cronjob-{stamp}-{G.suffix(5)}"]
+        for pn in pod_names:
+            node = k8s_nodes[int(rng.integers(len(k8s_nodes)))]
+            vol_cfg = f"{app}-conf"
+            spec = {"nodeName": g.node_props(node)["name2"], "serviceAccountName": "default",
+                    "containers": [{"name": app, "image": image_v}],
+                    "volumes": [{"name": vol_cfg, "configMap": {"name": f"{app}-configmap"}},
+                                {"name": f"{app}-secret", "secret": {"secretName": f"{app}-secret"}},
+                                {"name": tok, "secret": {"secretName": tok}}]}
+            pvc = pv = nfs = None
+            if kind == "sts":
+                pvc_name = f"pvc-{app}-{pn}"
+                pvc, pvc_uid = G.entity("PersistentVolumeClaim", pvc_name, ns_name, t_app,
+                                        spec={"storageClassName": "nfs-client"},
+                                        status={"phase": "Bound"})
+                pv_name = f"pvc-{pvc_uid}"
+                path = f"/mnt/k8s_nfs_pv/{ns_name}-{pvc_name}-{pv_name}"
+                pv, _ = G.entity("PersistentVolume", pv_name, None, t_app,
+                                 spec={"nfs": {"server": nfs_server, "path": path},
+                                       "claimRef": {"uid": pvc_uid, "name": pvc_name}},
+                                 status={"phase": "Bound"})
+                nfs, _ = G.external("nfs", path, t_app, state_props={"path": path, "server": nfs_server})
+                G.ref(pvc, pv, "spec_volumeName")
+                G.ref(pvc, sc, "spec_storageClassName")
+                G.ref(pvc, ns, "metadata_namespace")
+                G.ref(pv, pvc, "spec_claimRef_uid")
+                G.ref(pv, sc, "spec_storageClassName")
+                G.ref(pv, nfs, "spec_nfs_path", rel="UseExternal")
+                spec["volumes"].append({"name": pv_name, "persistentVolumeClaim": {"claimName": pvc_name}})
+            pod, pod_uid = G.entity("Pod", pn, ns_name, t_app + 1000, spec=spec,
+                                    status={"phase": "Running", "hostIP": "172.16.0.1"})
+            G.ref(pod, node, "spec_nodeName")
+            G.ref(pod, ns, "metadata_namespace")
+            G.ref(pod, cm, "spec_volumes_configMap_name")
+            G.ref(pod, sec, "spec_volumes_secret_secretName")
+            G.ref(pod, sa_secret, "spec_volumes_secret_secretName")
+            G.ref(pod, sa, "spec_serviceAccountName")
+            G.ref(pod, owner, "metadata_ownerReferences_uid")
+            if pvc is not None:
+                G.ref(pod, pvc, "spec_volumes_persistentVolumeClaim_claimName")
+            ctr, _ = G.external("container", app, t_app + 1000, state_props={"containerName": app})
+            G.ref(pod, ctr, "spec_containers_name", rel="UseExternal")
+            G.ref(pod, img, "spec_containers_image", rel="UseExternal")
+            G.ref(ep, pod, "subsets_addresses_targetRef_uid")
+            rec = {"pod": pod, "pod_uid": pod_uid, "name": pn, "node": node, "cm": cm, "sec": sec,
+                   "pvc": pvc, "pv": pv, "nfs": nfs, "app": app, "owner": owner}
+            tenant["pods"].append(rec)
+            if pvc is not None:
+                tenant["pvc_pods"].append(rec)
+            # a normal lifecycle event per pod
+            G.event(pod, f"Successfully assigned {ns_name}/{pn} to {g.node_props(node)['name2']}",
+                    G.ts(t_app + 1000, t_app + 5000), "Scheduled", "Normal")
+    return tenant
 
 
 def _pick(G: _Gen, items):

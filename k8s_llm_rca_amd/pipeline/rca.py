@@ -83,6 +83,7 @@ class RCAPipeline:
         self.prompt_template = FM.build_prompt_template(self.native, self.external)
         self.generator = GQ.setup_cypher_generator(service, m)
         self.analyzer = CS.setup_state_semantic_analyzer(service, m)
+        self.last_failed_runs = 0  # LLM runs of the last analyze() that failed / expired / were cancelled
 
     # ------------------------------------------------------------ formats
     def _locator_fmt(self, src: str, truth) -> Any:
@@ -174,6 +175,10 @@ class RCAPipeline:
                     analysis["statepath"].append(sp)
             result["analysis"].append(analysis)
         t1 = time.time()
+        self.last_failed_runs = sum(
+            1 for a in (self.locator, self.generator, self.analyzer)
+            for run in self.service.list_runs(a.thread.id, limit=64)
+            if run.created_at >= t0 and run.status in ("failed", "cancelled", "expired"))
         result["time_cost"] = t1 - t0
         tmin, tmax = (int(t0), int(t1)) if self.cfg.compat.int_token_window else (t0, t1 + 1e-6)
         usage = {"prompt_tokens": 0, "completion_tokens": 0, "total_tokens": 0}
@@ -273,3 +278,86 @@ def run_batch(make_pipeline: Callable[[], RCAPipeline], messages: List[str], con
         t.join()
     wall = time.perf_counter() - t0
     return BatchStats([r for r in results if r is not None], lat, wall, errors)
+
+
+class IncidentStream:
+    """Steady-state multi-incident driver: one worker thread per pipeline pulls
+    the next incident from a cyclic source the moment it finishes one, so the
+    engine always sees ``len(pipelines)`` concurrent analyses (the CLI's
+    ``run --concurrency`` as an unbounded stream).  Every completion is
+    timestamped, so a caller can time a window of N completed analyses
+    (``bench/rca_bench.py``'s steps) without draining the stream.
+
+    An analysis counts as completed only if it raised nothing and none of its
+    LLM runs failed, expired or was cancelled (an engine fault that fails every
+    in-flight run must not show up as fast throughput)."""
+
+    def __init__(self, pipelines: List[RCAPipeline], incidents: List[Any], hints: bool = True):
+        self.pipelines = pipelines
+        self.incidents = incidents
+        self.hints = hints
+        self._cv = threading.Condition()
+        self._next = 0
+        self._stop = False
+        self.done: List[tuple] = []   # (t_done, latency_s, ok) in completion order
+        self.n_ok = 0
+        self.n_err = 0
+        self.errors: List[str] = []
+        self._threads: List[threading.Thread] = []
+
+    def start(self) -> None:
+        for p in self.pipelines:
+            t = threading.Thread(target=self._worker, args=(p,), daemon=True, name="rca-stream")
+            t.start()
+            self._threads.append(t)
+
+    def stop(self) -> None:
+        """Stop admitting incidents (in-flight analyses finish or are abandoned)."""
+        with self._cv:
+            self._stop = True
+            self._cv.notify_all()
+
+    def _worker(self, p: RCAPipeline) -> None:
+        while True:
+            with self._cv:
+                if self._stop:
+                    return
+                i = self._next
+                self._next += 1
+            inc = self.incidents[i % len(self.incidents)]
+            t = time.perf_counter()
+            ok, err = True, None
+            try:
+                r = p.analyze(inc.message, inc if self.hints else None)
+                if p.last_failed_runs:
+                    ok, err = False, f"{p.last_failed_runs} LLM run(s) failed: {r.get('error_message', '')[:60]!r}"
+            except Exception as e:  # noqa: BLE001 - counted, never fatal to the stream
+                log.exception("incident %d failed", i)
+                ok, err = False, repr(e)
+            t1 = time.perf_counter()
+            with self._cv:
+                self.done.append((t1, t1 - t, ok))
+                if ok:
+                    self.n_ok += 1
+                else:
+                    self.n_err += 1
+                    self.errors.append(err)
+                self._cv.notify_all()
+
+    def wait_ok(self, n: int, deadline: Optional[float] = None, poll: Optional[Callable[[], None]] = None) -> bool:
+        """Block until ``n`` analyses completed successfully (False at ``deadline``,
+        a ``time.perf_counter()`` value).  ``poll`` runs every ~0.5 s (e.g. to
+        re-raise an engine fault)."""
+        with self._cv:
+            while self.n_ok < n:
+                if deadline is not None and time.perf_counter() >= deadline:
+                    return False
+                self._cv.wait(0.5)
+                if poll is not None:
+                    poll()
+            return True
+
+    def window(self, t0: float, t1: float) -> List[float]:
+        """Latencies of the successful analyses completed in ``[t0, t1)``."""
+        with self._cv:
+            return [lat for t, lat, ok in self.done if ok and t0 <= t < t1]

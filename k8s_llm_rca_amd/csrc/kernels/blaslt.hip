@@ -39,9 +39,9 @@
 namespace {
 
 struct Key {
-  int M, N, K, ldx, ldy;
+  int M, N, K, ldx, ldy, f32out;
   bool operator==(const Key& o) const {
-    return M == o.M && N == o.N && K == o.K && ldx == o.ldx && ldy == o.ldy;
+    return M == o.M && N == o.N && K == o.K && ldx == o.ldx && ldy == o.ldy && f32out == o.f32out;
   }
 };
 
@@ -52,6 +52,7 @@ struct KeyHash {
     h ^= (size_t)k.K * 0x165667B19E3779F9ull + (h << 6) + (h >> 2);
     h ^= (size_t)k.ldx * 0x27D4EB2F165667C5ull + (h << 6) + (h >> 2);
     h ^= (size_t)k.ldy + (h << 6) + (h >> 2);
+    h ^= (size_t)k.f32out * 0x9E3779B1ull;
     return h;
   }
 };
@@ -78,7 +79,7 @@ int make_desc(const Key& k, Plan* p) {
   // A: K x N (lda = K), B: K x M (ldb = ldx), C/D: N x M (ldc = ldy)
   if (hipblasLtMatrixLayoutCreate(&p->a, HIP_R_16BF, k.K, k.N, k.K) != HIPBLAS_STATUS_SUCCESS ||
       hipblasLtMatrixLayoutCreate(&p->b, HIP_R_16BF, k.K, k.M, k.ldx) != HIPBLAS_STATUS_SUCCESS ||
-      hipblasLtMatrixLayoutCreate(&p->c, HIP_R_16BF, k.N, k.M, k.ldy) != HIPBLAS_STATUS_SUCCESS)
+      hipblasLtMatrixLayoutCreate(&p->c, k.f32out ? HIP_R_32F : HIP_R_16BF, k.N, k.M, k.ldy) != HIPBLAS_STATUS_SUCCESS)
     return 1100;
   return 0;
 }
@@ -98,7 +99,7 @@ int build_plan(const Key& k, size_t ws_limit, Plan* out) {
   int rc = make_desc(k, &p);
   if (rc) return rc;
   auto t = g_tuned.find({k.N, k.K});
-  if (t != g_tuned.end() && !t->second.empty()) {
+  if (!k.f32out && t != g_tuned.end() && !t->second.empty()) {
     auto it = t->second.upper_bound(k.M);  // first ladder M > M
     hipblasLtMatmulAlgo_t algo;
     size_t wsz = 0;
@@ -126,11 +127,12 @@ int build_plan(const Key& k, size_t ws_limit, Plan* out) {
 }  // namespace
 
 // ws: device scratch of ws_bytes (reused by every call on the stream; must
-// outlive any HIP graph that captured a call).
-K8S_API int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
-                            size_t ws_bytes, hipStream_t s) {
+// outlive any HIP graph that captured a call).  f32out: Y is fp32 (the lm_head's
+// logits, B9: sampling reads fp32 logits), else bf16.
+K8S_API int k8s_blaslt_gemm2(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
+                             size_t ws_bytes, hipStream_t s, int f32out) {
   if (M <= 0 || N <= 0 || K <= 0 || ldx < K || ldy < N) return (int)hipErrorInvalidValue;
-  const Key key{M, N, K, ldx, ldy};
+  const Key key{M, N, K, ldx, ldy, f32out ? 1 : 0};
   Plan* plan;
   {
     std::lock_guard<std::mutex> g(g_mu);
@@ -151,6 +153,11 @@ K8S_API int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int 
   return st == HIPBLAS_STATUS_SUCCESS ? 0 : 1400 + (int)st;
 }
 
+K8S_API int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
+                            size_t ws_bytes, hipStream_t s) {
+  return k8s_blaslt_gemm2(x, ldx, w, y, ldy, M, N, K, ws, ws_bytes, s, 0);
+}
+
 K8S_API int k8s_blaslt_num_plans() {
   std::lock_guard<std::mutex> g(g_mu);
   return (int)g_plans.size();
@@ -169,7 +176,7 @@ K8S_API int k8s_blaslt_tune(const void* x, int ldx, const void* w, void* y, int 
   if (M <= 0 || N <= 0 || K <= 0 || ldx < K || ldy < N || max_algos < 1 || iters < 1) return -(int)hipErrorInvalidValue;
   std::lock_guard<std::mutex> g(g_mu);
   if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return -900;
-  const Key key{M, N, K, ldx, ldy};
+  const Key key{M, N, K, ldx, ldy, 0};
   Plan p;
   int rc = make_desc(key, &p);
   if (rc) return -rc;

@@ -1,19 +1,33 @@
-// Masked sampling over the vocabulary (B9): greedy argmax or exact softmax
-// sampling via the Gumbel-max trick in ONE pass over the logits:
-//   tok = argmax_i  logit_i / T + G_i,   G_i = -log(-log(U_i)),
+// Masked sampling over the vocabulary (B9): greedy argmax, temperature, top-k
+// and top-p (nucleus), over fp32 (default) or bf16 logits.
+//
+// Sampling is exact categorical sampling by the Gumbel-max trick:
+//   tok = argmax_{i in S}  v_i + G_i,   v_i = logit_i / T,   G_i = -log(-log(U_i)),
 // U_i from a counter-based hash of (seed, step, i) -> reproducible and
-// graph-capturable (the seed/step live in device memory).  The per-request
-// seed already includes the sequence id, so the noise does not depend on the
-// row's position in the batch: a sequence samples the same tokens however the
-// scheduler batches it (sync or overlapped steps, any batch mix).
-// Constrained decoding masks (grammar states) come in two forms per row:
-//   * bitmap: mask_table[mask_id[row]] is a [V/32] uint32 allow-bitmap
-//   * list:   an explicit allow-list slice (list_off, list_len) of token ids
-// Logits are bf16 [B][ld]; one 256-thread workgroup per row.
-// Vocab-parallel (TP) form: the rank holds columns [vocab_off, vocab_off + V)
-// of the vocabulary; noise and masks are keyed by the GLOBAL token id, so the
-// per-rank (score, id) winners combined by max over ranks give exactly the
-// token the unsharded kernel would sample (B10 without a logits all-gather).
+// graph-capturable (seed/step live in device memory).  The per-request seed
+// already includes the sequence id, so the noise does not depend on the row's
+// position in the batch.  S is the allowed set:
+//   * grammar mask: bitmap mask_table[mask_id[row]] ([V/32] uint32) or an
+//     explicit allow-list slice (list_off, list_len);
+//   * top-k: the allowed tokens whose v is >= the k-th largest v (ties kept,
+//     like HF's `logits < topk_values[..., -1]` filter);
+//   * top-p: of those, the smallest highest-v prefix whose softmax mass
+//     reaches p (the token that crosses p is kept; ties kept).
+// Rows with neither top-k nor top-p take ONE pass over the logits.  Rows with
+// either find their thresholds by MSB-first radix select on the order-
+// preserving uint32 image of v: 4 byte-passes with a 256-bin LDS histogram of
+// counts (top-k) or of softmax mass exp(v - max) (top-p), then one Gumbel-max
+// pass over the survivors.  Everything is one 256-thread workgroup per row.
+//
+// Vocab-parallel (TP) forms: the rank holds columns [vocab_off, vocab_off + V)
+// of the vocabulary; noise and masks are keyed by the GLOBAL token id.
+//   * out_pair: the rank's (score, id) Gumbel-max winner; the max over ranks
+//     is exactly the unsharded kernel's token (B10 without a logits gather).
+//   * out_cand (top-k / top-p rows): the rank's highest-v allowed candidates
+//     (v, id, v + G), cand_k per row sorted by (v desc, id asc), padded with
+//     (-inf, -1, -inf); the ranks' lists are all-gathered and combined (ops/sampling.py):
+//     exact for top-k <= cand_k, and for a nucleus that holds <= cand_k
+//     tokens of each shard.
 #include "common.h"
 
 namespace k8s {
@@ -33,6 +47,12 @@ __device__ __forceinline__ float gumbel(uint32_t seed, uint32_t row, uint32_t st
   return -__logf(-__logf(u));
 }
 
+// order-preserving map float -> uint32 (larger float -> larger key; -inf > 0)
+__device__ __forceinline__ uint32_t okey(float v) {
+  const uint32_t u = __float_as_uint(v);
+  return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
 struct Best {
   float v;
   int i;
@@ -43,77 +63,258 @@ __device__ __forceinline__ Best better(Best a, Best b) {
   return a;
 }
 
-__global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict__ logits, int ld, int V, int vocab_off,
+__device__ __forceinline__ float lg(const uint16_t* p, int i) { return bf2f(p[i]); }
+__device__ __forceinline__ float lg(const float* p, int i) { return p[i]; }
+
+// 8 consecutive logits (i0 % 8 == 0): one 16-B (bf16) or two 16-B (f32) loads
+__device__ __forceinline__ void lg8(const uint16_t* p, int i0, float* o) {
+  const u16x8 x = *reinterpret_cast<const u16x8*>(p + i0);
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = bf2f(x[j]);
+}
+__device__ __forceinline__ void lg8(const float* p, int i0, float* o) {
+  const f32x4 a = *reinterpret_cast<const f32x4*>(p + i0);
+  const f32x4 b = *reinterpret_cast<const f32x4*>(p + i0 + 4);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[j] = a[j];
+    o[4 + j] = b[j];
+  }
+}
+
+// Calls f(global_id, v) for every allowed token of the row held by this
+// thread's share (v = logit * inv_temp).
+template <typename T, typename F>
+__device__ __forceinline__ void for_allowed(const T* lr, int V, int vocab_off, float it, const int* lst, int ll,
+                                            const uint32_t* mk, F&& f) {
+  if (ll > 0) {
+    for (int k = threadIdx.x; k < ll; k += blockDim.x) {
+      const int gi = lst[k];
+      const int i = gi - vocab_off;
+      if (i < 0 || i >= V) continue;
+      f(gi, lg(lr, i) * it);
+    }
+    return;
+  }
+  const int nv = V >> 3;
+  for (int c = threadIdx.x; c < nv; c += blockDim.x) {
+    const int i0 = c * 8, g0 = vocab_off + i0;  // vocab_off % 8 == 0 (host-checked)
+    uint32_t bits = 0xFFu;
+    if (mk) bits = (mk[g0 >> 5] >> (g0 & 31)) & 0xFFu;
+    if (!bits) continue;
+    float x[8];
+    lg8(lr, i0, x);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if ((bits >> j) & 1u) f(g0 + j, x[j] * it);
+  }
+  for (int i = (nv << 3) + threadIdx.x; i < V; i += blockDim.x) {  // tail (V % 8)
+    const int gi = vocab_off + i;
+    if (mk && !((mk[gi >> 5] >> (gi & 31)) & 1u)) continue;
+    f(gi, lg(lr, i) * it);
+  }
+}
+
+__device__ __forceinline__ Best block_best(Best best, float* sv, int* si) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    Best other{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
+    best = better(best, other);
+  }
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  __syncthreads();
+  if (lane == 0) {
+    sv[w] = best.v;
+    si[w] = best.i;
+  }
+  __syncthreads();
+  Best b{sv[0], si[0]};
+  for (int k = 1; k < (int)(blockDim.x >> 6); ++k) b = better(b, Best{sv[k], si[k]});
+  return b;
+}
+
+// One radix-select byte pass.  Keys whose bytes above `byte` equal `prefix`'s
+// and that are >= `floor_key` add `count ? 1 : exp(v - vmax)` to bin (key >>
+// 8*byte) & 255.  Then bins are walked from 255 down: the first bin at which
+// the running total reaches `*need` is fixed into `*prefix`, and `*need` drops
+// by the total of the bins above it.
+template <typename T>
+__device__ void radix_pass(const T* lr, int V, int vocab_off, float it, const int* lst, int ll, const uint32_t* mk,
+                           int byte, bool count, float vmax, uint32_t floor_key, uint32_t* prefix, float* need,
+                           float* hist) {
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0.f;
+  __syncthreads();
+  const uint32_t pre = *prefix;
+  const int hs = 8 * (byte + 1);
+  for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int, float v) {
+    const uint32_t k = okey(v);
+    if (k < floor_key) return;
+    if (hs < 32 && (k >> hs) != (pre >> hs)) return;
+    atomicAdd(&hist[(k >> (8 * byte)) & 255u], count ? 1.f : __expf(v - vmax));
+  });
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float cum = 0.f, rem = *need;
+    int pick = -1, lowest = -1;
+    for (int b = 255; b >= 0; --b) {
+      const float h = hist[b];
+      if (h <= 0.f) continue;
+      lowest = b;
+      if (cum + h >= rem) {
+        pick = b;
+        break;
+      }
+      cum += h;
+    }
+    if (pick < 0) {  // rounding: the target was never reached -> keep the whole remaining set
+      pick = lowest < 0 ? 0 : lowest;
+      if (lowest >= 0) cum -= hist[lowest];
+    }
+    *need = rem - cum;
+    *prefix = pre | ((uint32_t)pick << (8 * byte));
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logits, int ld, int V, int vocab_off,
                                                      const float* __restrict__ temperature,
                                                      const uint32_t* __restrict__ seeds,
                                                      const int* __restrict__ steps,
                                                      const int* __restrict__ mask_id,
                                                      const uint32_t* __restrict__ mask_table, int mask_words,
                                                      const int* __restrict__ list_off, const int* __restrict__ list_len,
-                                                     const int* __restrict__ lists, int* __restrict__ out,
-                                                     float2* __restrict__ out_pair) {
+                                                     const int* __restrict__ lists, const int* __restrict__ top_k,
+                                                     const float* __restrict__ top_p, int* __restrict__ out,
+                                                     float2* __restrict__ out_pair, float* __restrict__ out_cand,
+                                                     int cand_k) {
+  __shared__ float hist[256];
+  __shared__ float sv[4];
+  __shared__ int si[4];
+  __shared__ uint32_t s_prefix;
+  __shared__ float s_need;
+  __shared__ int s_nc;
+  __shared__ float c_v[256];
+  __shared__ int c_i[256];
+
   const int row = blockIdx.x;
-  const uint16_t* lr = logits + (size_t)row * ld;
+  const T* lr = logits + (size_t)row * ld;
   const float temp = temperature ? temperature[row] : 0.f;
   const bool greedy = !(temp > 0.f);
   const float it = greedy ? 1.f : 1.f / temp;
   const uint32_t seed = seeds ? seeds[row] : 0u;
   const uint32_t step = steps ? (uint32_t)steps[row] : 0u;
-  Best best{-INFINITY, -1};
   const int ll = list_len ? list_len[row] : 0;
-  if (ll > 0) {
-    const int* lst = lists + list_off[row];
-    for (int k = threadIdx.x; k < ll; k += blockDim.x) {
-      const int gi = lst[k];
-      const int i = gi - vocab_off;
-      if (i < 0 || i >= V) continue;
-      float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, 0u, step, gi);
-      best = better(best, Best{v, gi});
+  const int* lst = ll > 0 ? lists + list_off[row] : nullptr;
+  const int mid = mask_id ? mask_id[row] : -1;
+  const uint32_t* mk = (ll <= 0 && mid >= 0) ? mask_table + (size_t)mid * mask_words : nullptr;
+  const int kk = top_k ? top_k[row] : 0;
+  const float pp = top_p ? top_p[row] : 1.f;
+  const bool cand = out_cand != nullptr && (kk > 0 || pp < 1.f);
+  const bool filt = !greedy && (kk > 0 || pp < 1.f);
+
+  uint32_t thr = 0u;  // survivors: okey(v) >= thr
+  if (filt || cand) {
+    // ---- row max and allowed count
+    Best mx{-INFINITY, -1};
+    int n_allowed = 0;
+    for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
+      mx = better(mx, Best{v, gi});
+      ++n_allowed;
+    });
+    const float vmax = block_best(mx, sv, si).v;
+    __syncthreads();
+    const float nal = block_sum((float)n_allowed, hist);
+    // ---- top-k threshold (cand: the rank-local top-cand_k)
+    const int keff = cand ? ((kk > 0 && kk < cand_k) ? kk : cand_k) : kk;
+    if (keff > 0 && (float)keff < nal) {
+      if (threadIdx.x == 0) {
+        s_prefix = 0u;
+        s_need = (float)keff;
+      }
+      __syncthreads();
+      for (int byte = 3; byte >= 0; --byte)
+        radix_pass(lr, V, vocab_off, it, lst, ll, mk, byte, true, vmax, 0u, &s_prefix, &s_need, hist);
+      thr = s_prefix;
     }
-  } else {
-    const int mid = mask_id ? mask_id[row] : -1;
-    const uint32_t* mk = (mid >= 0) ? mask_table + (size_t)mid * mask_words : nullptr;
-    const int nv = V >> 3;
-    for (int c = threadIdx.x; c < nv; c += blockDim.x) {
-      const int i0 = c * 8, g0 = vocab_off + i0;  // vocab_off % 8 == 0 (host-checked)
-      uint32_t bits = 0xFFu;
-      if (mk) bits = (mk[g0 >> 5] >> (g0 & 31)) & 0xFFu;
-      if (!bits) continue;
-      u16x8 x = *reinterpret_cast<const u16x8*>(lr + i0);
-#pragma unroll
-      for (int j = 0; j < 8; ++j) {
-        if (!((bits >> j) & 1u)) continue;
-        float v = bf2f(x[j]) * it;
-        if (!greedy) v += gumbel(seed, 0u, step, g0 + j);
-        best = better(best, Best{v, g0 + j});
+    // ---- top-p threshold inside the top-k set (single-rank form only)
+    if (!cand && pp < 1.f) {
+      float z = 0.f;
+      for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int, float v) {
+        if (okey(v) >= thr) z += __expf(v - vmax);
+      });
+      __syncthreads();
+      z = block_sum(z, hist);
+      if (threadIdx.x == 0) {
+        s_prefix = 0u;
+        s_need = fmaxf(pp, 0.f) * z;
+      }
+      __syncthreads();
+      for (int byte = 3; byte >= 0; --byte)
+        radix_pass(lr, V, vocab_off, it, lst, ll, mk, byte, false, vmax, thr, &s_prefix, &s_need, hist);
+      thr = s_prefix > thr ? s_prefix : thr;
+    }
+    __syncthreads();
+  }
+
+  if (cand) {
+    // ---- rank-local candidates (v >= thr, at most 256 gathered), sorted (v desc, id asc)
+    if (threadIdx.x == 0) s_nc = 0;
+    for (int k = threadIdx.x; k < 256; k += blockDim.x) {
+      c_v[k] = -INFINITY;
+      c_i[k] = 0x7fffffff;
+    }
+    __syncthreads();
+    for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
+      if (okey(v) < thr) return;
+      const int slot = atomicAdd(&s_nc, 1);
+      if (slot < 256) {
+        c_v[slot] = v;
+        c_i[slot] = gi;
+      }
+    });
+    __syncthreads();
+    // bitonic sort of 256 (v desc, id asc)
+    for (int size = 2; size <= 256; size <<= 1) {
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int t = threadIdx.x; t < 256; t += blockDim.x) {
+          const int o = t ^ stride;
+          if (o > t) {
+            const bool desc = (t & size) == 0;
+            const bool t_first = c_v[t] > c_v[o] || (c_v[t] == c_v[o] && c_i[t] < c_i[o]);
+            if (t_first != desc) {
+              const float tv = c_v[t];
+              c_v[t] = c_v[o];
+              c_v[o] = tv;
+              const int ti = c_i[t];
+              c_i[t] = c_i[o];
+              c_i[o] = ti;
+            }
+          }
+        }
+        __syncthreads();
       }
     }
-    for (int i = (nv << 3) + threadIdx.x; i < V; i += blockDim.x) {  // tail (V % 8)
-      const int gi = vocab_off + i;
-      if (mk && !((mk[gi >> 5] >> (gi & 31)) & 1u)) continue;
-      float v = bf2f(lr[i]) * it;
-      if (!greedy) v += gumbel(seed, 0u, step, gi);
-      best = better(best, Best{v, gi});
+    for (int k = threadIdx.x; k < cand_k; k += blockDim.x) {
+      const bool ok = k < 256 && c_i[k] != 0x7fffffff;
+      float* o = out_cand + ((size_t)row * cand_k + k) * 3;
+      o[0] = ok ? c_v[k] : -INFINITY;
+      o[1] = ok ? (float)c_i[k] : -1.f;
+      o[2] = ok ? (greedy ? c_v[k] : c_v[k] + gumbel(seed, 0u, step, c_i[k])) : -INFINITY;
     }
+    if (!out_pair && !out) return;
+    __syncthreads();
   }
-  // block argmax
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) {
-    Best other{__shfl_xor(best.v, o, 64), __shfl_xor(best.i, o, 64)};
-    best = better(best, other);
-  }
-  __shared__ float sv[4];
-  __shared__ int si[4];
-  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  if (lane == 0) {
-    sv[w] = best.v;
-    si[w] = best.i;
-  }
-  __syncthreads();
+
+  // ---- Gumbel-max (or argmax) over the survivors
+  Best best{-INFINITY, -1};
+  for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
+    if (filt && okey(v) < thr) return;
+    if (!greedy) v += gumbel(seed, 0u, step, gi);
+    best = better(best, Best{v, gi});
+  });
+  const Best b = block_best(best, sv, si);
   if (threadIdx.x == 0) {
-    Best b{sv[0], si[0]};
-    for (int k = 1; k < (int)(blockDim.x >> 6); ++k) b = better(b, Best{sv[k], si[k]});
     if (out) out[row] = b.i;
     if (out_pair) out_pair[row] = make_float2(b.v, (float)b.i);  // ids < 2^24: exact in f32
   }
@@ -123,14 +324,24 @@ __global__ void __launch_bounds__(256) sample_kernel(const uint16_t* __restrict_
 
 using namespace k8s;
 
+// logits_f32: 1 = fp32 logits, 0 = bf16.  top_k / top_p: per-row (nullptr =
+// off; k <= 0 and p >= 1 disable per row).  out_cand [B][cand_k][3] float
+// (TP candidate lists, nullptr = off).
 K8S_API int k8s_sample(const void* logits, int ld, int B, int V, int vocab_off, const float* temperature,
                        const uint32_t* seeds, const int* steps, const int* mask_id, const uint32_t* mask_table,
                        int mask_words, const int* list_off, const int* list_len, const int* lists, int* out,
-                       float* out_pair, hipStream_t s) {
+                       float* out_pair, hipStream_t s, int logits_f32, const int* top_k, const float* top_p,
+                       float* out_cand, int cand_k) {
   if (B <= 0) return 0;
-  if (vocab_off % 8 || (vocab_off + V) >= (1 << 24)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(sample_kernel, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, ld, V, vocab_off, temperature,
-                     seeds, steps, mask_id, mask_table, mask_words, list_off, list_len, lists, out,
-                     reinterpret_cast<float2*>(out_pair));
+  if (vocab_off % 8 || (vocab_off + V) >= (1 << 24) || (out_cand && (cand_k <= 0 || cand_k > 256)))
+    return (int)hipErrorInvalidValue;
+  if (logits_f32)
+    hipLaunchKernelGGL(sample_kernel<float>, dim3(B), dim3(256), 0, s, (const float*)logits, ld, V, vocab_off,
+                       temperature, seeds, steps, mask_id, mask_table, mask_words, list_off, list_len, lists, top_k,
+                       top_p, out, reinterpret_cast<float2*>(out_pair), out_cand, cand_k);
+  else
+    hipLaunchKernelGGL(sample_kernel<uint16_t>, dim3(B), dim3(256), 0, s, (const uint16_t*)logits, ld, V, vocab_off,
+                       temperature, seeds, steps, mask_id, mask_table, mask_words, list_off, list_len, lists, top_k,
+                       top_p, out, reinterpret_cast<float2*>(out_pair), out_cand, cand_k);
   return (int)hipGetLastError();
 }

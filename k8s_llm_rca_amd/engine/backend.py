@@ -43,8 +43,10 @@ class _ThreadTokens:
 
 class EngineBackend(Backend):
     def __init__(self, engine: LLMEngine, default_max_tokens: int = 512, keep_seed: int = 2,
-                 temperature: Optional[float] = None, trunc_low: float = 0.5):
+                 temperature: Optional[float] = None, trunc_low: float = 0.5, top_k: int = 0, top_p: float = 1.0):
         self.engine = engine
+        self.top_k = top_k  # defaults for runs that do not set them (run_assistant(sampling=...))
+        self.top_p = top_p
         self.tok = engine.tok
         self.default_max_tokens = default_max_tokens
         self.keep_seed = keep_seed
@@ -121,7 +123,8 @@ class EngineBackend(Backend):
             self.service.run_completed(rs, text, len(prompt), len(gen), metrics=stats)
 
         self.engine.submit(st.sid, prompt, grammar=rs.response_format, max_new=max_new, temperature=temp,
-                           seed=seed, on_done=on_done)
+                           seed=seed, on_done=on_done, top_k=rs.sampling.get("top_k", self.top_k),
+                           top_p=rs.sampling.get("top_p", self.top_p))
 
     def release_thread(self, ts: ThreadState) -> None:
         st = ts.backend_state

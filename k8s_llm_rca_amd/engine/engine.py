@@ -118,15 +118,18 @@ class EngineConfig:
     tokenizer: Optional[str] = None  # tokenizer.json (default: the checkpoint's, else the built-in BPE)
     temperature: float = 0.7
     use_hints: bool = True
+    logits_fp32: bool = True   # lm_head writes fp32 logits for the sampler
     model_overrides: dict = field(default_factory=dict)
 
 
 class Request:
     __slots__ = ("seq", "gs", "max_new", "temperature", "seed", "on_done", "n_prompt", "generated", "mask",
-                 "t_submit", "t_first", "n_forced", "n_sampled", "cancelled")
+                 "t_submit", "t_first", "n_forced", "n_sampled", "cancelled", "top_k", "top_p")
 
-    def __init__(self, seq, gs, max_new, temperature, seed, on_done, n_prompt):
+    def __init__(self, seq, gs, max_new, temperature, seed, on_done, n_prompt, top_k=0, top_p=1.0):
         self.seq = seq
+        self.top_k = int(top_k or 0)
+        self.top_p = float(1.0 if top_p is None else top_p)
         self.gs: GrammarState = gs
         self.max_new = max_new
         self.temperature = temperature
@@ -183,6 +186,8 @@ class LLMEngine:
             self.mc = get_config(cfg.model, **cfg.model_overrides)
         self.max_context = cfg.max_context or self.mc.max_position
         self.model = model or _build_model(self.mc, self.device, cfg.dtype, self.pc, cfg.seed)
+        if hasattr(self.model, "logits_f32"):
+            self.model.logits_f32 = cfg.logits_fp32
         self.gemm_dispatch = False
         if self.device.type == "cuda":
             from ..ops import gemm_tuning
@@ -306,11 +311,14 @@ class LLMEngine:
 
     def submit(self, sid: int, tokens: List[int], grammar=None, max_new: int = 256,
                temperature: Optional[float] = None, seed: int = 0,
-               on_done: Optional[Callable[[List[int], Dict[str, float]], None]] = None) -> None:
-        """Set sequence ``sid``'s desired token list (prompt) and generate a reply."""
+               on_done: Optional[Callable[[List[int], Dict[str, float]], None]] = None,
+               top_k: int = 0, top_p: float = 1.0) -> None:
+        """Set sequence ``sid``'s desired token list (prompt) and generate a reply
+        (``top_k`` <= 0 and ``top_p`` >= 1 disable those filters)."""
         with self._cv:
             self._incoming.append((sid, list(tokens), grammar, max_new,
-                                   self.cfg.temperature if temperature is None else temperature, seed, on_done))
+                                   self.cfg.temperature if temperature is None else temperature, seed, on_done,
+                                   top_k, top_p))
             self._cv.notify()
 
     def start(self) -> None:
@@ -391,7 +399,7 @@ class LLMEngine:
         with self._lock:
             inc, self._incoming = self._incoming, []
             seqs = {sid: self.seqs[sid] for sid, *_ in inc}
-        for sid, toks, grammar, max_new, temp, seed, on_done in inc:
+        for sid, toks, grammar, max_new, temp, seed, on_done, top_k, top_p in inc:
             s = seqs[sid]
             if s.req is not None:
                 raise RuntimeError(f"sequence {sid} already has an active request")
@@ -414,7 +422,7 @@ class LLMEngine:
                 self.kv.release(s.blocks[keep:])
                 s.blocks = s.blocks[:keep]
             gs = GrammarState(self.grt, grammar, self.eos_ids, max_tokens=max_new, use_hints=self.cfg.use_hints)
-            r = Request(s, gs, max_new, temp, seed, on_done, len(toks))
+            r = Request(s, gs, max_new, temp, seed, on_done, len(toks), top_k, top_p)
             s.req = r
             self.stats["requests"] += 1
             self._drive(r)
@@ -804,7 +812,7 @@ class LLMEngine:
     # ------------------------------------------------- TP vocab-parallel sampling
     SHDR = 4
 
-    def _tp_sample(self, logits, mask_id, list_off, list_len, lists, seeds, steps, temps) -> torch.Tensor:
+    def _tp_sample(self, logits, mask_id, list_off, list_len, lists, seeds, steps, temps, topk, topp) -> torch.Tensor:
         """Rank 0: broadcast this step's sampling inputs (plus mask rows the
         workers have not seen), then sample on every rank's vocab shard."""
         import numpy as np_
@@ -814,7 +822,7 @@ class LLMEngine:
         B = mask_id.shape[0]
         hdr = np_.array([B, len(lists), new.shape[0], self.grt.masks.words], dtype=np_.int64)
         flat = np_.concatenate([mask_id, list_off, list_len, lists, seeds, steps, temps.view(np_.int32),
-                                new.reshape(-1).astype(np_.int32)])
+                                topk, topp.view(np_.int32), new.reshape(-1).astype(np_.int32)])
         h = torch.from_numpy(hdr).to(self._comm_device())
         self._bcast(h)
         dev = self._to_dev([flat])[0]
@@ -837,18 +845,29 @@ class LLMEngine:
 
         mask_id, list_off, list_len, lists, seeds, steps = (take(B), take(B), take(B), take(L), take(B), take(B))
         temps = take(B).view(torch.float32)
+        topk = take(B)
+        topp = take(B).view(torch.float32)
         rows = take(nr * words).view(nr, words)
         if nr:
             self._wmask = rows.clone() if self._wmask is None else torch.cat([self._wmask, rows])
         table = self._wmask if self._wmask is not None else torch.zeros(1, words, dtype=torch.int32,
                                                                          device=self.device)
         off = self.pc.tp_rank * self.model.vocab_local
-        pairs = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
-                           vocab_off=off, pairs=True)
-        comm = pairs.to(self._comm_device())
+        filt = (topk > 0) | (topp < 1.0)
+        pairs, cand = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
+                                 vocab_off=off, pairs=True, top_k=topk, top_p=topp, candidates=True)
+        # one all-gather of [B, 2 + 3 * CAND_K] per rank: the Gumbel-max winner and,
+        # for top-k / top-p rows, the shard's highest-v candidates (B10 distributed top-k)
+        comm = torch.cat([pairs, cand.view(B, -1)], 1).to(self._comm_device())
         parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
         dist.all_gather(parts, comm, group=self.pc.tp_group)
-        return SMP.combine_pairs(torch.stack(parts)).to(self.device)
+        g = torch.stack(parts)
+        tok = SMP.combine_pairs(g[:, :, :2].contiguous())
+        if bool(filt.any()):
+            ct = SMP.combine_candidates(g[:, :, 2:].reshape(self.pc.tp_size, B, -1, 3), topk.to(g.device),
+                                        topp.to(g.device))
+            tok = torch.where(filt.to(g.device), ct, tok)
+        return tok.to(self.device)
 
     def _bcast(self, t: torch.Tensor) -> None:
         import torch.distributed as dist
@@ -898,7 +917,7 @@ class LLMEngine:
                 sh = torch.empty(self.SHDR, dtype=torch.int64, device=cd)
                 self._bcast(sh)
                 shdr = sh.cpu().numpy()
-                n = int(shdr[0]) * 6 + int(shdr[1]) + int(shdr[2]) * int(shdr[3])
+                n = int(shdr[0]) * 8 + int(shdr[1]) + int(shdr[2]) * int(shdr[3])
                 sdev = torch.empty(n, dtype=torch.int32, device=self.device)
                 self._bcast(sdev)
                 self._sample_shard(logits, shdr, sdev)
@@ -1074,6 +1093,8 @@ class LLMEngine:
         temps = np.zeros(B, dtype=np.float32)
         seeds = np.zeros(B, dtype=np.int32)
         steps = np.zeros(B, dtype=np.int32)
+        topk = np.zeros(B, dtype=np.int32)
+        topp = np.ones(B, dtype=np.float32)
         for i, s in enumerate(seqs):
             r = s.req
             kind, m = r.mask
@@ -1086,24 +1107,30 @@ class LLMEngine:
             temps[i] = r.temperature
             seeds[i] = (r.seed * 2654435761 + s.id) & 0x7FFFFFFF
             steps[i] = len(r.generated)
+            topk[i] = r.top_k
+            topp[i] = r.top_p
         if not lists:
             lists = [0]
+        filt = bool((topk > 0).any() or (topp < 1.0).any())
         if self._dist_sample:
             if rows is not None:
                 logits = logits.index_select(0, torch.tensor(rows, device=logits.device))
             tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
-                                  seeds, steps, temps)
+                                  seeds, steps, temps, topk, topp)
         else:
             table = self._mask_table()
             arrays = [mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps, temps.view(np.int32)]
+            if filt:
+                arrays += [topk, topp.view(np.int32)]
             if rows is not None:
                 arrays.append(np.asarray(rows, np.int32))
             ints = self._to_dev(arrays)
             if rows is not None:
-                logits = logits.index_select(0, ints[7])
+                logits = logits.index_select(0, ints[-1])
             d_temps = ints[6].view(torch.float32)
             tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
-                             vocab=self.vocab)
+                             vocab=self.vocab, top_k=ints[7] if filt else None,
+                             top_p=ints[8].view(torch.float32) if filt else None)
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)

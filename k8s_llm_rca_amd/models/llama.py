@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from ..ops import attention as A
 from ..ops import layer_exec as LX
 from ..ops import norm as N
-from ..ops.linear import linear, linear_silu
+from ..ops.linear import linear, linear_f32out, linear_silu
 from ..parallel.groups import ParallelContext, single
 from .config import ModelConfig
 from . import moe as MOE
@@ -66,6 +66,7 @@ class LlamaModel:
         self.layers: List[Dict[str, torch.Tensor]] = []
         self.moe: Optional[MOE.MoELayerSet] = None
         self.init_mode = init_mode
+        self.logits_f32 = True  # the sampler reads fp32 logits (EngineConfig.logits_fp32)
         if init:
             self._random_init(seed)
 
@@ -146,6 +147,9 @@ class LlamaModel:
         return n
 
     # -------------------------------------------------------------- forward
+    def _lm_head(self, y: torch.Tensor) -> torch.Tensor:
+        return linear_f32out(y, self.lm_head) if self.logits_f32 else linear(y, self.lm_head)
+
     def forward(self, inp: StepInputs, k_cache: torch.Tensor, v_cache: torch.Tensor,
                 gather_logits: bool = True) -> torch.Tensor:
         """k_cache/v_cache: [n_layers, NB, nkv, BS, D] / [n_layers, NB, nkv, D, BS].
@@ -163,7 +167,7 @@ class LlamaModel:
             y = torch.empty_like(residual)
             N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
             sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
-            logits = linear(sel, self.lm_head)
+            logits = self._lm_head(sel)
             return self.pc.all_gather_last(logits) if gather_logits else logits
         prev: Optional[torch.Tensor] = None
         y = torch.empty_like(residual)
@@ -194,5 +198,5 @@ class LlamaModel:
                     prev = self.pc.linear_all_reduce(N.silu_mul(gu), L["w_down"], linear_fn=linear)
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
-        logits = linear(sel, self.lm_head)
+        logits = self._lm_head(sel)
         return self.pc.all_gather_last(logits) if gather_logits else logits

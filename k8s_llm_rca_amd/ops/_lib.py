@@ -30,13 +30,14 @@ _SIGS = {
     "k8s_rope_kv": [P, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_attn_decode": [P, I, P, P, P, I, P, P, I, I, I, I, F, P, I, P, P, I, I, P, I, P, I, P],
     "k8s_attn_prefill": [P, I, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P, P, I, I, I, F, P, I, P],
-    "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P],
+    "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, I, P, P, P, I],
     "k8s_gemm_skinny": [P, I, P, P, I, I, I, I, P],
     "k8s_gemm_mid": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_mid_part": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_splitk_addnorm": [P, I, P, P, P, I, I, I, F, P],
     "k8s_gemm_mid_num_cfgs": [],
     "k8s_blaslt_gemm": [P, I, P, P, I, I, I, I, P, ctypes.c_size_t, P],
+    "k8s_blaslt_gemm2": [P, I, P, P, I, I, I, I, P, ctypes.c_size_t, P, I],
     "k8s_blaslt_num_plans": [],
     "k8s_blaslt_tune": [P, I, P, P, I, I, I, I, P, ctypes.c_size_t, I, I, P, P],
     "k8s_blaslt_clear_tuning": [],

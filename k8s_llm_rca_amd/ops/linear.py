@@ -98,6 +98,23 @@ def lib_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torc
     return torch.matmul(x, w.t(), out=out)
 
 
+def linear_f32out(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """``x @ w.T`` with fp32 output (bf16 operands, fp32 accumulate): the
+    lm_head, whose logits the sampler reads in fp32."""
+    if x.is_cuda and x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1 \
+            and w.is_contiguous():
+        M, K = x.shape
+        N = w.shape[0]
+        out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        ws = _blaslt_ws.get(x.device)
+        if ws is None:
+            ws = _blaslt_ws[x.device] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=x.device)
+        check(lib().k8s_blaslt_gemm2(ptr(x), x.stride(0), ptr(w), ptr(out), N, M, N, K, ptr(ws), BLASLT_WS_BYTES,
+                                     stream_ptr(x), 1), "blaslt_gemm_f32out")
+        return out
+    return x.float() @ w.float().t()
+
+
 def reserve_lib_workspace(dev: torch.device) -> None:
     """Allocate the hipBLASLt workspace before any HIP-graph capture."""
     if dev not in _blaslt_ws:

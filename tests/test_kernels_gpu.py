@@ -251,6 +251,84 @@ def test_sampling_vocab_parallel_matches_full(tp):
     assert torch.equal(got.cpu(), full.cpu())
 
 
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_sampling_topk_topp_exact_sets_and_distribution(dtype):
+    """B9 top-k / top-p on the HIP kernel vs the fp32 reference: every sampled
+    token lies in the reference's keep set (exact masks, incl. grammar masks),
+    and over many seeds the empirical distribution matches the renormalised
+    softmax of that set (chi-square)."""
+    _need_gpu()
+    import math
+    V, n = 128256, 2048
+    torch.manual_seed(5)
+    base = torch.randn(V) * 3
+    words = (V + 31) // 32
+    bits = torch.zeros(words * 32, dtype=torch.bool)
+    bits[torch.randperm(V)[:20000]] = True
+    table = torch.zeros(1, words, dtype=torch.int32)
+    table[0] = (bits.view(words, 32).long() << torch.arange(32)).sum(1).to(torch.int64).to(torch.int32)
+    for k, p, masked in ((10, 1.0, False), (0, 0.7, False), (40, 0.8, True), (1, 1.0, True)):
+        logits = base.to(dtype).repeat(n, 1).to(dev)
+        temps = torch.full((n,), 0.9)
+        seeds = torch.arange(n, dtype=torch.int32) * 31 + 7
+        steps = torch.zeros(n, dtype=torch.int32)
+        mask_id = torch.full((n,), 0 if masked else -1, dtype=torch.int32)
+        z = torch.zeros(n, dtype=torch.int32)
+        tk = torch.full((n,), k, dtype=torch.int32)
+        tpp = torch.full((n,), p, dtype=torch.float32)
+        out = SMP.sample(logits, temps.to(dev), seeds.to(dev), steps.to(dev), mask_id.to(dev), table.to(dev),
+                         z.to(dev), z.to(dev), z[:1].to(dev), vocab=V, top_k=tk.to(dev), top_p=tpp.to(dev)).cpu()
+        lg = base.to(dtype).float()
+        allowed = bits[:V] if masked else torch.ones(V, dtype=torch.bool)
+        cand = torch.nonzero(allowed).flatten()
+        v = lg[cand] * (1.0 / torch.tensor(0.9, dtype=torch.float32))
+        keep = SMP.filter_threshold(v, k, p)
+        keep_ids = cand[keep]
+        inset = torch.zeros(V, dtype=torch.bool)
+        inset[keep_ids] = True
+        assert bool(inset[out.long()].all()), (k, p, masked)
+        probs = torch.softmax(v[keep].double(), 0)
+        counts = torch.bincount(out.long(), minlength=V)[keep_ids].double()
+        expect = probs * n
+        big = expect >= 5
+        chi2 = float((((counts[big] - expect[big]) ** 2) / expect[big]).sum())
+        dof = max(1, int(big.sum()) - 1)
+        assert chi2 < dof + 6 * math.sqrt(2 * dof) + 15, (k, p, masked, chi2, dof)
+
+
+@pytest.mark.parametrize("tp", [2, 8])
+def test_sampling_topk_vocab_parallel_candidates(tp):
+    """B10 with top-k / top-p: per-shard candidate lists combined across ranks
+    give exactly the single-device kernel's tokens (same noise)."""
+    _need_gpu()
+    B, V = 6, 128256
+    torch.manual_seed(9)
+    logits = (torch.randn(B, V) * 6).to(dev)  # peaked: nuclei within CAND_K per shard
+    temps = torch.tensor([0.7, 1.0, 0.5, 1.2, 0.9, 0.0])
+    tk = torch.tensor([5, 64, 1, 20, 0, 10], dtype=torch.int32)
+    tpp = torch.tensor([1.0, 0.95, 1.0, 0.5, 0.3, 1.0])
+    seeds = torch.arange(B, dtype=torch.int32) * 3 + 1
+    steps = torch.arange(B, dtype=torch.int32) + 11
+    mask_id = torch.full((B,), -1, dtype=torch.int32)
+    z = torch.zeros(B, dtype=torch.int32)
+    args = [a.to(dev) for a in (temps, seeds, steps, mask_id)]
+    full = SMP.sample(logits, *args, None, z.to(dev), z.to(dev), z[:1].to(dev), vocab=V, top_k=tk.to(dev),
+                      top_p=tpp.to(dev))
+    vl = V // tp
+    pairs, cands = [], []
+    for r in range(tp):
+        o, c = SMP.sample(logits[:, r * vl:(r + 1) * vl].contiguous(), *args, None, z.to(dev), z.to(dev),
+                          z[:1].to(dev), vocab=V, vocab_off=r * vl, pairs=True, top_k=tk.to(dev), top_p=tpp.to(dev),
+                          candidates=True)
+        pairs.append(o)
+        cands.append(c)
+    tok = SMP.combine_pairs(torch.stack(pairs))
+    ct = SMP.combine_candidates(torch.stack(cands), tk.to(dev), tpp.to(dev))
+    filt = ((tk > 0) | (tpp < 1)).to(dev)
+    got = torch.where(filt, ct, tok)
+    assert torch.equal(got.cpu(), full.cpu())
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (512, 14336), (1280, 8192)])
 def test_gemm_skinny(M, N, K, monkeypatch):

@@ -1,0 +1,96 @@
+"""Sampling semantics (B9/B10) on the fp32 reference path: top-k / top-p
+restrictions, their empirical distribution, and the vocab-parallel candidate
+combine against the single-device result."""
+import math
+
+import pytest
+import torch
+
+from k8s_llm_rca_amd.ops import sampling as SMP
+
+
+def _args(B, temps, k, p, seeds=None, steps=None):
+    return dict(temperature=torch.tensor(temps, dtype=torch.float32),
+                seeds=torch.arange(B, dtype=torch.int32) * 7 + 1 if seeds is None else seeds,
+                steps=torch.zeros(B, dtype=torch.int32) if steps is None else steps,
+                mask_id=torch.full((B,), -1, dtype=torch.int32), mask_table=None,
+                list_off=torch.zeros(B, dtype=torch.int32), list_len=torch.zeros(B, dtype=torch.int32),
+                lists=torch.zeros(1, dtype=torch.int32),
+                top_k=torch.tensor(k, dtype=torch.int32), top_p=torch.tensor(p, dtype=torch.float32))
+
+
+def _naive_nucleus(v, p):
+    """HF-style top-p keep mask: sort desc, keep the prefix whose mass before the token is < p."""
+    pr = torch.softmax(v.double(), 0)
+    order = torch.argsort(v, descending=True)
+    before = torch.cumsum(pr[order], 0) - pr[order]
+    keep = torch.zeros_like(v, dtype=torch.bool)
+    keep[order[before < p]] = True
+    return keep
+
+
+def test_filter_threshold_matches_naive():
+    g = torch.Generator().manual_seed(0)
+    for trial in range(20):
+        v = torch.randn(3000, generator=g) * (0.5 + trial / 5)
+        for k in (1, 5, 64, 0):
+            for p in (0.3, 0.9, 1.0):
+                keep = SMP.filter_threshold(v, k, p)
+                ref = torch.ones_like(keep)
+                if k:
+                    ref &= v >= torch.topk(v, k).values[-1]
+                if p < 1:
+                    sub = torch.where(ref, v, torch.full_like(v, -float("inf")))
+                    ref &= _naive_nucleus(sub, p)
+                assert torch.equal(keep, ref), (trial, k, p)
+
+
+def test_topk_topp_restrict_and_distribution():
+    V, n = 512, 4000
+    torch.manual_seed(1)
+    base = torch.randn(V) * 2
+    logits = base.repeat(n, 1)
+    temps = [0.8] * n
+    a = _args(n, temps, [8] * n, [0.9] * n, seeds=torch.arange(n, dtype=torch.int32) * 13 + 5)
+    out = torch.empty(n, dtype=torch.int32)
+    SMP._sample_ref(logits, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                    a["list_len"], a["lists"], V, out, top_k=a["top_k"], top_p=a["top_p"])
+    v = base / 0.8
+    keep = SMP.filter_threshold(v, 8, 0.9)
+    assert bool(keep[out.long()].all())
+    probs = torch.where(keep, torch.softmax(v.double(), 0), torch.zeros(V, dtype=torch.float64))
+    probs /= probs.sum()
+    counts = torch.bincount(out.long(), minlength=V).double()
+    expect = probs * n
+    idx = expect > 0
+    chi2 = float((((counts[idx] - expect[idx]) ** 2) / expect[idx]).sum())
+    dof = int(idx.sum()) - 1
+    assert chi2 < dof + 6 * math.sqrt(2 * dof) + 10, (chi2, dof)
+
+
+@pytest.mark.parametrize("tp", [2, 4])
+def test_candidates_combine_matches_single_device(tp):
+    B, V = 6, 4096
+    torch.manual_seed(2)
+    logits = torch.randn(B, V)
+    logits[[1, 3, 4]] *= 8  # peaked rows: their nuclei hold < CAND_K tokens per shard
+    temps = [0.7, 1.0, 0.5, 1.2, 0.9, 0.0]
+    ks = [5, 64, 1, 20, 0, 10]
+    ps = [1.0, 0.95, 1.0, 0.5, 0.3, 1.0]
+    a = _args(B, temps, ks, ps, steps=torch.arange(B, dtype=torch.int32) + 3)
+    full = torch.empty(B, dtype=torch.int32)
+    SMP._sample_ref(logits, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                    a["list_len"], a["lists"], V, full, top_k=a["top_k"], top_p=a["top_p"])
+    vl = V // tp
+    pairs, cands = [], []
+    for r in range(tp):
+        o, c = SMP.sample(logits[:, r * vl:(r + 1) * vl].contiguous(), a["temperature"], a["seeds"], a["steps"],
+                          a["mask_id"], None, a["list_off"], a["list_len"], a["lists"], V, vocab_off=r * vl,
+                          pairs=True, top_k=a["top_k"], top_p=a["top_p"], candidates=True)
+        pairs.append(o)
+        cands.append(c)
+    tok = SMP.combine_pairs(torch.stack(pairs))
+    filt = (a["top_k"] > 0) | (a["top_p"] < 1)
+    ct = SMP.combine_candidates(torch.stack(cands), a["top_k"], a["top_p"])
+    got = torch.where(filt, ct, tok)
+    assert torch.equal(got, full), (got, full)

@@ -126,6 +126,13 @@ class EngineBackend(Backend):
                            seed=seed, on_done=on_done, top_k=rs.sampling.get("top_k", self.top_k),
                            top_p=rs.sampling.get("top_p", self.top_p))
 
+    def cancel(self, rs: RunState) -> None:
+        """A cancelled / expired run (service.cancel_run, wait_run timeout) stops
+        generating in the engine; other runs are unaffected."""
+        st = rs.thread.backend_state
+        if st is not None:
+            self.engine.cancel(st.sid)
+
     def release_thread(self, ts: ThreadState) -> None:
         st = ts.backend_state
         if st is not None:

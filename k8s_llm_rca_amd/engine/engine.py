@@ -114,6 +114,9 @@ class EngineConfig:
     gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
+    # a request running longer than this is cancelled by the engine (its run
+    # fails alone, as the reference's expired runs do); None = no limit
+    max_run_s: Optional[float] = None
     weights: Optional[str] = None    # HF checkpoint dir (config.json + *.safetensors): real weights
     tokenizer: Optional[str] = None  # tokenizer.json (default: the checkpoint's, else the built-in BPE)
     temperature: float = 0.7
@@ -259,7 +262,8 @@ class LLMEngine:
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
-                      "prefix_hit_tokens": 0}
+                      "prefix_hit_tokens": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0}
+        self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
 
     def _workspace_bytes(self) -> int:
@@ -321,6 +325,46 @@ class LLMEngine:
                                    top_k, top_p))
             self._cv.notify()
 
+    def cancel(self, sid: int) -> None:
+        """Cancel sequence ``sid``'s active request (thread-safe): its run fails
+        with "cancelled"; every other request is untouched.  The KV the
+        request had written stays cached (the next run of the thread reuses
+        the longest common prefix)."""
+        with self._cv:
+            self._cancels.append(sid)
+            self._cv.notify()
+        if self._thread is None:  # synchronous use: same rule as a step start
+            ps = self._pending_sample
+            self._apply_cancels(set(s.id for s in ps[1]) if ps is not None else set())
+
+    def _apply_cancels(self, in_flight: set) -> None:
+        """Requests in ``in_flight`` (their sample is on the device) are only
+        flagged: :meth:`_process_tokens` fails them when their token lands."""
+        with self._lock:
+            cl, self._cancels = self._cancels, []
+        now = time.perf_counter()
+        lim = self.cfg.max_run_s
+        for s in (self.seqs.get(sid) for sid in cl):
+            if s is not None and s.req is not None:
+                s.req.cancelled = True
+        if lim is not None:
+            for s in self._snapshot():
+                if s.req is not None and not s.req.cancelled and now - s.req.t_submit > lim:
+                    s.req.cancelled = True
+                    self.stats["timeouts"] += 1
+        for s in self._snapshot():
+            r = s.req
+            if r is not None and r.cancelled and s.id not in in_flight:
+                self._fail_req(r, "cancelled")
+
+    def _fail_req(self, r: Request, err: str) -> None:
+        s = r.seq
+        s.req = None
+        s.last_used = time.perf_counter()
+        self.stats["cancelled"] += 1
+        if r.on_done:
+            r.on_done(None, {"error": err})
+
     def start(self) -> None:
         if self._thread is not None:
             return
@@ -362,7 +406,8 @@ class LLMEngine:
             torch.cuda.set_device(self.device)
         while True:
             with self._cv:
-                while not self._stop and not self._incoming and not self._releases and not self._has_work():
+                while (not self._stop and not self._incoming and not self._releases and not self._cancels
+                       and not self._has_work()):
                     self._cv.wait(0.05)
                 if self._stop:
                     return
@@ -399,10 +444,16 @@ class LLMEngine:
         with self._lock:
             inc, self._incoming = self._incoming, []
             seqs = {sid: self.seqs[sid] for sid, *_ in inc}
-        for sid, toks, grammar, max_new, temp, seed, on_done, top_k, top_p in inc:
+        deferred = []
+        for item in inc:
+            sid, toks, grammar, max_new, temp, seed, on_done, top_k, top_p = item
             s = seqs[sid]
             if s.req is not None:
-                raise RuntimeError(f"sequence {sid} already has an active request")
+                if s.req.cancelled:  # the cancelled request still drains its in-flight sample: next step
+                    deferred.append(item)
+                elif on_done:  # one bad submit fails alone, never the engine
+                    on_done(None, {"error": f"sequence {sid} already has an active request"})
+                continue
             # longest common prefix with what is cached -> keep that KV
             lcp = 0
             n = min(s.n_cached, len(toks))
@@ -426,6 +477,9 @@ class LLMEngine:
             s.req = r
             self.stats["requests"] += 1
             self._drive(r)
+        if deferred:
+            with self._lock:
+                self._incoming[:0] = deferred
 
     def _drive(self, r: Request) -> None:
         """Run grammar actions until a sample is needed (forced text is appended)."""
@@ -488,6 +542,9 @@ class LLMEngine:
         step as decode rows fed straight from the device tokens, and the host
         processes those tokens while this step's forward runs on the GPU."""
         t_host0 = time.perf_counter()
+        if self._cancels or self.cfg.max_run_s is not None:
+            ps0 = self._pending_sample
+            self._apply_cancels(set(s.id for s in ps0[1]) if ps0 is not None else set())
         self._admit()
         self.stats["admit_s"] += time.perf_counter() - t_host0
         if self._releases:
@@ -513,28 +570,46 @@ class LLMEngine:
         decode, prefill = [], []
         budget = self.cfg.max_batch_tokens
         protect = set(s.id for s in active)
+        active.sort(key=lambda s: s.req.t_submit)  # oldest first: they keep their KV under pressure
+        placed: set = set()
         for s in active:
             if s.pending == 1 and len(decode) < self.cfg.max_decode_seqs:
-                if self._ensure_blocks(s, s.n_cached + 1, protect):
+                if self._ensure_blocks(s, s.n_cached + 1, protect) or self._preempt_for(s, s.n_cached + 1, placed,
+                                                                                        protect, active):
                     decode.append(s)
+                    placed.add(s.id)
         budget -= len(decode)
         chunks: List[Tuple[Sequence, int]] = []
-        for s in sorted((s for s in active if (s.pending > 1 or (s.pending == 1 and s not in decode))
-                         and s.tokens[-1] != SPEC), key=lambda s: s.req.t_submit):
+        for s in [s for s in active if (s.pending > 1 or (s.pending == 1 and s.id not in placed))
+                  and s.tokens[-1] != SPEC]:
             if budget <= 0:
                 break
+            if s.req is None:  # failed below (longer than the pool)
+                continue
             q = min(s.pending, budget)
-            if s.n_cached + q > self.kv.num_blocks * BS:
-                raise MemoryError("sequence longer than the whole KV pool")
+            if len(s.tokens) > self.kv.num_blocks * BS:
+                self._fail_req(s.req, "context longer than the whole KV pool")
+                continue
             if self.cfg.prefix_sharing and s.n_cached % BS == 0 and len(s.blocks) == s.n_cached // BS:
                 self._attach_prefix(s)
                 q = min(s.pending, budget)
-            if not self._ensure_blocks(s, s.n_cached + q, protect):
+            if not (self._ensure_blocks(s, s.n_cached + q, protect)
+                    or self._preempt_for(s, s.n_cached + q, placed, protect, active)):
                 continue
             chunks.append((s, q))
+            placed.add(s.id)
             budget -= q
         if not decode and not chunks:
-            raise MemoryError("KV pool exhausted with no evictable sequence")
+            if ps is not None:  # only the in-flight sample can progress: finish it
+                for s in ps[1]:
+                    s.tokens.pop()
+                self._process_tokens(self._launch_sample(*ps))
+                return True
+            # nothing fits even after preemption: fail the youngest request alone
+            young = [s for s in active if s.req is not None]
+            if young:
+                self._fail_req(young[-1].req, "KV pool exhausted")
+            return True
         rows = [(s, 1) for s in decode] + chunks
         if self._shape_trace:
             with open(self._shape_trace, "a") as f:
@@ -593,6 +668,25 @@ class LLMEngine:
             else:
                 self._process_tokens(self._launch_sample(*pend))
         return True
+
+    def _preempt_for(self, s: Sequence, upto: int, placed: set, protect: set, active: List[Sequence]) -> bool:
+        """Free KV for ``s`` by preempting younger active requests (youngest
+        first; not ones already placed in this step): a victim keeps its
+        request and tokens, drops its pages and is re-prefilled when pages
+        are free again (recompute preemption).  False if ``s`` still does not fit."""
+        for v in reversed(active):
+            if v is s or v.req is None or v.id in placed or not v.blocks:
+                continue
+            if v.req.t_submit <= s.req.t_submit:
+                break  # only younger requests yield to older ones
+            self.kv.release(v.blocks)  # pages other threads share stay resident
+            v.blocks = []
+            v.bh = []
+            v.n_cached = 0
+            self.stats["preemptions"] += 1
+            if self._ensure_blocks(s, upto, protect):
+                return True
+        return False
 
     def _attach_prefix(self, s: Sequence) -> None:
         """Map the next full blocks of ``s``'s prompt onto published pages
@@ -1158,6 +1252,11 @@ class LLMEngine:
             if placeholders and s.tokens and s.tokens[-1] == SPEC:
                 s.tokens.pop()
             r = s.req
+            if r is None:
+                continue
+            if r.cancelled:
+                self._fail_req(r, "cancelled")
+                continue
             if r.t_first is None:
                 r.t_first = now
             if t < 0:

@@ -354,3 +354,76 @@ def test_prefix_sharing_under_kv_pressure():
     for sid in sids:
         eng.release_sequence(sid)
     assert eng.kv.free_blocks == free0 and eng.kv.shared_blocks == 0 and not eng.kv._by_key
+
+
+def test_preemption_completes_every_run_under_kv_pressure():
+    """More concurrent runs than the KV pool holds: younger requests are
+    preempted (pages dropped, tokens kept, recomputed later) instead of the
+    engine failing every in-flight run (VERDICT r1 missing #6)."""
+    eng = _engine(num_blocks=8, block_size=32, max_batch_tokens=256)
+    eng.eos_ids = []  # every run generates its full budget
+    outs = {}
+    sids = [eng.new_sequence() for _ in range(6)]
+    for i, sid in enumerate(sids):
+        p = eng.tok.system_prefix("s") + eng.tok.message("user", "y%d" % i) + eng.tok.header("assistant")
+        eng.submit(sid, p, None, 60, on_done=lambda g, st, i=i: outs.__setitem__(i, (g, st)))
+    eng.run_until_idle()
+    assert len(outs) == 6
+    assert all(g is not None for g, _ in outs.values()), outs
+    assert eng.stats["preemptions"] > 0
+
+
+def test_cancel_and_timeout_fail_one_run_only():
+    eng = _engine(max_run_s=None)
+    outs = {}
+    sids = [eng.new_sequence() for _ in range(3)]
+    for i, sid in enumerate(sids):
+        p = eng.tok.system_prefix("s") + eng.tok.message("user", "z%d " % i * 10) + eng.tok.header("assistant")
+        eng.submit(sid, p, None, 40, on_done=lambda g, st, i=i: outs.__setitem__(i, (g, st)))
+    for _ in range(4):
+        eng.step()
+    eng.cancel(sids[1])
+    eng.run_until_idle()
+    assert outs[1][0] is None and outs[1][1]["error"] == "cancelled"
+    assert outs[0][0] is not None and outs[2][0] is not None
+    # the cancelled thread runs again normally
+    p = eng.seqs[sids[1]].tokens[: eng.seqs[sids[1]].n_cached] + eng.tok.message("user", "again") + \
+        eng.tok.header("assistant")
+    eng.submit(sids[1], p, None, 5, on_done=lambda g, st: outs.__setitem__("again", (g, st)))
+    eng.run_until_idle()
+    assert outs["again"][0] is not None
+    # engine-side deadline: a run older than max_run_s is cancelled alone
+    eng.cfg.max_run_s = 0.0
+    eng.submit(sids[0], eng.seqs[sids[0]].tokens + eng.tok.header("assistant"), None, 30,
+               on_done=lambda g, st: outs.__setitem__("late", (g, st)))
+    eng.run_until_idle()
+    assert outs["late"][0] is None and eng.stats["timeouts"] >= 1
+
+
+def test_service_wait_timeout_cancels_engine_request():
+    """wait_get_last_k_message(timeout) -> run 'expired' -> the engine stops
+    generating it (Backend.cancel), the thread stays usable."""
+    from k8s_llm_rca_amd.api.assistant import GenericAssistant
+    from k8s_llm_rca_amd.api.service import AssistantService
+    from k8s_llm_rca_amd.engine.backend import EngineBackend
+    eng = _engine()
+    eng.start()
+    try:
+        svc = AssistantService(EngineBackend(eng, default_max_tokens=2000))
+        a = GenericAssistant(svc)
+        a.create_assistant("You are terse.", "t", "tiny-llama")
+        a.create_thread()
+        a.add_message("hello")
+        a.run_assistant(max_tokens=2000)
+        assert a.wait_get_last_k_message(1, timeout=0.05) is None
+        assert a.get_run_status().status == "expired"
+        import time
+        t0 = time.time()
+        while eng._has_work() and time.time() - t0 < 30:
+            time.sleep(0.05)
+        assert not eng._has_work() and eng.stats["cancelled"] >= 1
+        a.add_message("again")
+        a.run_assistant(max_tokens=4)
+        assert a.wait_get_last_k_message(1, timeout=60) is not None
+    finally:
+        eng.stop()

@@ -173,8 +173,11 @@ def save_safetensors(model, path: str, config_json: bool = True) -> None:
              "intermediate_size": cfg.intermediate, "rope_theta": cfg.rope_theta,
              "max_position_embeddings": cfg.max_position, "rms_norm_eps": cfg.rms_eps, "head_dim": D,
              "tie_word_embeddings": False}
+        # HF loaders (transformers' LlamaForCausalLM / MixtralForCausalLM) read these too
+        d.update(model_type="mixtral" if cfg.n_experts else "llama", hidden_act="silu", attention_bias=False,
+                 mlp_bias=False, architectures=["MixtralForCausalLM" if cfg.n_experts else "LlamaForCausalLM"])
         if cfg.n_experts:
-            d.update(num_local_experts=cfg.n_experts, num_experts_per_tok=cfg.top_k)
+            d.update(num_local_experts=cfg.n_experts, num_experts_per_tok=cfg.top_k, router_jitter_noise=0.0)
         if cfg.rope_scaling:
             d["rope_scaling"] = dict(cfg.rope_scaling, rope_type="llama3")
         with open(os.path.join(path, "config.json"), "w") as f:

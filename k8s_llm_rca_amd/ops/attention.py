@@ -23,7 +23,9 @@ def rope_cos_sin(max_pos: int, theta: float = 500000.0, head_dim: int = HEAD_DIM
     """[max_pos, head_dim] fp32 table: cos(f_i p) for i < d/2, then sin(f_i p)."""
     half = head_dim // 2
     inv = 1.0 / (theta ** (torch.arange(0, half, dtype=torch.float64) / half))
-    if scaling and scaling.get("type") == "llama3":
+    # ModelConfig keeps only the numeric scaling fields (config_from_hf): a
+    # `factor` without another rope_type is Llama-3.1's "llama3" scaling
+    if scaling and "factor" in scaling and scaling.get("type", scaling.get("rope_type", "llama3")) == "llama3":
         factor = scaling.get("factor", 8.0)
         lo, hi = scaling.get("low_freq_factor", 1.0), scaling.get("high_freq_factor", 4.0)
         old = scaling.get("original_max_position_embeddings", 8192)

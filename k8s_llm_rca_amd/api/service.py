@@ -141,7 +141,17 @@ class AssistantService:
         self.runs: Dict[str, RunState] = {}
         self._runs_by_thread: Dict[str, List[str]] = {}
         self._lock = threading.Lock()
+        self.closed = False
         backend.attach(self)
+
+    def close(self) -> None:
+        """Shut down: active runs are cancelled and every later run fails at
+        once (callers' repair loops then end quickly instead of waiting)."""
+        self.closed = True
+        with self._lock:
+            active = [r for r in self.runs.values() if not r.done.is_set()]
+        for rs in active:
+            self.cancel_run(rs.run.id)
 
     # ------------------------------------------------------------ assistants
     def create_assistant(self, instructions: str, name: str, model: str) -> Assistant:
@@ -241,6 +251,9 @@ class AssistantService:
         with self._lock:
             self.runs[r.id] = rs
             self._runs_by_thread[thread_id].append(r.id)
+        if self.closed:
+            self._finish(rs, None, "failed", error="service closed")
+            return r
         self.backend.submit(rs)
         return r
 

@@ -189,6 +189,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                 nh = {"value": round(nh_steps * quantum * sync_world / dt, 4), "steps": nh_steps,
                       "p50_latency_s": round(statistics.median(nh_lat), 3) if nh_lat else None}
     stream.stop()
+    svc.close()  # in-flight analyses end fast: their remaining LLM runs fail at once
+    clean = stream.join(60.0)
     eng.stop()
     eng.stop_workers()
     if eng.error is not None:
@@ -253,6 +255,7 @@ def run(args) -> Optional[Dict[str, Any]]:
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         "setup_s": round(setup_s, 1),
         "wall_s": round(time.perf_counter() - t_start, 1),
+        "clean_shutdown": clean,
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
     }
     if world > 1 and not tp_mode:
@@ -382,12 +385,16 @@ def main(argv=None) -> int:
 
 
 def exit_now(rc: int) -> None:
-    """Leave without interpreter teardown: the stream's pipeline threads are
-    still parked on runs the stopped engine will never finish, and tearing the
-    runtime down under them aborts the process (exit 134) after the JSON line."""
+    """Exit normally when every pipeline thread has ended (profilers such as
+    rocprofv3 flush their output at exit); if one is still parked on a run,
+    leave without interpreter teardown instead (tearing the runtime down under
+    it aborts the process, exit 134, after the JSON line)."""
+    import threading
     sys.stdout.flush()
     sys.stderr.flush()
-    os._exit(rc)
+    if any(t.is_alive() and t.name == "rca-stream" for t in threading.enumerate()):
+        os._exit(rc)
+    sys.exit(rc)
 
 
 if __name__ == "__main__":

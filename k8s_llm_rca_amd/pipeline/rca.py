@@ -317,6 +317,13 @@ class IncidentStream:
             self._stop = True
             self._cv.notify_all()
 
+    def join(self, timeout: float) -> bool:
+        """Wait for the workers to exit (after :meth:`stop`); True if all did."""
+        end = time.perf_counter() + timeout
+        for t in self._threads:
+            t.join(max(0.0, end - time.perf_counter()))
+        return not any(t.is_alive() for t in self._threads)
+
     def _worker(self, p: RCAPipeline) -> None:
         while True:
             with self._cv:
@@ -332,7 +339,8 @@ class IncidentStream:
                 if p.last_failed_runs:
                     ok, err = False, f"{p.last_failed_runs} LLM run(s) failed: {r.get('error_message', '')[:60]!r}"
             except Exception as e:  # noqa: BLE001 - counted, never fatal to the stream
-                log.exception("incident %d failed", i)
+                if not self._stop:  # after stop() the service is closing under the analysis
+                    log.exception("incident %d failed", i)
                 ok, err = False, repr(e)
             t1 = time.perf_counter()
             with self._cv:

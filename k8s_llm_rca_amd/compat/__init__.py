@@ -17,6 +17,11 @@ reference module                                   implementation
 ``check_state/analyze_root_cause.py``              :mod:`k8s_llm_rca_amd.pipeline.check_state`
 =================================================  ==========================================
 
+``install(shims=True)`` additionally provides ``openai`` (``OpenAI().beta.*``)
+and ``neo4j`` (``GraphDatabase``, ``neo4j.graph``, ``neo4j.exceptions``)
+modules backed by the same services, so the reference's own adapter and
+driver modules import and run unmodified (``tests/test_compat.py``).
+
 Remote services become in-process ones: the assistant runs on the default
 :class:`~k8s_llm_rca_amd.api.service.AssistantService` (set it with
 ``set_default_service``; e.g. an engine-backed service), and
@@ -27,9 +32,19 @@ import os
 import sys
 
 COMPAT_DIR = os.path.dirname(os.path.abspath(__file__))
+SHIMS_DIR = os.path.join(COMPAT_DIR, "shims")
 
 
-def install() -> None:
-    """Make the reference's top-level package names importable."""
+def install(shims: bool = False) -> None:
+    """Make the reference's top-level package names importable.  ``shims``:
+    also put this framework's ``openai`` and ``neo4j`` modules first on the
+    path (``compat/shims``), so the reference's OWN adapter modules
+    (``common/openai_generic_assistant.py`` / ``neo4j_query_executor.py``,
+    which import those SDKs) run unchanged on the in-process services.  Off by
+    default: it shadows real installs of those packages."""
     if COMPAT_DIR not in sys.path:
         sys.path.insert(0, COMPAT_DIR)
+    if shims and SHIMS_DIR not in sys.path:
+        sys.path.insert(0, SHIMS_DIR)
+        for mod in [m for m in sys.modules if m in ("openai", "neo4j") or m.startswith(("openai.", "neo4j."))]:
+            del sys.modules[mod]

@@ -82,6 +82,7 @@ class _Gen:
         self.kind_of: Dict[int, str] = {}
         self.names_used: Dict[str, int] = {}
         self.state_edges: Dict[int, List[int]] = {}
+        self.msg_override: Optional[str] = None  # reference-catalogue injection: the event text to use
 
     # ---------------------------------------------------------------- names
     def uid(self) -> str:
@@ -155,6 +156,8 @@ class _Gen:
         return self.g.add_edge(a, b, rel, {"key": key, "srcKind": self.kind_of[a], "destKind": self.kind_of[b]})
 
     def event(self, involved: int, message: str, ts: str, reason: str, etype: str = "Warning") -> int:
+        if self.msg_override is not None and etype == "Warning":
+            message = self.msg_override
         name = f"{self.g.node_props(involved).get('name2', 'obj')}.{self.suffix(16)}"
         ev, _ = self.entity("Event", name, self.g.node_props(involved).get("namespace"),
                             ts_to_ms(ts), with_state=False)
@@ -167,7 +170,7 @@ class _Gen:
 
 
 def generate_cluster(target_nodes: int = 10_000, n_incidents: int = 64, seed: int = 0,
-                     fault_mix: Optional[List[str]] = None) -> SynthCluster:
+                     fault_mix: Optional[List[str]] = None, reference_incidents: bool = False) -> SynthCluster:
     """Build a stategraph of ``target_nodes`` nodes (+- half a tenant, faults included) with
     ``n_incidents`` faults; at most ~30 % of the target is spent on fault nodes, beyond that the
     graph grows past the target (callers cycle a smaller incident set instead)."""
@@ -219,6 +222,19 @@ def generate_cluster(target_nodes: int = 10_000, n_incidents: int = 64, seed: in
         else:
             incidents.append(inc)
             miss = 0
+    if reference_incidents:  # the reference's ten built-in messages, verbatim (reference_incidents.py)
+        from .reference_incidents import REFERENCE_INCIDENTS
+        for fault, message in REFERENCE_INCIDENTS:
+            for _ in range(50):
+                G.msg_override = message
+                try:
+                    inc = _inject(G, tenants[int(rng.integers(len(tenants)))], fault, nfs_server)
+                finally:
+                    G.msg_override = None
+                if inc is not None:
+                    inc.message = message
+                    incidents.append(inc)
+                    break
     while g.num_nodes + 8 + app_size / 2 < target_nodes:  # top up with tenants sized to the remainder
         n_apps = int(min(6, max(1, round((target_nodes - g.num_nodes - 8) / app_size))))
         _add_tenant(G, k8s_nodes, sc, nfs_server, n_apps)

@@ -2,6 +2,7 @@
 the reference's ``test_all.py:54-131`` runs unchanged against this framework
 (scripted replies in place of GPT-4, a synthetic graph file in place of Neo4j)."""
 import json
+import os
 
 import pytest
 
@@ -82,3 +83,71 @@ def test_reference_driver_runs_on_compat_paths(ref_env):
     assert n_records >= 1
     metagraph.close()
     stategraph.close()
+
+
+REF = "/root/reference"
+
+
+@pytest.mark.skipif(not os.path.isfile(os.path.join(REF, "test_all.py")), reason="reference checkout not present")
+def test_reference_test_all_runs_unchanged_on_shims(monkeypatch, capsys):
+    """The reference's OWN ``test_all.py`` (and its ``common/``, ``find_metapath/``,
+    ``generate_query/``, ``check_state/`` modules, none of them modified) runs
+    end to end on this framework: ``openai`` / ``neo4j`` resolve to the
+    compat shims, the hard-coded ``bolt://`` URIs to a synthetic graph that
+    holds the reference's built-in incident messages, GPT-4 to a scripted
+    responder.  VERDICT r1 missing #8."""
+    import importlib.util
+    import sys
+    import time as _time
+
+    from k8s_llm_rca_amd.compat import COMPAT_DIR, SHIMS_DIR
+    from k8s_llm_rca_amd.graph.synth import generate_cluster
+    from k8s_llm_rca_amd.pipeline.generate_query import human_generate_cypher_query
+
+    c = generate_cluster(600, 0, seed=4, reference_incidents=True)
+    inc = next(i for i in c.incidents if i.fault == "nfs_missing")  # test_all.py processes errorMessages[1:2]
+    saved_path = list(sys.path)
+    names = ("common", "find_metapath", "generate_query", "check_state", "openai", "neo4j", "test_all")
+    saved_mods = {k: v for k, v in sys.modules.items() if k.split(".")[0] in names}
+    for k in saved_mods:
+        del sys.modules[k]
+    # the reference's `common` is a namespace package: our compat copy (a regular
+    # package) would win over it, so it is taken off the path here
+    sys.path[:] = [SHIMS_DIR, REF] + [p for p in saved_path if p != COMPAT_DIR]
+    try:
+        import neo4j  # the shim
+        assert neo4j.__file__.startswith(SHIMS_DIR)
+        neo4j.map_uri("bolt://10.1.0.176:7687", c.metagraph)
+        neo4j.map_uri("bolt://10.1.0.174:7687", c.stategraph)
+
+        def responder(rs):
+            last = rs.thread.messages[-1].text
+            if "DestinationKind" in last:
+                return "```json\n" + json.dumps({"SourceKind": inc.src_kind, "DestinationKind": inc.dest_kind,
+                                                 "RelevantResources": inc.path_kinds, "PrimaryPath": []}) + "\n```"
+            if "generation-template-1" in last:
+                mp = last.split("the provided metapath is:\n")[1].split("\n    the error message to filtering")[0]
+                mp = mp.strip("\n").replace("\n    ", "\n")
+                mp = "\n" + "\n".join("    " + ln.strip() for ln in mp.splitlines() if ln.strip()) + "\n"
+                return "```cypher\n" + human_generate_cypher_query(mp, inc.message) + "\n```"
+            if "relevance_score" in last:
+                return '{"summary": [], "conclusion": "nfs path missing", "resolution": "kubectl describe pv"}'
+            return "the STATE shows the nfs export is gone"
+
+        set_default_service(AssistantService(ScriptedBackend(responder)))
+        monkeypatch.setattr(_time, "sleep", lambda s: None)  # the reference polls with sleep(5 * i)
+        spec = importlib.util.spec_from_file_location("test_all", os.path.join(REF, "test_all.py"))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        assert mod.Neo4jQueryExecutor.__module__ == "common.neo4j_query_executor"
+        assert sys.modules["common.neo4j_query_executor"].__file__.startswith(REF)  # the reference's own adapter
+        mod.main()
+    finally:
+        sys.path[:] = saved_path
+        for k in [k for k in sys.modules if k.split(".")[0] in names]:
+            del sys.modules[k]
+        sys.modules.update(saved_mods)
+        set_default_service(None)
+    out = capsys.readouterr().out
+    assert "nfs path missing" in out  # check_statepath's summary report was printed
+    assert "close connection" in out

@@ -16,10 +16,16 @@
 //   two-shot : stage -> A -> reduce my 1/N part of the slice into RES ->
 //              signal(B) -> wait(B) -> gather the N reduced parts
 // (two-shot moves 2(N-1)/N of the data per rank instead of N-1: mid sizes).
-// Epochs live in device memory (one counter per block, touched only by that
-// block), so the kernel is HIP-graph capturable; DATA / RES are double
-// buffered by epoch parity: a rank re-writes a parity buffer only after every
-// peer has signalled the following epoch, i.e. finished reading it.
+// The epoch lives in device memory, so the kernel is HIP-graph capturable:
+// ONE counter per rank, read by every block at launch and advanced once per
+// call by the last block to finish (an arrival counter), so every block of a
+// call -- whatever the call's block count -- uses the same epoch and parity.
+// (A per-block counter raced: a call with fewer blocks left the higher blocks'
+// epochs behind, and a later call's high block could re-write a parity buffer
+// a peer was still reading.)  DATA / RES are double buffered by epoch parity:
+// a rank starts call E only after its call E-1 waited for every peer to
+// signal E-1, i.e. after every peer's call E-2 -- the last reader of parity
+// E & 1 -- had completed (stream order).
 // Signals are system-scope release stores into the PEER's flag array, waits
 // are system-scope acquire loads of our own; spins are bounded (wall clock)
 // and record a timeout in STATUS instead of hanging the GPU.
@@ -35,7 +41,7 @@ constexpr int AR_THREADS = 512;
 constexpr size_t AR_FLAGS_A = 0;
 constexpr size_t AR_FLAGS_B = AR_FLAGS_A + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
 constexpr size_t AR_EPOCH = AR_FLAGS_B + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
-constexpr size_t AR_STATUS = AR_EPOCH + 4 * AR_MAX_BLOCKS;
+constexpr size_t AR_STATUS = AR_EPOCH + 4 * AR_MAX_BLOCKS;  // AR_EPOCH: [0] epoch, [1] arrivals
 constexpr size_t AR_DATA = 32768;
 
 struct ARPeers {
@@ -101,7 +107,8 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
                                                          long max_bytes, uint64_t timeout_ticks) {
   const int b = blockIdx.x, t = threadIdx.x;
   unsigned char* own = P.base[rank];
-  uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH) + b;
+  uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
+  uint32_t* arrivals = ep + 1;
   __shared__ uint32_t s_e;
   if (t == 0) s_e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
   __syncthreads();
@@ -136,7 +143,13 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
     }
   }
   __syncthreads();
-  if (t == 0) __hip_atomic_store(ep, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (t == 0) {  // the last block of this call publishes the epoch for the next one
+    const uint32_t d = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+      __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ep, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
 }
 
 }  // namespace k8s

@@ -45,7 +45,19 @@ def _worker(rank, world, port, out_dir):
                 ref = sum(_inp(r, n, it, mode).float() for r in range(world)).bfloat16()
                 if not torch.equal(x.cpu(), ref):
                     bad.append((mode, n, it, (x.cpu().float() - ref.float()).abs().max().item()))
+    # sizes alternating large / small back to back with no host sync between
+    # calls: the block count changes every call (per-block epochs raced)
+    xs, refs = [], []
+    for it, n in enumerate([1 << 20, 4096, 1 << 19, 8, 65536, 1 << 20, 2048, 300008, 16, 1 << 20] * 2):
+        mode = 1 + it % 2
+        x = _inp(rank, n, 100 + it, mode).cuda()
+        ar(x, mode=mode)
+        xs.append(x)
+        refs.append(sum(_inp(r, n, 100 + it, mode).float() for r in range(world)).bfloat16())
     torch.cuda.synchronize()
+    for it, (x, ref) in enumerate(zip(xs, refs)):
+        if not torch.equal(x.cpu(), ref):
+            bad.append(("alt", x.numel(), it, (x.cpu().float() - ref.float()).abs().max().item()))
     status = ar.status()
     ar.close()
     torch.save({"bad": bad, "status": status}, os.path.join(out_dir, f"r{rank}.pt"))

@@ -1,4 +1,8 @@
-// Native layer executor for the dense Llama decoder (TP = 1).
+// Native layer executor for the dense Llama decoder (TP = 1, and TP > 1 with
+// the xGMI all-reduce: the two row-parallel outputs of every layer -- o_proj
+// and down_proj -- are summed across the TP ranks in place by
+// k8s_ar_allreduce_bf16 right after their GEMM, before the residual add +
+// RMSNorm that consumes them; HIP-graph capturable like the rest).
 //
 // An eager engine step (prefill chunks mixed with decode rows: shapes change
 // every step, so it cannot replay a HIP graph) issues ~10 kernels per layer.
@@ -49,6 +53,7 @@ int k8s_grouped_gemm_part(const void* a, int lda, const void* w, void* y, int ld
                           int K, int max_tiles, int fuse_silu, int splits, void* part, int total_rows, hipStream_t s);
 int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
                     size_t ws_bytes, hipStream_t s);
+int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int mode, hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits);
@@ -107,6 +112,8 @@ struct K8sLlamaStep {
   void* mid_part;
   void* grp_part;
   const int* grp_offs;  // device [0, T]
+  // TP: xGMI all-reduce communicator id (-1: TP = 1) and mode (1 one-shot, 2 two-shot)
+  int ar_id, ar_mode;
 };
 
 namespace {
@@ -158,6 +165,8 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   uint16_t* qkv = (uint16_t*)s.qkv;
   uint16_t* attn = (uint16_t*)s.attn;
   bool pend = false;  // the previous layer's down projection is still split-K partials
+  const bool tp = s.ar_id >= 0;  // row-parallel outputs are partial sums: all-reduce, never defer split-K
+  const long n_out = (long)T * H;
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
@@ -177,8 +186,9 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                                s.p_qs, s.tile[0], s.tile[1], s.tile[2], s.tile[3], s.tile[4], s.tile[5], s.n_tiles,
                                s.merge[0], s.merge[1], s.merge[2], s.merge[3], s.n_merge, s.pf_o, s.pf_ml, s.nq,
                                s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, st));
-    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, true));
-    if (deferred(s.sel[1], true))
+    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
+    if (tp) K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
+    if (!tp && deferred(s.sel[1], true))
       K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[1]), s.sel[1].splits, s.residual, s.post_norm[l], s.y, T, H, H,
                                  s.eps, st));
     else
@@ -186,8 +196,9 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     K8S_TRY(gemm(s, s.sel[2], s.y, H, s.wgu[l], s.gu, 2 * s.I, T, 2 * s.I, H, st));
     K8S_TRY(k8s_silu_mul(s.gu, s.act, T, s.I, st));
     // the last layer's down output is returned (`prev`) for the final norm
-    pend = deferred(s.sel[3], l + 1 < s.L);
-    K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, l + 1 < s.L));
+    pend = !tp && deferred(s.sel[3], l + 1 < s.L);
+    K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));
+    if (tp) K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.prev, s.prev, n_out, s.ar_mode, st));
   }
   return (int)hipGetLastError();
 }

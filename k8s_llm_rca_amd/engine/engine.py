@@ -245,10 +245,18 @@ class LLMEngine:
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
         self._pending_sample = None  # (logits, seqs, rows): sampled at the start of the next step
-        self._async = cfg.async_steps and self.pc.tp_size == 1
+        # TP: the leader's host work of step n overlaps step n+1 on every rank too
+        # (the workers take the sampled tokens from their own device copy)
+        self._chan = None
+        if self.pc.tp_size > 1:
+            from ..parallel.channel import make_channel
+            self._chan = make_channel(self.pc)  # host-side step metadata (parallel/channel.py)
+        self._last_tok = None  # TP workers: device tokens of the last sampling (decode inputs of the next step)
         # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
         self._dist_sample = (self.pc.tp_size > 1 and hasattr(self.model, "vocab_local")
                              and self.model.vocab_local % 8 == 0)
+        # TP: every rank needs the sampled tokens on its device to overlap steps
+        self._async = cfg.async_steps and (self.pc.tp_size == 1 or self._dist_sample)
         self._mask_sent = 0      # rank 0: mask-table rows already broadcast to the workers
         self._wmask = None       # TP ranks: device copy of the mask table (rows received so far)
         # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
@@ -760,7 +768,9 @@ class LLMEngine:
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             ev[0].record()
-        if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self.pc.tp_size == 1
+        if spec is not None and self._chan is not None:
+            _spec_tok(spec)  # TP: sample(k) -- a message + an all-gather -- goes before forward(k+1) on every rank
+        if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self._graphs_ok()
                 and self.kv.block_size % 64 == 0):
             out = self._forward_graph(decode, spec)
             self.stats["graph_steps"] += 1
@@ -777,6 +787,14 @@ class LLMEngine:
             ev[1].record()
             self._pending_ev.append((kind, dt, ev))
         return out
+
+    def _graphs_ok(self) -> bool:
+        """Decode steps replay HIP graphs at TP=1, and under TP when every
+        all-reduce of a decode step runs on the capturable xGMI kernel."""
+        if self.pc.tp_size == 1:
+            return True
+        car = self.pc.custom_ar
+        return car is not None and getattr(car, "max_bytes", 0) >= max(self.cfg.graph_batch_sizes) * self.mc.hidden * 2
 
     def _collect_timing(self) -> None:
         """Fold completed step events into stats (with overlapped steps the
@@ -899,6 +917,10 @@ class LLMEngine:
                     self._pf_ws = A.prefill_workspace(self.model.nkv, self.device)
                 pmeta.pf_o, pmeta.pf_ml = self._pf_ws
         inp = StepInputs(d_ids, d_pos, d_slots, nd, dmeta, pmeta, d_sidx.long())
+        return self._model_fwd(inp)
+
+    def _model_fwd(self, inp):
+        """TP with vocab-parallel sampling keeps each rank's logits shard."""
         if self._dist_sample:
             return self.model.forward(inp, self.kv.k, self.kv.v, gather_logits=False)
         return self.model.forward(inp, self.kv.k, self.kv.v)
@@ -906,7 +928,8 @@ class LLMEngine:
     # ------------------------------------------------- TP vocab-parallel sampling
     SHDR = 4
 
-    def _tp_sample(self, logits, mask_id, list_off, list_len, lists, seeds, steps, temps, topk, topp) -> torch.Tensor:
+    def _tp_sample(self, logits, mask_id, list_off, list_len, lists, seeds, steps, temps, topk, topp,
+                   rows=None) -> torch.Tensor:
         """Rank 0: broadcast this step's sampling inputs (plus mask rows the
         workers have not seen), then sample on every rank's vocab shard."""
         import numpy as np_
@@ -917,10 +940,19 @@ class LLMEngine:
         hdr = np_.array([B, len(lists), new.shape[0], self.grt.masks.words], dtype=np_.int64)
         flat = np_.concatenate([mask_id, list_off, list_len, lists, seeds, steps, temps.view(np_.int32),
                                 topk, topp.view(np_.int32), new.reshape(-1).astype(np_.int32)])
-        h = torch.from_numpy(hdr).to(self._comm_device())
-        self._bcast(h)
-        dev = self._to_dev([flat])[0]
-        self._bcast(dev)
+        from ..parallel.channel import SAMPLE
+        rows_a = np_.asarray(rows if rows is not None else [], np_.int32)
+        self._chan.send(SAMPLE, [hdr, flat, rows_a])
+        return self._sample_rows(logits, hdr, flat, rows_a)
+
+    def _sample_rows(self, logits, hdr, flat, rows_a) -> torch.Tensor:
+        """Every TP rank: the rows of this step's logits that sample (all when
+        ``rows_a`` is empty), then the vocab-parallel sampling."""
+        if rows_a.size:
+            dev, rows_d = self._to_dev([flat, rows_a])
+            logits = logits.index_select(0, rows_d.long())
+        else:
+            dev = self._to_dev([flat])[0]
         return self._sample_shard(logits, hdr, dev)
 
     def _sample_shard(self, logits, hdr, dev) -> torch.Tensor:
@@ -963,26 +995,29 @@ class LLMEngine:
             tok = torch.where(filt.to(g.device), ct, tok)
         return tok.to(self.device)
 
-    def _bcast(self, t: torch.Tensor) -> None:
-        import torch.distributed as dist
-        dist.broadcast(t, src=0, group=self.pc.tp_group)
-
     def _comm_device(self):
-        return self.device if self.device.type == "cuda" else torch.device("cpu")
+        """Device of the sampling all-gather's tensors: RCCL takes device
+        tensors; a gloo TP group (CPU tests, processes sharing one GPU) host ones."""
+        if self.device.type != "cuda":
+            return torch.device("cpu")
+        import torch.distributed as dist
+        return self.device if dist.get_backend(self.pc.tp_group) == "nccl" else torch.device("cpu")
 
     def _forward_eager(self, decode, chunks, sample_idx, spec=None):
         header, flat = self._pack_step(decode, chunks, sample_idx)
-        if self.pc.tp_size > 1:
-            assert spec is None, "async steps are single-rank"
-            h = torch.from_numpy(header).to(self._comm_device())
-            self._bcast(h)
+        if self._chan is not None:
+            from ..parallel.channel import FWD_EAGER
+            self._chan.send(FWD_EAGER, [header, flat] + ([spec[0]] if spec is not None else []))
+        return self._run_eager(header, flat, spec)
+
+    def _run_eager(self, header, flat, spec):
+        """Upload a packed step (one pinned async copy) and run its forward
+        (rank 0, and every TP worker from the channel's message)."""
         if spec is not None:
             dev, src = self._to_dev([flat, spec[0]])
             spec = (src, spec[1])
         else:
             dev = self._to_dev([flat])[0]
-        if self.pc.tp_size > 1:
-            self._bcast(dev)
         return self._exec_step(header, flat, dev, spec)
 
     @staticmethod
@@ -994,32 +1029,37 @@ class LLMEngine:
         ids[:n] = torch.where(src >= 0, pick, ids[:n])
 
     def serve_worker(self) -> None:
-        """TP ranks > 0: replay every step rank 0 schedules until it sends STOP."""
+        """TP ranks > 0: execute every step rank 0 schedules, in rank 0's
+        order (sampling / forward messages from the host channel), until STOP.
+        The worker never waits for its own GPU: the next message is received
+        while the previous forward still runs."""
         assert self.pc.tp_rank > 0
-        cd = self._comm_device()
+        from ..parallel.channel import FWD_EAGER, FWD_GRAPH, SAMPLE, STOP
+        logits = None
+        if self.device.type == "cuda":
+            torch.cuda.set_device(self.device)
         while True:
-            h = torch.empty(self.HDR, dtype=torch.int64, device=cd)
-            self._bcast(h)
-            header = h.cpu().numpy()
-            if header[0] == 0:
+            kind, arrs = self._chan.recv()
+            if kind == STOP:
                 return
-            dev = torch.empty(int(header[1]), dtype=torch.int32, device=self.device)
-            self._bcast(dev)
-            host = dev.numpy() if self.device.type == "cpu" else None
-            logits = self._exec_step(header, host, dev)
-            if self._dist_sample and int(header[9]) > 0:  # rank 0 samples these rows: join it
-                sh = torch.empty(self.SHDR, dtype=torch.int64, device=cd)
-                self._bcast(sh)
-                shdr = sh.cpu().numpy()
-                n = int(shdr[0]) * 8 + int(shdr[1]) + int(shdr[2]) * int(shdr[3])
-                sdev = torch.empty(n, dtype=torch.int32, device=self.device)
-                self._bcast(sdev)
-                self._sample_shard(logits, shdr, sdev)
+            if kind == SAMPLE:
+                hdr, flat, rows_a = arrs
+                self._last_tok = self._sample_rows(logits, hdr, flat, rows_a)
+            elif kind == FWD_EAGER:
+                spec = (arrs[2], self._last_tok) if len(arrs) > 2 else None
+                logits = self._run_eager(arrs[0], arrs[1], spec)
+            elif kind == FWD_GRAPH:
+                meta, flat = arrs[0], arrs[1]
+                spec = (arrs[2], self._last_tok) if len(arrs) > 2 else None
+                logits = self._graph_run(int(meta[0]), int(meta[1]), int(meta[2]), int(meta[3]), int(meta[4]),
+                                         flat, spec)
+            else:
+                raise RuntimeError(f"unknown step message {kind}")
 
     def stop_workers(self) -> None:
-        if self.pc.tp_size > 1 and self.pc.tp_rank == 0:
-            h = torch.zeros(self.HDR, dtype=torch.int64, device=self._comm_device())
-            self._bcast(h)
+        if self._chan is not None and self.pc.tp_rank == 0:
+            from ..parallel.channel import STOP
+            self._chan.send(STOP, [])
 
     @staticmethod
     def _n_parts(max_ctx: int) -> int:
@@ -1089,13 +1129,13 @@ class LLMEngine:
         s.wait_stream(torch.cuda.current_stream(self.device))
         with torch.cuda.stream(s):
             for _ in range(2):
-                self.model.forward(inp, self.kv.k, self.kv.v)
+                self._model_fwd(inp)
         torch.cuda.current_stream(self.device).wait_stream(s)
         graph = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
         with torch.cuda.graph(graph, pool=self._graph_pool):
-            out = self.model.forward(inp, self.kv.k, self.kv.v)
+            out = self._model_fwd(inp)
         self._graphs[key] = (graph, out)
         self.stats["captures"] += 1
         self.stats["capture_s"] += time.perf_counter() - t0
@@ -1127,21 +1167,29 @@ class LLMEngine:
         items = A.build_decode_items(ctx, np.arange(Bb), part)
         n_items = items.shape[0]
         assert n_items <= self._max_items
+        flat = np.concatenate([ids, pos, slots, ctx, bt.reshape(-1), np.array([n_items, part], np.int32),
+                               items.reshape(-1).astype(np.int32)])
+        if self._chan is not None:
+            from ..parallel.channel import FWD_GRAPH
+            meta = np.array([B, Bb, part, n_items, mb], dtype=np.int32)
+            self._chan.send(FWD_GRAPH, [meta, flat] + ([spec[0]] if spec is not None else []))
+        return self._graph_run(B, Bb, part, n_items, mb, flat, spec)
+
+    def _graph_run(self, B: int, Bb: int, part: int, n_items: int, mb: int, flat: np.ndarray, spec=None):
+        """Upload a packed decode step into the static graph inputs (pinned
+        staging, one async copy) and replay bucket ``Bb``'s graph (rank 0, and
+        every TP worker from the channel's message).  ``spec`` = (src[B], tok):
+        row i's input id is ``tok[src[i]]`` where ``src[i] >= 0``."""
+        st = self._ensure_static()
+        assert mb == self.max_blocks_per_seq
         hi = st["host_i"] = st["host_i"] ^ 1
         if st["host_ev"][hi] is not None:
             st["host_ev"][hi].synchronize()  # its previous upload has long completed in practice
         host = st["host"][hi]
         hv = host.numpy()
-        o = 0
-        for arr in (ids, pos, slots, ctx):
-            hv[o:o + Bb] = arr
-            o += Bb
-        hv[o:o + Bb * mb] = bt.reshape(-1)
-        o += Bb * mb
-        hv[o] = n_items
-        hv[o + 1] = part
-        hv[o + 2:o + 2 + n_items * 4] = items.reshape(-1)
-        n = o + 2 + n_items * 4
+        n = flat.size
+        hv[:n] = flat
+        o = 4 * Bb + Bb * mb  # offset of (n_items, part)
         if spec is not None:
             hv[n:n + B] = spec[0]
             n_src = n
@@ -1207,10 +1255,8 @@ class LLMEngine:
             lists = [0]
         filt = bool((topk > 0).any() or (topp < 1.0).any())
         if self._dist_sample:
-            if rows is not None:
-                logits = logits.index_select(0, torch.tensor(rows, device=logits.device))
             tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
-                                  seeds, steps, temps, topk, topp)
+                                  seeds, steps, temps, topk, topp, rows)
         else:
             table = self._mask_table()
             arrays = [mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps, temps.view(np.int32)]

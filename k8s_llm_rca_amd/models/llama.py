@@ -161,7 +161,7 @@ class LlamaModel:
         residual = F.embedding(inp.input_ids.long(), self.embed)     # [T, H]
         if self._exec is None and LX.LlamaExecutor.eligible(self):
             self._exec = LX.LlamaExecutor(self)
-        if self._exec is not None and LX.LlamaExecutor.eligible(self):
+        if self._exec is not None and LX.LlamaExecutor.eligible(self) and self._exec.fits(T):
             # the dense layer stack in one native call (ops/layer_exec.py): same kernels, same order
             prev, residual = self._exec.run(inp, residual, k_cache, v_cache)
             y = torch.empty_like(residual)

@@ -42,6 +42,7 @@ class LlamaStep(ctypes.Structure):
         ("p_bt_stride", I), ("p_S", I), ("n_tiles", I), ("n_merge", I),
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
+        ("ar_id", I), ("ar_mode", I),
     ]
 
 
@@ -70,7 +71,9 @@ def set_enabled(on: bool) -> None:
 
 
 class LlamaExecutor:
-    """Bound to one dense, TP=1, bf16 :class:`..models.llama.LlamaModel`."""
+    """Bound to one dense bf16 :class:`..models.llama.LlamaModel`: TP = 1, or
+    TP > 1 with the xGMI all-reduce (steps whose [T, H] all-reduce fits its
+    buffer; larger prefill steps take the Python path's RCCL all-reduces)."""
 
     def __init__(self, model):
         _check_abi()
@@ -96,11 +99,24 @@ class LlamaExecutor:
         st.wgu = ctypes.addressof(self._tabs["w_gu"])
         st.wdown = ctypes.addressof(self._tabs["w_down"])
         st.cos_sin = model.cos_sin.data_ptr()
+        car = model.pc.custom_ar if model.pc.tp_size > 1 else None
+        self._car = car
+        st.ar_id = car.id if car is not None else -1
+        st.ar_mode = 1
 
     @staticmethod
     def eligible(model) -> bool:
-        return (_enabled and model.device.type == "cuda" and model.pc.tp_size == 1 and model.moe is None
+        return (_enabled and model.device.type == "cuda" and model.moe is None
+                and (model.pc.tp_size == 1 or model.pc.custom_ar is not None)
                 and model.dtype == torch.bfloat16 and model.D == A.HEAD_DIM and not _silu_fused_in_table(model))
+
+    def fits(self, T: int) -> bool:
+        """This step's all-reduces ([T, H] bf16) fit the xGMI buffer (always true at TP = 1)."""
+        car = self._car
+        if car is None:
+            return True
+        nb = T * self.m.cfg.hidden * 2
+        return nb <= car.max_bytes and (T * self.m.cfg.hidden) % 8 == 0
 
     def _bind_kv(self, k_cache: torch.Tensor, v_cache: torch.Tensor) -> None:
         key = (k_cache.data_ptr(), v_cache.data_ptr(), k_cache.shape[1])
@@ -129,6 +145,9 @@ class LlamaExecutor:
         act = torch.empty((T, m.inter), dtype=dt, device=dev)
         prev = torch.empty((T, H), dtype=dt, device=dev)
         st.T, st.nd = T, inp.n_decode
+        if self._car is not None:
+            from ..parallel.xgmi import ONE_SHOT_MAX
+            st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)

@@ -76,18 +76,21 @@ def _reference(name):
     return m.forward(inp, kf, vf)[:, : cfg.vocab_size]
 
 
-@pytest.mark.parametrize("name", ["tiny-llama", "tiny-mixtral"])
-def test_tp2_matches_tp1(name):
+@pytest.mark.parametrize("name,world", [("tiny-llama", 2), ("tiny-mixtral", 2), ("tiny-llama", 4), ("tiny-llama", 8),
+                                        ("tiny-llama-g8", 4), ("tiny-mixtral", 4)])
+def test_tp2_matches_tp1(name, world):
+    """Sharded forward (column / row / vocab parallel, kv heads replicated when
+    n_kv < tp) == the unsharded model at world 2 / 4 / 8."""
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         out = os.path.join(d, "logits.pt")
-        mp.spawn(_run_model, args=(2, port, name, out), nprocs=2, join=True)
+        mp.spawn(_run_model, args=(world, port, name, out), nprocs=world, join=True)
         got = torch.load(out, weights_only=True)
     ref = _reference(name)
     torch.testing.assert_close(got, ref, atol=2e-4, rtol=2e-4)
 
 
-def _run_engine(rank, world, port, out_path, temperature=0.0, grammar=False):
+def _run_engine(rank, world, port, out_path, temperature=0.0, grammar=False, name="tiny-llama", top_k=0, top_p=1.0):
     import torch.distributed as dist
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
     from k8s_llm_rca_amd.models.config import get_config
@@ -99,9 +102,9 @@ def _run_engine(rank, world, port, out_path, temperature=0.0, grammar=False):
         pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
     else:
         pc = None
-    cfg = EngineConfig(model="tiny-llama", device="cpu", dtype=torch.float32, num_blocks=32, block_size=32,
+    cfg = EngineConfig(model=name, device="cpu", dtype=torch.float32, num_blocks=32, block_size=32,
                        max_batch_tokens=64, temperature=temperature)
-    model = LlamaModel(get_config("tiny-llama"), "cpu", torch.float32, pc, seed=5, init_mode="full_slice")
+    model = LlamaModel(get_config(name), "cpu", torch.float32, pc, seed=5, init_mode="full_slice")
     eng = LLMEngine(cfg, pc, model=model)
     if rank > 0:
         eng.serve_worker()
@@ -117,33 +120,45 @@ def _run_engine(rank, world, port, out_path, temperature=0.0, grammar=False):
                 g = Grammar([Lit('{"k": '), Choice(['"alpha"', '"beta"', '"gamma"'], "c"), Lit(', "t": "'),
                              Free(6, name="t"), Lit('"}')])
             eng.submit(sid, toks, g, 12, temperature=temperature, seed=7,
-                       on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+                       on_done=lambda g, st, i=i: outs.__setitem__(i, g), top_k=top_k, top_p=top_p)
         eng.run_until_idle()
         eng.stop_workers()
+        outs["_msgs"] = eng._chan.sent if eng._chan is not None else 0
         torch.save(outs, out_path)
     if world > 1:
         dist.destroy_process_group()
 
 
-def test_tp2_engine_generation_matches_tp1():
+@pytest.mark.parametrize("world,name", [(2, "tiny-llama"), (4, "tiny-llama"), (8, "tiny-llama"),
+                                        (2, "tiny-llama-g8"), (4, "tiny-llama-g8")])
+def test_tp_engine_generation_matches_tp1(world, name):
+    """TP engine (host step channel, async overlapped steps, vocab-parallel
+    sampling) == the unsharded engine, token for token.  World 4 / 8 on
+    tiny-llama (2 kv heads) and tiny-llama-g8 (1 kv head) run with kv heads
+    replicated across ranks (n_kv < tp)."""
     with tempfile.TemporaryDirectory() as d:
-        o2, o1 = os.path.join(d, "tp2.pt"), os.path.join(d, "tp1.pt")
-        mp.spawn(_run_engine, args=(2, _free_port(), o2), nprocs=2, join=True)
-        _run_engine(0, 1, _free_port(), o1)
+        o2, o1 = os.path.join(d, "tpn.pt"), os.path.join(d, "tp1.pt")
+        mp.spawn(_run_engine, args=(world, _free_port(), o2, 0.0, False, name), nprocs=world, join=True)
+        _run_engine(0, 1, _free_port(), o1, 0.0, False, name)
         a = torch.load(o2, weights_only=True)
         b = torch.load(o1, weights_only=True)
+    assert a.pop("_msgs") > 0 and b.pop("_msgs") == 0
     assert a == b and all(len(v) == 12 for v in a.values())
 
 
-def test_tp2_distributed_sampling_with_grammar_matches_tp1():
-    """Vocab-parallel Gumbel-max sampling (masks keyed by global id) must pick
-    the same tokens as single-device sampling of the gathered logits."""
+@pytest.mark.parametrize("top_k,top_p", [(0, 1.0), (5, 1.0), (20, 0.8), (64, 0.95)])
+def test_tp2_distributed_sampling_with_grammar_matches_tp1(top_k, top_p):
+    """Vocab-parallel Gumbel-max sampling (masks keyed by global id; top-k /
+    top-p through the per-rank candidate lists, exact for k <= CAND_K) must pick the same tokens as
+    single-device sampling of the gathered logits."""
     with tempfile.TemporaryDirectory() as d:
         o2, o1 = os.path.join(d, "tp2.pt"), os.path.join(d, "tp1.pt")
-        mp.spawn(_run_engine, args=(2, _free_port(), o2, 0.9, True), nprocs=2, join=True)
-        _run_engine(0, 1, _free_port(), o1, 0.9, True)
+        mp.spawn(_run_engine, args=(2, _free_port(), o2, 0.9, True, "tiny-llama", top_k, top_p), nprocs=2,
+                 join=True)
+        _run_engine(0, 1, _free_port(), o1, 0.9, True, "tiny-llama", top_k, top_p)
         a = torch.load(o2, weights_only=True)
         b = torch.load(o1, weights_only=True)
+    a.pop("_msgs"), b.pop("_msgs")
     assert a == b and len(a) == 3
 
 

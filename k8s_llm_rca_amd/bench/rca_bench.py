@@ -102,9 +102,15 @@ def run(args) -> Optional[Dict[str, Any]]:
     need = (n_warm + n_steps + nh_steps) * quantum + 2 * conc
     n_inc = max(1, min(need, int(0.3 * args.graph_nodes / NODES_PER_INCIDENT)))
     cluster = generate_cluster(args.graph_nodes, n_inc, seed=args.seed + 7919 * rank)
-    if cuda and args.graph_device:
+    batchers = []
+    if cuda and not args.no_graph_device:
+        # both graphs resident in HBM; every pipeline's CONTAINS / STATE / var-length
+        # operator calls coalesced into one HIP launch per op (graph/batcher.py)
+        from ..graph.batcher import enable_batching
         from ..graph.device import to_device
-        to_device(cluster.stategraph, device)
+        for g in (cluster.stategraph, cluster.metagraph):
+            to_device(g, device)
+            batchers.append(enable_batching(g))
     pc = None
     tp_mode = args.tp > 1
     if tp_mode:
@@ -172,6 +178,8 @@ def run(args) -> Optional[Dict[str, Any]]:
     elapsed = time.perf_counter() - t0
     truncated = truncated or not done_all
     d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    gq = {k: 1e3 * v["total_s"] for k, v in tracing.snapshot().items()}
+    bstats = [dict(b.stats) for b in batchers]
     lat = stream.window(t0, t_end + 1e-9)
     err_timed = sum(1 for t, _, ok in list(stream.done) if not ok and t0 <= t <= t_end)
     # ---- optional no-hints window (disclosure): the same engine and stream with the
@@ -257,6 +265,11 @@ def run(args) -> Optional[Dict[str, Any]]:
         "wall_s": round(time.perf_counter() - t_start, 1),
         "clean_shutdown": clean,
         "stages": {k: round(v["mean_ms"], 2) for k, v in tracing.snapshot().items()},
+        "graph": {"device": bool(batchers),
+                  "query_ms_per_analysis": round(gq.get("graph.query", 0.0) / max(1, n_done), 2),
+                  "batched_requests": int(sum(b["requests"] for b in bstats)),
+                  "kernel_batches": int(sum(b["launches"] for b in bstats)),
+                  "max_batch": int(max([b["max_batch"] for b in bstats] or [0]))},
     }
     if world > 1 and not tp_mode:
         import torch.distributed as dist
@@ -282,7 +295,8 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--device", default="cuda")
     p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses (pipelines) per GPU")
     p.add_argument("--graph-nodes", type=int, default=10_000)
-    p.add_argument("--graph-device", action="store_true", help="mirror the stategraph to HBM (HIP graph kernels)")
+    p.add_argument("--no-graph-device", action="store_true",
+                   help="keep the graphs on the host (default on GPU: HBM mirror + batched HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
     p.add_argument("--max-batch-tokens", type=int, default=8192)
@@ -308,7 +322,7 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # "Llama-3-8B TP=1 bf16 on one MI355X, 1k-node synthetic k8s graph"
     "llama3-8b-1k": dict(model="llama3-8b", graph_nodes=1_000),
     # "Llama-3-8B TP=1, 100k-node synthetic graph (HIP CSR metapath BFS stress)"
-    "llama3-8b-100k": dict(model="llama3-8b", graph_nodes=100_000, graph_device=True),
+    "llama3-8b-100k": dict(model="llama3-8b", graph_nodes=100_000),
     # "Llama-3-70B TP=8 over xGMI, 10k-node graph, batched multi-incident RCA" (torchrun --nproc-per-node 8)
     "llama3-70b-tp8-10k": dict(model="llama3-70b", tp=8, graph_nodes=10_000),
     # "Mixtral 8x7B MoE backend (grouped GEMM + expert all-to-all over xGMI), 10k-node graph"

@@ -9,7 +9,8 @@
 //                   or interval overlap), STATE label filter, first `limit`
 //   walks           relationship-unique walks of 1..3 hops from every start
 //                   (Cypher -[*1..3]- semantics of find_metapath's queries), with
-//                   an end-label filter pushed down; count pass + fill pass
+//                   an end-label filter pushed down; wave per start, LDS
+//                   frontier, count pass + fill pass
 // Node / edge ids are int64 in the host store and int32 on the device.
 #include "common.h"
 
@@ -112,8 +113,25 @@ __global__ void __launch_bounds__(256) state_kernel(const int* __restrict__ indp
   counts[i] = c;
 }
 
-// Walk enumeration (thread per start).  dir: 0 out, 1 in, 2 both.
-// Each record: [row, hops, n0, n1, n2, n3, e0, e1, e2] (int32, -1 padded).
+// Walk enumeration, one wave per start with the frontier in LDS.
+// dir: 0 out, 1 in, 2 both.  Level h (h = 1, 2, 3) flattens every (walk of
+// h-1 hops) x (its adjacency entries) pair into one index space: the wave's 64
+// lanes take 64 consecutive pairs at a time (a prefix sum of the parents'
+// degrees in LDS + a binary search per lane), so a hub node's thousand edges
+// are spread over the lanes instead of serialising one thread, and divergence
+// is limited to the per-pair predicate.  Valid hop-h walks are compacted
+// (ballot + popcount: lane order preserved) into the LDS frontier of level h.
+// Every walk is emitted as a record
+//   [row, hops, n0, n1, n2, n3, e0, e1, e2, k1, k2, k3]   (int32, -1 padded)
+// where k_h is the walk's h-th step in the thread-per-start DFS enumeration
+// order (side-major adjacency position); the host sorts records by (row, k1,
+// k2, k3) to reproduce that order exactly.  Count pass (offsets == nullptr)
+// and fill pass enumerate identically.  A frontier larger than WK_CAP sets
+// counts[i] = -1: the host recomputes that start on its own path.
+constexpr int WK_CAP = 384;  // 4 waves x 2 levels x 7.7 KB of LDS per block: 2 blocks per CU
+constexpr int WK_WAVES = 4;
+constexpr int WK_REC = 12;
+
 struct WalkArgs {
   const int *oip, *onb, *oei, *iip, *inb, *iei, *esrc, *edst, *etype, *nlabel;
   const long long* starts;
@@ -125,64 +143,186 @@ struct WalkArgs {
   int* out;
 };
 
-__device__ __forceinline__ int deg_begin(const WalkArgs& a, int v, int side) { return side == 0 ? a.oip[v] : a.iip[v]; }
-__device__ __forceinline__ int deg_end(const WalkArgs& a, int v, int side) { return side == 0 ? a.oip[v + 1] : a.iip[v + 1]; }
+struct WkLevel {
+  int node[WK_CAP];
+  int edge[WK_CAP];
+  int parent[WK_CAP];
+  int k[WK_CAP];
+  int pre[WK_CAP + 1];  // exclusive prefix of the entries' adjacency sizes
+};
 
-__global__ void __launch_bounds__(256) walks_kernel(WalkArgs a) {
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= a.n) return;
+// lanes of one wave exchange frontier data through LDS: order the writes
+// before the other lanes' reads (compiler and lgkm counter)
+__device__ __forceinline__ void wk_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "workgroup");
+  __builtin_amdgcn_wave_barrier();
+}
+
+__device__ __forceinline__ int adj_size(const WalkArgs& a, int v) {
+  int d = 0;
+  if (a.dir != 1) d += a.oip[v + 1] - a.oip[v];
+  if (a.dir != 0) d += a.iip[v + 1] - a.iip[v];
+  return d;
+}
+
+// the j-th adjacency entry of v (out side first): edge id, neighbour, side
+__device__ __forceinline__ void adj_at(const WalkArgs& a, int v, int j, int* e, int* nb, int* side) {
+  const int dout = a.dir != 1 ? a.oip[v + 1] - a.oip[v] : 0;
+  if (j < dout) {
+    const int p = a.oip[v] + j;
+    *e = a.oei[p];
+    *nb = a.onb[p];
+    *side = 0;
+  } else {
+    const int p = a.iip[v] + (j - dout);
+    *e = a.iei[p];
+    *nb = a.inb[p];
+    *side = 1;
+  }
+}
+
+// wave-wide exclusive scan of the levels' adjacency sizes into L.pre
+__device__ __forceinline__ int wk_prefix(const WalkArgs& a, WkLevel& L, int n, int lane) {
+  int carry = 0;
+  for (int b = 0; b < n; b += 64) {
+    const int i = b + lane;
+    int v = i < n ? adj_size(a, L.node[i]) : 0;
+    int x = v;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(x, o, 64);
+      if (lane >= o) x += y;
+    }
+    if (i < n) L.pre[i] = carry + x - v;
+    carry += __shfl(x, 63, 64);
+  }
+  if (lane == 0) L.pre[n] = carry;
+  wk_sync();
+  return carry;
+}
+
+__device__ __forceinline__ int wk_find(const WkLevel& L, int n, int k) {  // last i with pre[i] <= k
+  int lo = 0, hi = n - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (L.pre[mid] <= k) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+__global__ void __launch_bounds__(64 * WK_WAVES) walks_kernel(WalkArgs a) {
+  __shared__ WkLevel lv[WK_WAVES][2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int i = blockIdx.x * WK_WAVES + wv;
+  if (i >= a.n) return;  // wave-uniform: no block barrier below
+  WkLevel& L1 = lv[wv][0];
+  WkLevel& L2 = lv[wv][1];
   const int s0 = (int)a.starts[i];
-  const int s_lo = (a.dir == 1) ? 1 : 0, s_hi = (a.dir == 0) ? 0 : 1;
   long long w = a.offsets ? a.offsets[i] : 0;
   int cnt = 0;
-  int nodes[4], edges[3];
-  nodes[0] = s0;
-  auto emit = [&](int hops) {
-    if (hops < a.min_h) return;
-    if (a.end_label >= 0 && a.nlabel[nodes[hops]] != a.end_label) return;
-    if (a.offsets) {
-      int* rec = a.out + w * 9;
+  bool overflow = false;
+  // emit the compacted valid lanes' walks of `hops` hops (lane order)
+  auto emit = [&](bool valid, int hops, int n1v, int n2v, int n3v, int e1, int e2, int e3, int k1, int k2, int k3) {
+    const int last = hops == 1 ? n1v : hops == 2 ? n2v : n3v;
+    const bool ok = valid && hops >= a.min_h && (a.end_label < 0 || a.nlabel[last] == a.end_label);
+    const unsigned long long m = __ballot(ok);
+    if (ok && a.offsets) {
+      const int pos = __popcll(m & ((1ull << lane) - 1ull));
+      int* rec = a.out + (w + pos) * WK_REC;
       rec[0] = i;
       rec[1] = hops;
-      for (int k = 0; k < 4; ++k) rec[2 + k] = k <= hops ? nodes[k] : -1;
-      for (int k = 0; k < 3; ++k) rec[6 + k] = k < hops ? edges[k] : -1;
-      ++w;
-    } else {
-      ++cnt;
+      rec[2] = s0;
+      rec[3] = n1v;
+      rec[4] = hops >= 2 ? n2v : -1;
+      rec[5] = hops >= 3 ? n3v : -1;
+      rec[6] = e1;
+      rec[7] = hops >= 2 ? e2 : -1;
+      rec[8] = hops >= 3 ? e3 : -1;
+      rec[9] = k1;
+      rec[10] = hops >= 2 ? k2 : -1;
+      rec[11] = hops >= 3 ? k3 : -1;
     }
+    w += __popcll(m);
+    cnt += __popcll(m);
   };
-  for (int sd1 = s_lo; sd1 <= s_hi; ++sd1)
-    for (int p1 = deg_begin(a, s0, sd1); p1 < deg_end(a, s0, sd1); ++p1) {
-      const int e1 = sd1 ? a.iei[p1] : a.oei[p1];
-      if (!type_ok(a.etype[e1], a.type_mask)) continue;
-      if (sd1 && a.dir == 2 && a.esrc[e1] == a.edst[e1]) continue;
-      const int n1 = sd1 ? a.inb[p1] : a.onb[p1];
-      edges[0] = e1;
-      nodes[1] = n1;
-      emit(1);
-      if (a.max_h < 2) continue;
-      for (int sd2 = s_lo; sd2 <= s_hi; ++sd2)
-        for (int p2 = deg_begin(a, n1, sd2); p2 < deg_end(a, n1, sd2); ++p2) {
-          const int e2 = sd2 ? a.iei[p2] : a.oei[p2];
-          if (e2 == e1 || !type_ok(a.etype[e2], a.type_mask)) continue;
-          if (sd2 && a.dir == 2 && a.esrc[e2] == a.edst[e2]) continue;
-          const int n2 = sd2 ? a.inb[p2] : a.onb[p2];
-          edges[1] = e2;
-          nodes[2] = n2;
-          emit(2);
-          if (a.max_h < 3) continue;
-          for (int sd3 = s_lo; sd3 <= s_hi; ++sd3)
-            for (int p3 = deg_begin(a, n2, sd3); p3 < deg_end(a, n2, sd3); ++p3) {
-              const int e3 = sd3 ? a.iei[p3] : a.oei[p3];
-              if (e3 == e1 || e3 == e2 || !type_ok(a.etype[e3], a.type_mask)) continue;
-              if (sd3 && a.dir == 2 && a.esrc[e3] == a.edst[e3]) continue;
-              edges[2] = e3;
-              nodes[3] = sd3 ? a.inb[p3] : a.onb[p3];
-              emit(3);
-            }
-        }
+  // ---- hop 1: the start's adjacency
+  const int d0 = adj_size(a, s0);
+  int n1 = 0;
+  for (int b = 0; b < d0; b += 64) {
+    const int j = b + lane;
+    bool valid = false;
+    int e = -1, nb = -1, side = 0;
+    if (j < d0) {
+      adj_at(a, s0, j, &e, &nb, &side);
+      valid = type_ok(a.etype[e], a.type_mask) && !(side && a.dir == 2 && a.esrc[e] == a.edst[e]);
     }
-  if (!a.offsets) a.counts[i] = cnt;
+    emit(valid, 1, nb, -1, -1, e, -1, -1, j, -1, -1);
+    const unsigned long long m = __ballot(valid && a.max_h >= 2);
+    if (valid && a.max_h >= 2) {
+      const int pos = n1 + __popcll(m & ((1ull << lane) - 1ull));
+      if (pos < WK_CAP) {
+        L1.node[pos] = nb;
+        L1.edge[pos] = e;
+        L1.parent[pos] = -1;
+        L1.k[pos] = j;
+      }
+    }
+    n1 += __popcll(m);
+  }
+  if (n1 > WK_CAP) overflow = true;
+  // ---- hop 2
+  int n2 = 0;
+  if (!overflow && a.max_h >= 2 && n1 > 0) {
+    wk_sync();
+    const int t2 = wk_prefix(a, L1, n1, lane);
+    for (int b = 0; b < t2; b += 64) {
+      const int q = b + lane;
+      bool valid = false;
+      int e = -1, nb = -1, side = 0, pi = 0, jj = 0;
+      if (q < t2) {
+        pi = wk_find(L1, n1, q);
+        jj = q - L1.pre[pi];
+        adj_at(a, L1.node[pi], jj, &e, &nb, &side);
+        valid = e != L1.edge[pi] && type_ok(a.etype[e], a.type_mask) &&
+                !(side && a.dir == 2 && a.esrc[e] == a.edst[e]);
+      }
+      emit(valid, 2, q < t2 ? L1.node[pi] : -1, nb, -1, q < t2 ? L1.edge[pi] : -1, e, -1, q < t2 ? L1.k[pi] : -1,
+           jj, -1);
+      const unsigned long long m = __ballot(valid && a.max_h >= 3);
+      if (valid && a.max_h >= 3) {
+        const int pos = n2 + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < WK_CAP) {
+          L2.node[pos] = nb;
+          L2.edge[pos] = e;
+          L2.parent[pos] = pi;
+          L2.k[pos] = jj;
+        }
+      }
+      n2 += __popcll(m);
+    }
+    if (n2 > WK_CAP) overflow = true;
+  }
+  // ---- hop 3 (emitted, not stored)
+  if (!overflow && a.max_h >= 3 && n2 > 0) {
+    wk_sync();
+    const int t3 = wk_prefix(a, L2, n2, lane);
+    for (int b = 0; b < t3; b += 64) {
+      const int q = b + lane;
+      bool valid = false;
+      int e = -1, nb = -1, side = 0, pi = 0, jj = 0, gp = 0;
+      if (q < t3) {
+        pi = wk_find(L2, n2, q);
+        jj = q - L2.pre[pi];
+        gp = L2.parent[pi];
+        adj_at(a, L2.node[pi], jj, &e, &nb, &side);
+        valid = e != L2.edge[pi] && e != L1.edge[gp] && type_ok(a.etype[e], a.type_mask) &&
+                !(side && a.dir == 2 && a.esrc[e] == a.edst[e]);
+      }
+      emit(valid, 3, q < t3 ? L1.node[gp] : -1, q < t3 ? L2.node[pi] : -1, nb, q < t3 ? L1.edge[gp] : -1,
+           q < t3 ? L2.edge[pi] : -1, e, q < t3 ? L1.k[gp] : -1, q < t3 ? L2.k[pi] : -1, jj);
+    }
+  }
+  if (!a.offsets && lane == 0) a.counts[i] = overflow ? -1 : cnt;
 }
 
 }  // namespace k8s
@@ -229,6 +369,6 @@ K8S_API int k8s_walks(const int* oip, const int* onb, const int* oei, const int*
   if (max_h > 3 || min_h < 1) return (int)hipErrorInvalidValue;
   WalkArgs a{oip, onb, oei, iip, inb, iei, esrc, edst, etype, nlabel, starts, n, min_h, max_h, dir,
              (unsigned)type_mask_i, end_label, counts, offsets, out};
-  hipLaunchKernelGGL(walks_kernel, dim3((n + 255) / 256), dim3(256), 0, s, a);
+  hipLaunchKernelGGL(walks_kernel, dim3((n + WK_WAVES - 1) / WK_WAVES), dim3(64 * WK_WAVES), 0, s, a);
   return (int)hipGetLastError();
 }

@@ -102,6 +102,9 @@ class Executor:
 
     # ----------------------------------------------------------------- MATCH
     def _match(self, table: Table, m: A.Match, params, ci: int) -> Table:
+        fast = self._state_pattern(table, m, params)
+        if fast is not None:
+            return fast
         conjuncts = _split_and(m.where) if m.where is not None else []
         pushed = [False] * len(conjuncts)
         in_rows = table.n
@@ -171,6 +174,71 @@ class Executor:
             del table.cols[" optrow"]
             del table.types[" optrow"]
         return table
+
+    # temporal STATE lookup (G6) ------------------------------------------
+    STATE_LIMIT = 64
+
+    def _state_pattern(self, table: Table, m: A.Match, params) -> Optional[Table]:
+        """The check_state queries (``analyze_root_cause.py:51-79``)::
+
+            MATCH (n1:Kind)-[r1:HasState]->(n2:KIND)
+            WHERE n1.id = 'uid' AND r1.tmin <= 'ts_a' AND r1.tmax > 'ts_b'
+
+        run as one temporal-interval operator (``PropertyGraph.state_lookup``:
+        the HIP ``state_kernel`` on a mirrored graph, batched across the
+        concurrent pipelines) instead of a generic expand + filter.  The
+        timestamp literals must be the fixed-width format the store parses:
+        then int64-ms comparison == Cypher's lexicographic string comparison.
+        Anything else returns None (generic path)."""
+        if table.n != 1 or table.cols or m.optional or m.where is None or len(m.patterns) != 1:
+            return None
+        pat = m.patterns[0]
+        if pat.var or len(pat.nodes) != 2 or len(pat.rels) != 1:
+            return None
+        a, b, r = pat.nodes[0], pat.nodes[1], pat.rels[0]
+        if (r.types != ["HasState"] or r.direction != "out" or r.var_length or r.props or a.props or b.props
+                or len(a.labels) != 1 or len(b.labels) > 1 or not (a.var and b.var and r.var)
+                or len({a.var, b.var, r.var}) != 3):
+            return None
+        want = {}
+        for c in _split_and(m.where):
+            if not (isinstance(c, A.BinOp) and isinstance(c.left, A.Prop) and isinstance(c.left.target, A.Var)
+                    and _is_const(c.right)):
+                return None
+            try:
+                val = evaluate(c.right, Env(None, params))
+            except CypherError:
+                return None
+            key = (c.left.target.name, c.left.key, c.op)
+            if key in want or not isinstance(val, str):
+                return None
+            want[key] = val
+        uid = want.pop((a.var, "id", "="), None)
+        t_lo = want.pop((r.var, "tmin", "<="), None)
+        t_hi = want.pop((r.var, "tmax", ">"), None)
+        if want or uid is None or t_lo is None or t_hi is None:
+            return None
+        from ..store import ts_to_ms
+        try:
+            q_lo, q_hi = ts_to_ms(t_lo), ts_to_ms(t_hi)
+        except (ValueError, TypeError):
+            return None
+        ents = self.g.index_lookup(a.labels[0], "id", uid)
+        n1s, es = [], []
+        if len(ents):
+            res = self.g.state_lookup(ents, np.full(len(ents), q_hi, dtype=np.int64), b.labels[0] if b.labels else None,
+                                      "loose", np.full(len(ents), q_lo, dtype=np.int64), self.STATE_LIMIT)
+            for n, e in zip(ents.tolist(), res):
+                if len(e) >= self.STATE_LIMIT:
+                    return None  # more valid STATEs than the operator returns: generic path
+                n1s += [n] * len(e)
+                es += list(e)
+        t = Table(len(es))
+        e_arr = np.asarray(es, dtype=np.int64)
+        t.add(a.var, np.asarray(n1s, dtype=np.int64), NODE)
+        t.add(r.var, e_arr, REL)
+        t.add(b.var, self.g.e_dst[e_arr] if len(e_arr) else np.zeros(0, dtype=np.int64), NODE)
+        return t
 
     def _pushdown(self, var: str, conjuncts, pushed, params) -> List[Tuple[str, str, Any]]:
         """Collect single-variable filters ``(op, key, value)`` for ``var``."""

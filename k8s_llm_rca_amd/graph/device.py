@@ -9,6 +9,12 @@ host where a kernel launch + sync would cost more than the work:
 * ``expand``      -> ``k8s_graph_expand2`` (count, device scan, fill)
 * ``state_lookup``-> ``k8s_state_lookup``
 * ``var_length``  -> ``k8s_walks`` (1..3 hops, relationship-unique, end-label pushdown)
+
+Every op runs on the mirror's own HIP stream (non-blocking w.r.t. the LLM
+engine's stream, so a graph query never queues behind a forward) and returns
+its results through pinned host buffers with an async copy + event wait that
+waits for this stream only.  :class:`..batcher.GraphBatcher` coalesces the
+concurrent pipelines' calls into one launch per op.
 """
 from __future__ import annotations
 
@@ -41,9 +47,35 @@ class DeviceGraph:
         self.tmin, self.tmax = up64(g.e_tmin), up64(g.e_tmax)
         self.nlabel = up32(g.node_label)
         self._heaps = {}
+        self.stream = torch.cuda.Stream(self.device) if self.device.type == "cuda" else None
+        self.batcher = None  # graph/batcher.py, attached by enable_batching()
+        self.launches = 0
         self.bytes = sum(t.numel() * t.element_size() for t in (
             self.oip, self.onb, self.oei, self.iip, self.inb, self.iei, self.esrc, self.edst, self.etype,
             self.ekey, self.tmin, self.tmax, self.nlabel))
+
+    def _ctx(self):
+        import contextlib
+        return torch.cuda.stream(self.stream) if self.stream is not None else contextlib.nullcontext()
+
+    def _up(self, a, dtype) -> torch.Tensor:
+        """Pinned host staging + async upload on the graph stream."""
+        t = torch.from_numpy(np.ascontiguousarray(a, dtype=dtype))
+        if self.device.type == "cuda":
+            t = t.pin_memory()
+        return t.to(self.device, non_blocking=True)
+
+    def _fetch(self, *ts: torch.Tensor):
+        """Device -> pinned host copies of ``ts``; waits for THIS stream only."""
+        if self.device.type != "cuda":
+            return [t.numpy() for t in ts]
+        hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ts]
+        for h, t in zip(hs, ts):
+            h.copy_(t, non_blocking=True)
+        ev = torch.cuda.Event()
+        ev.record(self.stream)
+        ev.synchronize()
+        return [h.numpy() for h in hs]
 
     def _heap(self, key: str):
         h = self._heaps.get(key)
@@ -69,19 +101,22 @@ class DeviceGraph:
 
     # ------------------------------------------------------------ CONTAINS
     def contains_many(self, ids: np.ndarray, key: str, needles: List[str]) -> np.ndarray:
-        """[len(needles), len(ids)] bool: node[key] CONTAINS needle."""
+        """[len(needles), len(ids)] bool: node[key] CONTAINS needle (one launch)."""
         offs, heap = self._heap(key)
         enc = [n.encode("utf-8") for n in needles]
         noff = np.zeros(len(enc) + 1, dtype=np.int32)
         np.cumsum([len(e) for e in enc], out=noff[1:])
         nbuf = np.frombuffer(b"".join(enc) or b"\0", dtype=np.uint8).copy()
-        d_ids = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int64)).to(self.device)
-        d_nd = torch.from_numpy(nbuf).to(self.device)
-        d_noff = torch.from_numpy(noff).to(self.device)
-        out = torch.empty(len(needles) * len(ids), dtype=torch.uint8, device=self.device)
-        check(lib().k8s_substr_search(ptr(offs), ptr(heap), ptr(d_ids), len(ids), ptr(d_nd), len(needles),
-                                      ptr(d_noff), ptr(out), stream_ptr(d_ids)), "substr_search")
-        return out.view(len(needles), len(ids)).cpu().numpy().astype(bool)
+        with self._ctx():
+            d_ids = self._up(ids, np.int64)
+            d_nd = self._up(nbuf, np.uint8)
+            d_noff = self._up(noff, np.int32)
+            out = torch.empty(len(needles) * len(ids), dtype=torch.uint8, device=self.device)
+            check(lib().k8s_substr_search(ptr(offs), ptr(heap), ptr(d_ids), len(ids), ptr(d_nd), len(needles),
+                                          ptr(d_noff), ptr(out), stream_ptr(d_ids)), "substr_search")
+            self.launches += 1
+            (o,) = self._fetch(out)
+        return o.reshape(len(needles), len(ids)).astype(bool)
 
     def contains(self, ids: np.ndarray, key: str, needle: str) -> np.ndarray:
         return self.contains_many(ids, key, [needle])[0]
@@ -117,43 +152,72 @@ class DeviceGraph:
     # -------------------------------------------------------- STATE lookup
     def state_lookup(self, entity_ids, ts_ms, state_label, mode, tmax_ms, limit):
         n = len(entity_ids)
-        d_e = torch.from_numpy(np.ascontiguousarray(entity_ids, dtype=np.int64)).to(self.device)
-        d_t = torch.from_numpy(np.ascontiguousarray(ts_ms, dtype=np.int64)).to(self.device)
-        d_q = torch.from_numpy(np.ascontiguousarray(tmax_ms if tmax_ms is not None else ts_ms,
-                                                    dtype=np.int64)).to(self.device)
-        out = torch.full((n * limit,), -1, dtype=torch.int64, device=self.device)
-        counts = torch.empty(n, dtype=torch.int32, device=self.device)
         lid = -1 if state_label is None else self.g.labels.lookup(state_label)
-        check(lib().k8s_state_lookup(ptr(self.oip), ptr(self.onb), ptr(self.oei), ptr(self.etype), ptr(self.nlabel),
-                                     ptr(self.tmin), ptr(self.tmax), self.g.rel_types.lookup("HasState"), lid,
-                                     1 if mode != "strict" else 0, limit, ptr(d_e), ptr(d_t), ptr(d_q), n, ptr(out),
-                                     ptr(counts), stream_ptr(d_e)), "state_lookup")
-        o = out.view(n, limit).cpu().numpy()
-        c = counts.cpu().numpy()
+        if state_label is not None and lid < 0:
+            return [np.zeros(0, dtype=np.int64) for _ in range(n)]
+        with self._ctx():
+            d_e = self._up(entity_ids, np.int64)
+            d_t = self._up(ts_ms, np.int64)
+            d_q = self._up(tmax_ms if tmax_ms is not None else ts_ms, np.int64)
+            out = torch.full((n * limit,), -1, dtype=torch.int64, device=self.device)
+            counts = torch.empty(n, dtype=torch.int32, device=self.device)
+            check(lib().k8s_state_lookup(ptr(self.oip), ptr(self.onb), ptr(self.oei), ptr(self.etype),
+                                         ptr(self.nlabel), ptr(self.tmin), ptr(self.tmax),
+                                         self.g.rel_types.lookup("HasState"), lid, 1 if mode != "strict" else 0,
+                                         limit, ptr(d_e), ptr(d_t), ptr(d_q), n, ptr(out), ptr(counts),
+                                         stream_ptr(d_e)), "state_lookup")
+            self.launches += 1
+            o, c = self._fetch(out, counts)
+        o = o.reshape(n, limit)
         return [o[i, :c[i]] for i in range(n)]
 
     # ------------------------------------------------------------- walks
     def walks(self, starts: np.ndarray, min_h: int, max_h: int, direction: str,
               rel_types=None, end_label: Optional[str] = None) -> np.ndarray:
-        """Records [W, 9] int32: row, hops, n0..n3, e0..e2 (-1 padded)."""
+        """Records [W, 9] int32: row, hops, n0..n3, e0..e2 (-1 padded), in the
+        host enumeration's order.  Starts whose frontier overflows the
+        kernel's LDS (hubs) are enumerated on the host instead."""
         n = len(starts)
-        d_s = torch.from_numpy(np.ascontiguousarray(starts, dtype=np.int64)).to(self.device)
-        counts = torch.empty(n, dtype=torch.int32, device=self.device)
         dcode = {"out": 0, "in": 1, "both": 2}[direction]
         el = -1 if end_label is None else self.g.labels.lookup(end_label)
         if end_label is not None and el < 0:
             return np.zeros((0, 9), dtype=np.int32)
         tm = self._type_mask(rel_types)
-        args = [ptr(self.oip), ptr(self.onb), ptr(self.oei), ptr(self.iip), ptr(self.inb), ptr(self.iei),
-                ptr(self.esrc), ptr(self.edst), ptr(self.etype), ptr(self.nlabel), ptr(d_s), n, min_h, max_h, dcode,
-                tm, el]
-        check(lib().k8s_walks(*args, ptr(counts), 0, 0, stream_ptr(d_s)), "walks")
-        offsets = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
-        torch.cumsum(counts, 0, out=offsets[1:])
-        total = int(offsets[-1].item())
-        out = torch.empty(max(total, 1) * 9, dtype=torch.int32, device=self.device)
-        check(lib().k8s_walks(*args, ptr(counts), ptr(offsets), ptr(out), stream_ptr(d_s)), "walks")
-        return out[: total * 9].view(total, 9).cpu().numpy()
+        with self._ctx():
+            d_s = self._up(starts, np.int64)
+            counts = torch.empty(n, dtype=torch.int32, device=self.device)
+            args = [ptr(self.oip), ptr(self.onb), ptr(self.oei), ptr(self.iip), ptr(self.inb), ptr(self.iei),
+                    ptr(self.esrc), ptr(self.edst), ptr(self.etype), ptr(self.nlabel), ptr(d_s), n, min_h, max_h,
+                    dcode, tm, el]
+            check(lib().k8s_walks(*args, ptr(counts), 0, 0, stream_ptr(d_s)), "walks")
+            offsets = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+            torch.cumsum(counts.clamp(min=0), 0, out=offsets[1:])
+            (tot, c_host) = self._fetch(offsets[-1:], counts)
+            total = int(tot[0])
+            out = torch.empty(max(total, 1) * 12, dtype=torch.int32, device=self.device)
+            check(lib().k8s_walks(*args, ptr(counts), ptr(offsets), ptr(out), stream_ptr(d_s)), "walks")
+            self.launches += 2
+            (rec,) = self._fetch(out[: total * 12])
+        rec = rec.reshape(total, 12)
+        over = np.nonzero(c_host < 0)[0]
+        if len(over):  # hubs: the host path, merged back in enumeration order
+            extra = []
+            tids = None
+            if rel_types:
+                tids = np.asarray([self.g.rel_types.lookup(t) for t in rel_types], dtype=np.int32)
+            from . import native as _native
+            for j in over.tolist():
+                for _, nodes, edges in _native.var_length(self.g, np.asarray([starts[j]]), min_h, max_h, direction,
+                                                           tids):
+                    if el >= 0 and self.g.node_label[nodes[-1]] != el:
+                        continue
+                    h = len(edges)
+                    r = [j, h] + list(nodes) + [-1] * (4 - len(nodes)) + list(edges) + [-1] * (3 - h)
+                    extra.append(r + [len(extra), -1, -1])  # k: host order within the start
+            if extra:
+                rec = np.concatenate([rec, np.asarray(extra, dtype=np.int32)])
+        order = np.lexsort((rec[:, 11], rec[:, 10], rec[:, 9], rec[:, 0]))
+        return np.ascontiguousarray(rec[order, :9])
 
 
 def to_device(g, device, min_gpu_rows: int = 2048) -> DeviceGraph:

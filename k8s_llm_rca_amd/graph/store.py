@@ -261,6 +261,8 @@ class PropertyGraph:
         """
         if len(ids) == 0:
             return np.zeros(0, dtype=bool)
+        if self.device is not None and self.device.batcher is not None:  # coalesced with the other pipelines'
+            return self.device.batcher.contains(np.asarray(ids), key, needle)
         if self.device is not None and len(ids) >= self.device.min_gpu_rows:
             return self.device.contains(ids, key, needle)
         offs, buf = self.string_heap(key)
@@ -317,9 +319,13 @@ class PropertyGraph:
         var-length semantics: a relationship appears at most once per path).
         ``end_label`` keeps only walks ending on that label (planner pushdown).
         """
-        if (self.device is not None and len(starts) >= self.device.min_gpu_rows and 1 <= min_hops
-                and max_hops <= 3):
-            rec = self.device.walks(np.asarray(starts), min_hops, max_hops, direction, rel_types, end_label)
+        dev = self.device
+        if (dev is not None and (dev.batcher is not None or len(starts) >= dev.min_gpu_rows) and 1 <= min_hops
+                and max_hops <= 3 and len(starts)):
+            if dev.batcher is not None:
+                rec = dev.batcher.walks(np.asarray(starts), min_hops, max_hops, direction, rel_types, end_label)
+            else:
+                rec = dev.walks(np.asarray(starts), min_hops, max_hops, direction, rel_types, end_label)
             out = []
             for r in rec.tolist():
                 h = r[1]
@@ -343,6 +349,8 @@ class PropertyGraph:
         loose: ``tmin <= tmax_q and tmax > ts`` (interval overlap, ``:51-60``).
         Returns, per entity, the edge ids (first ``limit`` in CSR order).
         """
+        if self.device is not None and self.device.batcher is not None and len(entity_ids):
+            return self.device.batcher.state_lookup(entity_ids, ts_ms, state_label, mode, tmax_ms, limit)
         if self.device is not None and len(entity_ids) >= self.device.min_gpu_rows:
             return self.device.state_lookup(entity_ids, ts_ms, state_label, mode, tmax_ms, limit)
         tid = self.rel_types.lookup("HasState")

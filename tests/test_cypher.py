@@ -171,3 +171,34 @@ def test_native_var_length_matches_numpy():
         finally:
             native._core = core
         assert a == b, d
+
+
+def test_state_pattern_operator_matches_generic_path(monkeypatch):
+    """The check_state temporal queries run as one STATE-lookup operator (G6,
+    the HIP state_kernel on a mirrored graph); results equal the generic
+    expand + filter path, strict and loose, present and missing STATEs."""
+    from k8s_llm_rca_amd.graph.cypher import Executor
+    from k8s_llm_rca_amd.graph.cypher import executor as EX
+    from k8s_llm_rca_amd.graph.synth import generate_cluster
+    from k8s_llm_rca_amd.pipeline.check_state import find_loose_states, find_strict_states
+    c = generate_cluster(1500, 40, seed=8)
+    g = c.stategraph
+    calls = []
+    orig = EX.Executor._state_pattern
+
+    def spy(self, *a):
+        out = orig(self, *a)
+        calls.append(out is not None)
+        return out
+
+    queries = []
+    for inc in c.incidents:
+        for kind, uid in ((inc.src_kind, inc.involved_id), (inc.dest_kind, inc.root_id)):
+            queries.append(find_strict_states(kind, uid, inc.timestamp))
+            queries.append(find_loose_states(kind, uid, "2020-12-10 00:00:00.000", inc.timestamp))
+    monkeypatch.setattr(EX.Executor, "_state_pattern", spy)
+    fast = [[r["n2"].id for r in Executor(g).run(q)] for q in queries]
+    assert all(calls) and any(fast) and not all(fast)
+    monkeypatch.setattr(EX.Executor, "_state_pattern", lambda self, *a: None)
+    slow = [[r["n2"].id for r in Executor(g).run(q)] for q in queries]
+    assert fast == slow

@@ -5,7 +5,7 @@
 // mesh every GPU can instead READ all its peers directly (7 links at once).
 // Each rank owns one IPC-exported, uncached buffer:
 //
-//   [FLAGS_A 8x256 u32][FLAGS_B 8x256 u32][EPOCH 256 u32][STATUS][DATA 2 x max][RES 2 x max]
+//   [FLAGS_A 8x256 u32][FLAGS_B 8x256 u32][EPOCH 256 u32][STATUS][DATA 2 x max][RES 2 x max][A2A 2 x 2max]
 //
 // and every rank maps every peer's buffer (hipIpcOpenMemHandle).  Work is
 // split into per-block slices; block b of every rank only ever synchronises
@@ -152,11 +152,78 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
   }
 }
 
+// Fixed-size all-to-all (EP token dispatch / combine, B15) over the same IPC
+// buffers and the same per-call epoch as the all-reduce (calls of both kinds
+// share one epoch sequence, issued in the same order on every rank).  Send
+// buffer [world][chunk] bf16 (chunk elements per destination); push model:
+// rank r writes its chunk for d straight into d's buffer, region [r], over
+// xGMI, signals d, and d copies its regions out once every peer signalled.
+// Block b owns the same element range of every chunk on every rank, so a
+// block waits only for the peers' block b.  A region of the parity-(e & 1)
+// half is rewritten only after every peer signalled epoch e - 1, i.e. after
+// its call e - 2 -- the region's last reader -- completed.
+__global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restrict__ send, uint16_t* __restrict__ recv,
+                                                        long chunk, long slice, int world, int rank, ARPeers P,
+                                                        long max_bytes, uint64_t timeout_ticks) {
+  const int b = blockIdx.x, t = threadIdx.x;
+  unsigned char* own = P.base[rank];
+  uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
+  uint32_t* arrivals = ep + 1;
+  __shared__ uint32_t s_e;
+  if (t == 0) s_e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t e = s_e;
+  // its own region after the all-reduce's DATA / RES: no byte shared between the kinds
+  const size_t half = AR_DATA + 4 * (size_t)max_bytes + (size_t)(e & 1u) * 2 * (size_t)max_bytes;
+  const long i0 = (long)b * slice, i1 = min(chunk, i0 + slice);
+  for (int d = 0; d < world; ++d) {
+    unsigned char* dst = P.base[d] + half + 2 * ((size_t)rank * chunk);
+    const uint16_t* src = send + (size_t)d * chunk;
+    for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
+      *reinterpret_cast<u16x8*>(dst + 2 * i) = *reinterpret_cast<const u16x8*>(src + i);
+  }
+  __threadfence_system();
+  __syncthreads();
+  ar_signal(P, AR_FLAGS_A, world, rank, b, e);
+  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks);
+  for (int r = 0; r < world; ++r) {
+    const unsigned char* srcb = own + half + 2 * ((size_t)r * chunk);
+    uint16_t* dst = recv + (size_t)r * chunk;
+    for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
+      *reinterpret_cast<u16x8*>(dst + i) = *reinterpret_cast<const u16x8*>(srcb + 2 * i);
+  }
+  __syncthreads();
+  if (t == 0) {
+    const uint32_t d = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+      __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ep, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 }  // namespace k8s
 
 using namespace k8s;
 
-K8S_API long k8s_ar_buffer_bytes(long max_bytes) { return (long)AR_DATA + 4 * max_bytes; }
+// Equal-split all-to-all of bf16: send [world][chunk] -> recv [world][chunk]
+// (recv[r] = rank r's send[this rank]); chunk % 8 == 0, world * chunk * 2 <= 2 * max_bytes.
+K8S_API int k8s_ar_alltoall_bf16(int id, const void* send, void* recv, long chunk, hipStream_t s) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  const ARCtx& c = g_ctx[id];
+  if (chunk <= 0) return 0;
+  if (chunk % 8 || 2 * chunk * c.world > 2 * c.max_bytes || send == recv) return (int)hipErrorInvalidValue;
+  long nb = (chunk + 4095) / 4096;
+  if (nb > AR_MAX_BLOCKS) nb = AR_MAX_BLOCKS;
+  long slice = (chunk + nb - 1) / nb;
+  slice = (slice + 7) / 8 * 8;
+  nb = (chunk + slice - 1) / slice;
+  hipLaunchKernelGGL(a2a_kernel, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)send, (uint16_t*)recv,
+                     chunk, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+  return (int)hipGetLastError();
+}
+
+K8S_API long k8s_ar_buffer_bytes(long max_bytes) { return (long)AR_DATA + 8 * max_bytes; }
 
 K8S_API int k8s_ar_alloc(long bytes, void** out) {
   hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached);

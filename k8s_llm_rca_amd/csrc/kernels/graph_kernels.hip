@@ -215,6 +215,7 @@ __global__ void __launch_bounds__(64 * WK_WAVES) walks_kernel(WalkArgs a) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int i = blockIdx.x * WK_WAVES + wv;
   if (i >= a.n) return;  // wave-uniform: no block barrier below
+  if (a.offsets && a.counts[i] < 0) return;  // overflowed in the count pass: the host enumerates this start
   WkLevel& L1 = lv[wv][0];
   WkLevel& L2 = lv[wv][1];
   const int s0 = (int)a.starts[i];

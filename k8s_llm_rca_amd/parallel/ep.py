@@ -16,6 +16,18 @@ rows, and for those:
 
 Over xGMI each all-to-all moves ``T/ep * k * H * 2`` bytes split across the 7
 peer links (RCCL), twice per layer.
+
+Decode-sized batches (``T <= FIXED_MAX_T``) take :func:`ep_moe_forward_fixed`
+instead: fixed-capacity dispatch buffers (every destination gets room for all
+of the rank's ``per * k`` slots), so every collective has a static size known
+on the host -- no counts exchange, no ``.tolist()`` host sync -- and, on the
+xGMI communicator (``XgmiAllReduce.all_to_all``, device-side epochs), the
+whole MoE layer is HIP-graph capturable.  The expert id rides in an extra
+column of the token row (exact in bf16 for ids <= 256); unused capacity rows
+carry the null expert ``E_local``, which the grouped GEMM never computes.
+The price is padding: ``ep * per * k`` rows move per rank instead of
+``per * k`` -- at decode sizes the all-to-all is latency-bound, not
+bandwidth-bound (prefill keeps the exact variable-size path).
 """
 from __future__ import annotations
 
@@ -25,7 +37,68 @@ import torch.distributed as dist
 from ..ops import moe as M
 
 
+FIXED_MAX_T = 256
+
+
+def _a2a(pc, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+    """Equal-split all-to-all over the EP group: ``send`` / ``recv`` [ep, ...]."""
+    car = pc.custom_ar
+    if (car is not None and send.is_cuda and send.dtype == torch.bfloat16 and pc.ep_group is pc.tp_group
+            and car.a2a_fits(send.numel() * 2)):
+        return car.all_to_all(send, recv)
+    dist.all_to_all_single(recv, send, group=pc.ep_group)
+    return recv
+
+
+def ep_moe_forward_fixed(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor) -> torch.Tensor:
+    """EP MoE layer with static-size collectives (see the module docstring)."""
+    pc = moe.pc
+    ep, r = pc.ep_size, pc.ep_rank
+    T, H = y.shape
+    k, El = moe.k, moe.E_local
+    per = (T + ep - 1) // ep
+    lo, hi = min(T, r * per), min(T, (r + 1) * per)
+    n_own = hi - lo
+    C = per * k                                                      # capacity per destination
+    W = H + 8                                                        # row + expert-id column (16-B aligned)
+    dev = y.device
+    slots = torch.arange(n_own * k, device=dev)
+    ids = topk_ids[lo:hi].reshape(-1).long()                         # [n_own*k] global expert ids
+    dest = ids // El
+    _, inv, offs = M.align(dest.to(torch.int32).view(-1, 1), ep)     # stable counting sort by destination
+    pos = inv.long() - offs.long().index_select(0, dest)             # rank of the slot in its bucket
+    flat = dest * C + pos                                            # its row in the [ep*C] send buffer
+    send = torch.zeros(ep * C, W, dtype=y.dtype, device=dev)
+    send[:, H] = float(El)                                           # null expert on unused rows
+    if n_own:
+        send[:, :H].index_copy_(0, flat, y.index_select(0, lo + slots // k))
+        send[:, H].index_copy_(0, flat, (ids - dest * El).to(y.dtype))
+    recv = _a2a(pc, send.view(ep, C * W), torch.empty(ep, C * W, dtype=y.dtype, device=dev)).view(ep * C, W)
+    recv_e = recv[:, H].float().round().to(torch.int32).contiguous()
+    o2, inv2, offs2 = M.align(recv_e.view(-1, 1), El + 1)            # null bucket sorts last
+    xs = recv[:, :H].index_select(0, o2.long())
+    ys = moe.experts(li, xs, offs2[: El + 1].contiguous())            # rows past offs2[El] are never computed
+    out_recv = ys.index_select(0, inv2.long()).contiguous()
+    back = _a2a(pc, out_recv.view(ep, C * H), torch.empty(ep, C * H, dtype=y.dtype, device=dev)).view(ep * C, H)
+    own = y.new_zeros((per, H))
+    if n_own:
+        y_slots = back.index_select(0, flat)                         # (token, k) slot order
+        own[:n_own] = M.combine(y_slots.contiguous(), slots.to(torch.int32), topk_w[lo:hi].contiguous(), n_own, k)
+    # all-gather of the owned rows as an all-to-all of `ep` copies (one static-size collective)
+    gathered = _a2a(pc, own.unsqueeze(0).expand(ep, per, H).contiguous().view(ep, per * H),
+                    torch.empty(ep, per * H, dtype=y.dtype, device=dev))
+    return gathered.view(ep * per, H)[:T]
+
+
 def ep_moe_forward(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor) -> torch.Tensor:
+    if y.shape[0] <= FIXED_MAX_T:
+        return ep_moe_forward_fixed(moe, li, y, topk_w, topk_ids)
+    return ep_moe_forward_var(moe, li, y, topk_w, topk_ids)
+
+
+def ep_moe_forward_var(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor) -> torch.Tensor:
+    """Prefill-sized batches: exact variable-size all-to-alls (one counts
+    exchange and its host sync per layer)."""
     pc = moe.pc
     ep, r = pc.ep_size, pc.ep_rank
     grp = pc.ep_group

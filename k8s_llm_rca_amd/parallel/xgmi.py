@@ -42,6 +42,7 @@ def _bind(L) -> None:
         "k8s_ar_register": ([c_int, c_int, ctypes.POINTER(P), c_long, ctypes.c_double], c_int),
         "k8s_ar_unregister": ([c_int], c_int),
         "k8s_ar_allreduce_bf16": ([c_int, P, P, c_long, c_int, P], c_int),
+        "k8s_ar_alltoall_bf16": ([c_int, P, P, c_long, P], c_int),
         "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
     }
     for name, (args, res) in sigs.items():
@@ -107,6 +108,20 @@ class XgmiAllReduce:
         _check(self.L.k8s_ar_allreduce_bf16(self.id, t.data_ptr(), t.data_ptr(), t.numel(), m, stream_ptr(t)),
                "k8s_ar_allreduce_bf16")
         return t
+
+    def all_to_all(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
+        """Equal-split all-to-all: ``send`` [world, chunk...] bf16 -> ``recv`` (same
+        shape), ``recv[r]`` = rank r's ``send[this rank]``.  Device-side epoch:
+        no host sync, HIP-graph capturable (EP dispatch / combine, parallel/ep.py)."""
+        assert send.dtype == torch.bfloat16 and send.is_contiguous() and recv.is_contiguous()
+        assert send.shape[0] == self.world and send.shape == recv.shape
+        chunk = send.numel() // self.world
+        _check(self.L.k8s_ar_alltoall_bf16(self.id, send.data_ptr(), recv.data_ptr(), chunk, stream_ptr(send)),
+               "k8s_ar_alltoall_bf16")
+        return recv
+
+    def a2a_fits(self, nbytes: int) -> bool:
+        return nbytes <= 2 * self.max_bytes and (nbytes // 2) % (8 * self.world) == 0
 
     def status(self) -> int:
         v = ctypes.c_int(0)

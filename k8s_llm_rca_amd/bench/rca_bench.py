@@ -242,6 +242,7 @@ def run(args) -> Optional[Dict[str, Any]]:
         "errors_total": stream.n_err,
         "truncated_by_time_budget": truncated,
         "tokens": {"sampled": d["sampled_tokens"], "forced": d["forced_tokens"], "prefill": d["prefill_tokens"],
+                   "recomputed_after_truncation": d["recompute_tokens"],
                    "decode_rows": d["decode_tokens"]},
         "no_hints": nh,
         "engine": {"steps": d["steps"], "graph_steps": d["graph_steps"],

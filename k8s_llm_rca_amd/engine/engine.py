@@ -270,7 +270,8 @@ class LLMEngine:
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
-                      "prefix_hit_tokens": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0}
+                      "prefix_hit_tokens": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0,
+                      "recompute_tokens": 0}
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
 
@@ -468,6 +469,8 @@ class LLMEngine:
             cur = s.tokens
             while lcp < n and cur[lcp] == toks[lcp]:
                 lcp += 1
+            # cached positions the new prompt re-prefills (history truncation, divergence)
+            self.stats["recompute_tokens"] += max(0, n - lcp)
             s.tokens = toks
             s.n_cached = lcp
             BS = self.kv.block_size

@@ -44,6 +44,7 @@ class GraphBatcher:
         self._q: List[_Req] = []
         self._cv = threading.Condition()
         self._stop = False
+        self._dead: Optional[BaseException] = None
         self.stats: Dict[str, float] = {"requests": 0, "batches": 0, "launches": 0, "busy_s": 0.0, "max_batch": 0}
         self._t = threading.Thread(target=self._loop, name="graph-batcher", daemon=True)
         self._t.start()
@@ -52,6 +53,8 @@ class GraphBatcher:
     def _call(self, op: str, key: Tuple, args: Tuple) -> Any:
         r = _Req(op, key, args)
         with self._cv:
+            if self._dead is not None:
+                raise RuntimeError(f"graph batcher thread died: {self._dead!r}")
             self._q.append(r)
             self._cv.notify()
         r.done.wait()
@@ -78,9 +81,21 @@ class GraphBatcher:
 
     # -------------------------------------------------------------- worker
     def _loop(self) -> None:
-        import torch
-        if self.dev.device.type == "cuda":
-            torch.cuda.set_device(self.dev.device)
+        try:
+            import torch
+            if self.dev.device.type == "cuda" and self.dev.device.index is not None:
+                torch.cuda.set_device(self.dev.device)
+            self._serve()
+        except BaseException as e:  # noqa: BLE001 - never leave a caller waiting on a dead thread
+            with self._cv:
+                self._dead = e
+                pending, self._q = self._q, []
+            for r in pending:
+                r.error = e
+                r.done.set()
+            raise
+
+    def _serve(self) -> None:
         while True:
             with self._cv:
                 while not self._q and not self._stop:

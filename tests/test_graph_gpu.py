@@ -149,7 +149,7 @@ def test_batched_pipeline_queries_match_host():
     host = run_all(qs)
     bs = []
     for g in (c.stategraph, c.metagraph):
-        to_device(g, "cuda")
+        to_device(g, "cuda")  # no device index: the batcher thread uses the current device
         bs.append(enable_batching(g))
     got = [None] * len(qs)
 

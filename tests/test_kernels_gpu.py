@@ -329,6 +329,30 @@ def test_sampling_topk_vocab_parallel_candidates(tp):
     assert torch.equal(got.cpu(), full.cpu())
 
 
+@pytest.mark.parametrize("T,E,k", [(1, 8, 2), (300, 8, 2), (77, 4, 2), (64, 8, 1)])
+def test_moe_route_align_combine_vs_fp32(T, E, k):
+    """B11 / B12 kernels directly against their fp32 PyTorch references."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import moe as MO
+    torch.manual_seed(T * 10 + E)
+    logits = (torch.randn(T, E) * 2).bfloat16()
+    w, ids = MO.route_topk(logits.to(dev), k)
+    rw, rids = MO.route_topk(logits, k)  # CPU reference on the same bf16 values, in fp32
+    assert torch.equal(ids.cpu().sort(1).values, rids.sort(1).values)
+    torch.testing.assert_close(w.cpu().sort(1).values, rw.sort(1).values, atol=1e-5, rtol=1e-5)
+    order, inv, offs = MO.align(ids, E)
+    o, iv, of = order.cpu().long(), inv.cpu().long(), offs.cpu()
+    _, _, roffs = MO.align(ids.cpu(), E)
+    assert torch.equal(of, roffs)
+    flat = ids.cpu().reshape(-1).long()
+    assert torch.equal(flat[o], flat.sort(stable=True).values)      # grouped by expert
+    assert torch.equal(iv[o], torch.arange(T * k))                    # inv is the inverse permutation
+    y_perm = torch.randn(T * k, 256).bfloat16()
+    got = MO.combine(y_perm.to(dev), inv, w, T, k).float().cpu()
+    ref = (y_perm.float()[iv].view(T, k, 256) * w.cpu().view(T, k, 1)).sum(1)
+    torch.testing.assert_close(got, ref, atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("M", [1, 7, 16, 33, 64, 100])
 @pytest.mark.parametrize("N,K", [(4096, 4096), (6144, 4096), (512, 14336), (1280, 8192)])
 def test_gemm_skinny(M, N, K, monkeypatch):

@@ -31,9 +31,8 @@ def test_forward_gpu_matches_cpu(name):
     from k8s_llm_rca_amd.models.config import get_config
     from k8s_llm_rca_amd.models.llama import LlamaModel
     from tests.test_parallel import _inputs
-    cfg = get_config(name)
+    cfg = get_config(name, init_std=0.08)  # peaked logits: the argmax is stable under bf16 rounding
     ref_m = LlamaModel(cfg, "cpu", torch.float32, None, seed=3, init_mode="full_slice")
-    # exercise real attention: scale weights up so logits are not flat
     inp, BS = _inputs(cfg)
     kf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, BS, 128, generator=torch.Generator().manual_seed(7)) * 0.5
     vf = torch.randn(cfg.n_layers, 6, cfg.n_kv_heads, 128, BS, generator=torch.Generator().manual_seed(8))
@@ -54,9 +53,10 @@ def test_forward_gpu_matches_cpu(name):
     out = gm.forward(inp, kf.cuda().bfloat16(), vf.cuda().bfloat16())[:, : cfg.vocab_size].float().cpu()
     err = (out - ref).abs().max().item()
     scale = ref.abs().max().item()
-    assert err <= 0.05 * scale + 1e-3, (err, scale)
-    # the argmax token should agree on the vast majority of rows
-    assert (out.argmax(-1) == ref.argmax(-1)).float().mean() >= 0.66
+    rel = ((out - ref).norm() / ref.norm()).item()
+    # bf16 weights / activations with fp32 accumulation and fp32 logits vs the fp32 reference
+    assert rel <= 0.03 and err <= 0.03 * scale, (rel, err, scale)
+    assert torch.equal(out.argmax(-1), ref.argmax(-1))
 
 
 def test_engine_graph_vs_eager_decode():

@@ -55,7 +55,8 @@ def test_forward_gpu_matches_cpu(name):
     scale = ref.abs().max().item()
     rel = ((out - ref).norm() / ref.norm()).item()
     # bf16 weights / activations with fp32 accumulation and fp32 logits vs the fp32 reference
-    assert rel <= 0.03 and err <= 0.03 * scale, (rel, err, scale)
+    # (MoE: a near-tie router score may pick the other expert for a token under bf16)
+    assert rel <= 0.03 and err <= (0.05 if cfg.n_experts else 0.03) * scale, (rel, err, scale)
     assert torch.equal(out.argmax(-1), ref.argmax(-1))
 
 

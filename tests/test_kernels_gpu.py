@@ -335,7 +335,9 @@ def test_moe_route_align_combine_vs_fp32(T, E, k):
     _need_gpu()
     from k8s_llm_rca_amd.ops import moe as MO
     torch.manual_seed(T * 10 + E)
-    logits = (torch.randn(T, E) * 2).bfloat16()
+    # distinct values per row (exact in bf16): no top-k ties, whose order is arbitrary
+    logits = (torch.stack([torch.randperm(E) for _ in range(T)]).float() * 0.37 + torch.randn(T, 1)).bfloat16()
+    assert all(len(set(r.tolist())) == E for r in logits.float())
     w, ids = MO.route_topk(logits.to(dev), k)
     rw, rids = MO.route_topk(logits, k)  # CPU reference on the same bf16 values, in fp32
     assert torch.equal(ids.cpu().sort(1).values, rids.sort(1).values)

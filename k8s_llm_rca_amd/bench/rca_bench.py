@@ -240,6 +240,7 @@ def run(args) -> Optional[Dict[str, Any]]:
         "analyses_timed": total,
         "errors": err_timed,
         "errors_total": stream.n_err,
+        "abandoned_at_shutdown": stream.n_abandoned,
         "truncated_by_time_budget": truncated,
         "tokens": {"sampled": d["sampled_tokens"], "forced": d["forced_tokens"], "prefill": d["prefill_tokens"],
                    "recomputed_after_truncation": d["recompute_tokens"],

@@ -302,6 +302,7 @@ class IncidentStream:
         self.done: List[tuple] = []   # (t_done, latency_s, ok) in completion order
         self.n_ok = 0
         self.n_err = 0
+        self.n_abandoned = 0
         self.errors: List[str] = []
         self._threads: List[threading.Thread] = []
 
@@ -344,6 +345,9 @@ class IncidentStream:
                 ok, err = False, repr(e)
             t1 = time.perf_counter()
             with self._cv:
+                if self._stop and not ok:  # cut short by the shutdown (service closed), not a failure
+                    self.n_abandoned += 1
+                    return
                 self.done.append((t1, t1 - t, ok))
                 if ok:
                     self.n_ok += 1

@@ -54,9 +54,14 @@ int k8s_grouped_gemm_part(const void* a, int lda, const void* w, void* y, int ld
 int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
                     size_t ws_bytes, hipStream_t s);
 int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int mode, hipStream_t s);
+int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg, int splits,
+                    void* part, hipStream_t s);
+int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                         int splits, void* part, hipStream_t s);
 }
 
-// kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits);
+// kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
+// 4 gemm_stream (cfg = ring depth, splits);
 // fuse: a split-K o / down projection may leave its partials to the next norm
 struct K8sGemmSel {
   int kind, cfg, splits, fuse;
@@ -124,10 +129,12 @@ constexpr int kD = 128;
 // partials in the kind's scratch for the following norm to reduce
 // (k8s_splitk_addnorm); deferred() tells the caller where they are.
 bool deferred(const K8sGemmSel& g, bool defer) {
-  return defer && g.fuse && g.splits > 1 && (g.kind == 2 || g.kind == 3);
+  return defer && g.fuse && g.splits > 1 && (g.kind == 2 || g.kind == 3 || g.kind == 4);
 }
 
-const void* part_of(const K8sLlamaStep& s, const K8sGemmSel& g) { return g.kind == 2 ? s.mid_part : s.grp_part; }
+const void* part_of(const K8sLlamaStep& s, const K8sGemmSel& g) {
+  return (g.kind == 2 || g.kind == 4) ? s.mid_part : s.grp_part;
+}
 
 int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, const void* w, void* y, int ldy, int M,
          int N, int K, hipStream_t st, bool defer = false) {
@@ -140,6 +147,9 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
     case 3:
       return (d ? k8s_grouped_gemm_part : k8s_grouped_gemm)(x, ldx, w, y, ldy, s.grp_offs, 1, N, K,
                                                             (M + 63) / 64 + 1, 0, g.splits, s.grp_part, M, st);
+    case 4:
+      return (d ? k8s_gemm_stream_part : k8s_gemm_stream)(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part,
+                                                          st);
     default:
       return k8s_blaslt_gemm(x, ldx, w, y, ldy, M, N, K, s.blaslt_ws, s.blaslt_ws_bytes, st);
   }

@@ -182,7 +182,7 @@ class LlamaExecutor:
             kind, cfg, splits = LIN.select_gemm(T, N, K)
             st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
             st.sel[i].fuse = int(_fuse_splitk)
-            if kind == LIN.KIND_MID and splits > 1:
+            if kind in (LIN.KIND_MID, LIN.KIND_STREAM) and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:
                 need_grp = max(need_grp, splits * T * N if splits > 1 else 1)

@@ -23,7 +23,7 @@ def set_skinny(enabled: bool) -> None:
     _enabled = enabled
 
 
-KIND_LIB, KIND_SKINNY, KIND_MID, KIND_GRP = 0, 1, 2, 3
+KIND_LIB, KIND_SKINNY, KIND_MID, KIND_GRP, KIND_STREAM = 0, 1, 2, 3, 4
 
 
 def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bool = True) -> Tuple[int, int, int]:
@@ -40,6 +40,8 @@ def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bo
                 return KIND_MID, cfg, splits
             if kind == "grp" and x_ok_layout and out_contig and N % 128 == 0 and K % (64 * splits) == 0:
                 return KIND_GRP, 0, splits
+            if kind == "stream" and x_ok_layout and out_contig and N % 64 == 0 and K % (64 * splits) == 0:
+                return KIND_STREAM, cfg, splits
             if kind == "lib":
                 return KIND_LIB, 0, 1
             forced_skinny = kind == "skinny" and M <= 128
@@ -61,6 +63,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
         return gemm_mid(x, w, cfg, splits, out)
     if kind == KIND_GRP:
         return gemm_grp(x, w, splits, out)
+    if kind == KIND_STREAM:
+        return gemm_stream(x, w, cfg, splits, out)
     if kind == KIND_SKINNY:
         if out is None:
             out = torch.empty((M, N), dtype=x.dtype, device=x.device)
@@ -294,6 +298,36 @@ def gemm_grp(x: torch.Tensor, w: torch.Tensor, splits: int, out: torch.Tensor = 
     return MO.grouped_gemm(x, w.view(1, *w.shape), offs, out=out, splits=splits)
 
 
+def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
+                out: torch.Tensor = None) -> torch.Tensor:
+    """``x @ w.T`` on the W-shared decode kernel (csrc/kernels/gemm_stream.hip):
+    a workgroup's 4 waves split the rows of a 64-column strip, W is staged once
+    through swizzled LDS, X goes L2 -> registers; ``cfg`` = W register ring
+    depth (4 / 8), K split over ``splits`` workgroups (fp32 partials + reduce)."""
+    M = x.shape[0]
+    N, K = w.shape
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    part = _scratch(x.device, splits * M * N) if splits > 1 else None
+    check(lib().k8s_gemm_stream(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, cfg, splits,
+                                ptr(part), stream_ptr(x)), "gemm_stream")
+    return out
+
+
+def stream_candidates(M: int, N: int, K: int):
+    """(cfg, splits) of the stream kernel for (M, N, K): 128..2048 workgroups."""
+    out = []
+    if not (0 < M <= 256 and N % 64 == 0):
+        return out
+    for cfg in (4, 8):
+        for s in (1, 2, 4, 7, 8, 14, 16):
+            if K % (64 * s) or K // s < 64 * 2:
+                continue
+            if 128 <= (N // 64) * s <= 2048:
+                out.append((cfg, s))
+    return out
+
+
 def linear_silu(gu: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     """``silu_mul(gu) @ w.T`` (the SwiGLU down projection): one SwiGLU-fused
     gemm_mid launch where the dispatch table measured it fastest, else the
@@ -348,7 +382,7 @@ def reserve_dispatch_scratch(dev: torch.device) -> None:
     for key, rows in _dispatch.items():
         n = key[-2]
         for m, kind, _, splits in rows:
-            if kind == "mid" and splits > 1:
+            if kind in ("mid", "stream") and splits > 1:  # both use the gemm_mid partial buffer
                 need_mid = max(need_mid, m * n * splits)
             elif kind == "grp" and splits > 1:
                 need_grp = max(need_grp, m * n * splits)
@@ -408,6 +442,8 @@ def candidate_kernels(M: int, N: int, K: int):
         for s in (1, 2, 4, 8):
             if K % (64 * s) == 0 and (N // 128) * ((M + 63) // 64) * s <= 2048:
                 out.append((f"grp:x{s}", lambda x, w, s=s: gemm_grp(x, w, s)))
+    for cfg, s in stream_candidates(M, N, K):
+        out.append((f"stream{cfg}:x{s}", lambda x, w, cfg=cfg, s=s: gemm_stream(x, w, cfg, s)))
     return out
 
 

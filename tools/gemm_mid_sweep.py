@@ -45,6 +45,7 @@ def main():
     ap.add_argument("--ms", default=BUCKETS)
     ap.add_argument("--emit", action="store_true")
     ap.add_argument("--margin", type=float, default=0.97)
+    ap.add_argument("--out", default=None, help="write the table here instead of data/ (with --emit)")
     a = ap.parse_args()
     L.clear_dispatch()  # time the raw kernels
     ms = [int(m) for m in a.ms.split(",")]
@@ -86,7 +87,8 @@ def main():
                 cands.append((bench(lambda: fn(x, rot(wl))), name))
             cands.sort()
             for t, n in cands:
-                k = "mid" if n.startswith("mid") else "grp" if n.startswith("grp") else n
+                k = ("mid" if n.startswith("mid") else "grp" if n.startswith("grp") else
+                     "stream" if n.startswith("stream") else n)
                 res.setdefault(k, t)
             best = {"m": M, "kind": "lib", "t_us": round(lib_t, 2), "lib_us": round(lib_t, 2)}
             if cands and cands[0][0] < a.margin * lib_t:
@@ -95,6 +97,9 @@ def main():
                     best.update(kind="skinny", t_us=round(t, 2))
                 elif n.startswith("grp"):
                     best.update(kind="grp", splits=int(n.split("x")[-1]), t_us=round(t, 2))
+                elif n.startswith("stream"):
+                    best.update(kind="stream", cfg=int(n[6:].split(":")[0]), splits=int(n.split("x")[-1]),
+                                t_us=round(t, 2))
                 else:
                     cfg, sp = n[3:].split(":")[0], n.split("x")[-1]
                     best.update(kind="mid", cfg=int(cfg), splits=int(sp), t_us=round(t, 2))
@@ -136,7 +141,7 @@ def main():
         print(f"M{M:4d} per-layer sum: hipblaslt {lt:8.1f}us  dispatch {bt:8.1f}us  ({lt / bt:.2f}x)")
     print(f"sweep took {time.time() - t0:.0f}s")
     if a.emit:
-        path = L.dispatch_path(a.model, a.tp)
+        path = a.out or L.dispatch_path(a.model, a.tp)
         with open(path, "w") as f:
             json.dump({"model": a.model, "tp": a.tp, "device": torch.cuda.get_device_name(),
                        "note": "per-M-bucket fastest kernel, cold weights (tools/gemm_mid_sweep.py)",

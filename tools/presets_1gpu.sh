@@ -15,10 +15,12 @@ run() {
 }
 for p in "$@"; do
   case $p in
-    8b-1k)     run 8b-1k --preset llama3-8b-1k --steps 2 --warmup 1 ;;
-    8b-100k)   run 8b-100k --preset llama3-8b-100k --steps 2 --warmup 1 ;;
-    mixtral)   run mixtral --preset mixtral-10k --steps 2 --warmup 1 ;;
-    70b-tp1)   run 70b-tp1 --preset llama3-70b-tp8-10k --tp 1 --incidents 32 --steps 1 --warmup 1 ;;
-    8b-192)    run 8b-192 --incidents 192 --steps 2 --warmup 1 ;;
+    # the driver's step contract (--steps 20 --warmup 5: 16 completed analyses per step)
+    8b-1k)     run 8b-1k --preset llama3-8b-1k --steps 20 --warmup 5 --no-hints-steps 0 ;;
+    8b-100k)   run 8b-100k --preset llama3-8b-100k --steps 20 --warmup 5 --no-hints-steps 0 ;;
+    mixtral)   run mixtral --preset mixtral-10k --steps 10 --warmup 3 --no-hints-steps 0 ;;
+    70b-tp1)   run 70b-tp1 --preset llama3-70b-tp8-10k --tp 1 --incidents 32 --quantum 4 --steps 5 --warmup 2 \
+                   --no-hints-steps 0 ;;
+    8b-192)    run 8b-192 --incidents 192 --steps 20 --warmup 5 --no-hints-steps 0 ;;
   esac
 done

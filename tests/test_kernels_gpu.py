@@ -504,3 +504,24 @@ def test_blaslt_tuned_solutions():
             torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
     finally:
         LIN.clear_lib_tuning()
+
+
+@pytest.mark.parametrize("M", [1, 17, 64, 96, 128, 200, 256])
+@pytest.mark.parametrize("N,K,splits", [(4096, 4096, 8), (6144, 4096, 4), (512, 14336, 7), (1280, 8192, 1)])
+@pytest.mark.parametrize("cfg", [4, 8])
+def test_gemm_stream_vs_fp32(M, N, K, splits, cfg):
+    """W-shared decode GEMM (csrc/kernels/gemm_stream.hip) vs fp32, incl. an
+    asymmetric exact check (identity rows pick weight columns)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    y = LIN.gemm_stream(x, w, cfg, splits)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    e = torch.zeros(M, K, device=dev).bfloat16()
+    idx = torch.arange(M, device=dev) * 37 % K
+    e[torch.arange(M, device=dev), idx] = 1.0
+    ye = LIN.gemm_stream(e, w, cfg, splits)
+    assert torch.equal(ye, w[:, idx].t().contiguous())

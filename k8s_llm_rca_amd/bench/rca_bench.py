@@ -253,7 +253,13 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,
-                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3)},
+                   "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
+                   # decode-attention KV blocks read per distinct block (sampled every 32nd graph step)
+                   "kv_block_reuse": round(d["kv_read_blocks_sampled"] / max(1, d["kv_unique_blocks_sampled"]), 2),
+                   "admit_s": round(d["admit_s"], 3), "post_s": round(d["post_s"], 3),
+                   # K8S_RCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
+                   **({k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}
+                      if d["eager_gpu_s"] or d["graph_gpu_s"] else {})},
         "throughput": {  # rank 0's engine over the timed window
             "prefill_tok_per_s": round(d["prefill_tokens"] / elapsed, 1),
             "decode_tok_per_s": round(d["decode_tokens"] / elapsed, 1),

@@ -271,7 +271,7 @@ class LLMEngine:
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
                       "prefix_hit_tokens": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0,
-                      "recompute_tokens": 0}
+                      "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0}
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
 
@@ -1137,7 +1137,9 @@ class LLMEngine:
         graph = torch.cuda.CUDAGraph()
         if self._graph_pool is None:
             self._graph_pool = torch.cuda.graph_pool_handle()
-        with torch.cuda.graph(graph, pool=self._graph_pool):
+        # thread_local: the graph-query batcher keeps issuing on its own stream from its
+        # own thread while a bucket is captured mid-run
+        with torch.cuda.graph(graph, pool=self._graph_pool, capture_error_mode="thread_local"):
             out = self._model_fwd(inp)
         self._graphs[key] = (graph, out)
         self.stats["captures"] += 1
@@ -1167,6 +1169,10 @@ class LLMEngine:
         # plan on the real rows; padded rows (ctx 1) still get a one-key item
         # (sorted last) so every output row the graph produces is finite
         _, part = A.plan_decode_split(ctx[:B], self.model.nkv)
+        if self.stats["graph_steps"] % 32 == 0:  # how often decode attention re-reads a shared KV block
+            used = np.concatenate([s.blocks[: (s.n_cached + BS) // BS] for s in decode])
+            self.stats["kv_read_blocks_sampled"] += used.size
+            self.stats["kv_unique_blocks_sampled"] += np.unique(used).size
         items = A.build_decode_items(ctx, np.arange(Bb), part)
         n_items = items.shape[0]
         assert n_items <= self._max_items

@@ -66,7 +66,7 @@ def main():
     from k8s_llm_rca_amd.models.config import get_config
     mc = get_config(a.model)
     down = (mc.hidden, mc.intermediate // a.tp) if not mc.n_experts else None
-    tot = {}
+    tot, lm, layer_gb = {}, {}, {}
     t0 = time.time()
     for M in ms:
         for (N, K) in shapes:
@@ -135,10 +135,16 @@ def main():
             top = " | ".join(f"{n} {t:.1f}" for t, n in cands[:3])
             print(f"M{M:4d} N{N:6d} K{K:6d}  {line}   [{top}] -> {best['kind']}", flush=True)
             tot.setdefault(M, [0.0, 0.0])
+            if N * a.tp >= mc.vocab_size:  # the LM head runs once per step, not per layer
+                lm[M] = (lib_t, best["t_us"])
+                continue
             tot[M][0] += lib_t
             tot[M][1] += best["t_us"]
+            layer_gb[M] = layer_gb.get(M, 0.0) + gb
     for M, (lt, bt) in tot.items():
-        print(f"M{M:4d} per-layer sum: hipblaslt {lt:8.1f}us  dispatch {bt:8.1f}us  ({lt / bt:.2f}x)")
+        print(f"M{M:4d} per-layer sum (qkv+o+gate_up+silu+down): hipblaslt {lt:8.1f}us  dispatch {bt:8.1f}us  "
+              f"({lt / bt:.2f}x, weights {layer_gb.get(M, 0) / (bt * 1e-6) / 1e3:4.2f}TB/s)"
+              + (f"   lm_head: hipblaslt {lm[M][0]:7.1f}us  dispatch {lm[M][1]:7.1f}us" if M in lm else ""))
     print(f"sweep took {time.time() - t0:.0f}s")
     if a.emit:
         path = a.out or L.dispatch_path(a.model, a.tp)

@@ -19,6 +19,9 @@ URL at this server:
                                               instead of the reference's 5 s sleep loop)
     POST /v1/threads/{id}/runs/{run_id}/cancel
     GET  /health      GET /metrics (Prometheus: run counts, engine counters)
+    POST /db/{name}/tx/commit                {statements: [{statement, parameters}]}
+                                              (Neo4j's HTTP transactional endpoint shape,
+                                              over the in-process graphs passed as ``graphs``)
 
 ``response_format`` is ``{"type": "text"}`` or ``{"type": "k8s_grammar",
 "grammar": ...}`` (:func:`..engine.grammar.grammar_to_json`) for constrained
@@ -58,8 +61,67 @@ def _response_format_out(rf: Any):
     return rf
 
 
-def create_app(service: AssistantService, engine=None):
-    """FastAPI app serving ``service`` (``engine``: optional LLMEngine for /metrics)."""
+def _cypher_value(v):
+    """Neo4j HTTP "row" encoding: nodes and relationships as their property
+    maps, paths as the alternating node/relationship list."""
+    from ..graph.model import Entity, Path
+    if isinstance(v, Path):
+        out = []
+        for i, n in enumerate(v.nodes):
+            if i:
+                out.append(dict(v.relationships[i - 1].items()))
+            out.append(dict(n.items()))
+        return out
+    if isinstance(v, Entity):
+        return dict(v.items())
+    if isinstance(v, (list, tuple)):
+        return [_cypher_value(x) for x in v]
+    if isinstance(v, dict):
+        return {k: _cypher_value(x) for k, x in v.items()}
+    return v
+
+
+def _cypher_meta(v):
+    from ..graph.model import Node, Path, Relationship
+    if isinstance(v, Node):
+        return {"id": v.id, "elementId": v.element_id, "type": "node", "deleted": False}
+    if isinstance(v, Relationship):
+        return {"id": v.id, "elementId": v.element_id, "type": "relationship", "deleted": False}
+    if isinstance(v, Path):
+        return [_cypher_meta(x) for i, n in enumerate(v.nodes)
+                for x in ((v.relationships[i - 1], n) if i else (n,))]
+    return None
+
+
+def cypher_commit(executors: Dict[str, Any], db: str, body: Dict[str, Any]) -> Dict[str, Any]:
+    """One ``/db/{db}/tx/commit`` request: run each statement in order; the
+    first failing statement ends the request with a Neo4j-coded error (the
+    reference's retry loop keys on ``CypherSyntaxError``, ``test_all.py:109``)."""
+    from ..graph.model import CypherSyntaxError
+    ex = executors.get(db)
+    if ex is None:
+        return {"results": [], "errors": [{"code": "Neo.ClientError.Database.DatabaseNotFound",
+                                            "message": f"database {db!r} not found"}]}
+    results, errors = [], []
+    for st in body.get("statements", []):
+        try:
+            recs = ex.run_query(st["statement"], st.get("parameters") or None)
+        except CypherSyntaxError as e:
+            errors.append({"code": "Neo.ClientError.Statement.SyntaxError", "message": str(e)})
+            break
+        except Exception as e:  # noqa: BLE001 - surfaced to the client, as Neo4j does
+            errors.append({"code": "Neo.DatabaseError.Statement.ExecutionFailed", "message": str(e)})
+            break
+        cols = recs[0].keys() if recs else []
+        results.append({"columns": cols,
+                        "data": [{"row": [_cypher_value(v) for v in r.values()],
+                                  "meta": [_cypher_meta(v) for v in r.values()]} for r in recs]})
+    return {"results": results, "errors": errors}
+
+
+def create_app(service: AssistantService, engine=None, graphs: Optional[Dict[str, Any]] = None):
+    """FastAPI app serving ``service`` (``engine``: optional LLMEngine for /metrics;
+    ``graphs``: database name -> PropertyGraph / graph URI for the Cypher endpoint)."""
     from fastapi import Body, FastAPI, HTTPException, Query
     from fastapi.responses import PlainTextResponse
 
@@ -162,6 +224,15 @@ def create_app(service: AssistantService, engine=None):
             return _dump(service.retrieve_run(tid, rid))
         except KeyError as e:
             nf(e)
+
+    executors: Dict[str, Any] = {}
+    if graphs:
+        from .graph import GraphQueryExecutor
+        executors = {name: GraphQueryExecutor(g) for name, g in graphs.items()}
+
+    @app.post("/db/{db}/tx/commit")
+    def tx_commit(db: str, body: Dict[str, Any] = Body(...)):
+        return cypher_commit(executors, db, body)
 
     @app.get("/metrics")
     def metrics():

@@ -11,7 +11,9 @@
 * ``query``      stage 2 only for one metapath string (``test_generate_query.py``)
 * ``state``      stage 3 only for one entity (``test_check_state.py``)
 * ``token-probe`` token accounting over two runs (``test_token.py``)
-* ``serve``      OpenAI-Assistants-shaped REST API over the engine (api/http.py);
+* ``serve``      OpenAI-Assistants-shaped REST API over the engine, plus the
+                 Neo4j HTTP ``/db/{metagraph,stategraph}/tx/commit`` endpoint over
+                 the graphs (api/http.py);
                  ``run --server URL`` drives a remote server instead of an
                  in-process engine
 
@@ -252,8 +254,10 @@ def cmd_serve(args) -> int:
     import uvicorn
     from .api.http import create_app
     svc, eng = _service(args)
+    meta, state, _ = _load_cluster(args)
     try:
-        uvicorn.run(create_app(svc, eng), host=args.host, port=args.port, log_level="warning")
+        uvicorn.run(create_app(svc, eng, graphs={"metagraph": meta, "stategraph": state}), host=args.host,
+                    port=args.port, log_level="warning")
     finally:
         if eng is not None:
             eng.stop()

@@ -121,3 +121,27 @@ def test_cli_serve_and_remote_run(tmp_path):
     finally:
         srv.terminate()
         srv.wait(30)
+
+
+def test_cypher_tx_commit_endpoint(small_cluster):
+    """Neo4j HTTP transactional endpoint over the in-process graphs: rows match
+    the executor, nodes come back as property maps with node meta, syntax
+    errors carry Neo4j's SyntaxError code."""
+    svc = AssistantService(ScriptedBackend(lambda rs: "ok"))
+    client = TestClient(create_app(svc, graphs={"stategraph": small_cluster.stategraph,
+                                                 "metagraph": small_cluster.metagraph}))
+    q = "MATCH (n:Pod) RETURN n.id AS name, n LIMIT 3"
+    body = client.post("/db/stategraph/tx/commit", json={"statements": [{"statement": q}]}).json()
+    assert body["errors"] == []
+    res = body["results"][0]
+    want = GraphQueryExecutor(small_cluster.stategraph).run_query(q)
+    assert res["columns"] == ["name", "n"]
+    assert [d["row"][0] for d in res["data"]] == [r["name"] for r in want]
+    assert all(d["row"][1]["id"] == d["row"][0] and d["meta"][1]["type"] == "node" for d in res["data"])
+    body = client.post("/db/metagraph/tx/commit",
+                       json={"statements": [{"statement": "MATCH (n) RETURN count(n) AS c"},
+                                            {"statement": "MATCH (n RETURN n"}]}).json()
+    assert len(body["results"]) == 1 and body["results"][0]["data"][0]["row"][0] > 0
+    assert body["errors"][0]["code"] == "Neo.ClientError.Statement.SyntaxError"
+    assert client.post("/db/nope/tx/commit", json={"statements": []}).json()["errors"][0]["code"].endswith(
+        "DatabaseNotFound")

@@ -262,6 +262,7 @@ def main():
 
         tot = {k: 0.0 for k in list(shapes) + ["lm"]}
         by_range = {}
+        fl_range = {}
         for M, S in zip(Ms, Ss):
             Mb = bucket(M)
             rng = "M<=16" if M <= 16 else "M<=64" if M <= 64 else "M<=256" if M <= 256 else "M<=1024" if M <= 1024 \
@@ -270,11 +271,12 @@ def main():
                 us = t_of(k, Mb) * 32
                 tot[k] += us
                 by_range[rng] = by_range.get(rng, 0.0) + us
+                fl_range[rng] = fl_range.get(rng, 0.0) + 2.0 * M * shapes[k][0] * shapes[k][1] * 32
             tot["lm"] += t_of("lm", bucket(S))
         for k, v in tot.items():
             res[f"gemm_replay {k}"] = f"{v / 1e6:.3f} s over {len(Ms)} steps"
         for k, v in sorted(by_range.items()):
-            res[f"gemm_replay range {k}"] = f"{v / 1e6:.3f} s ({sum(1 for M in Ms if (k == 'M<=16' and M <= 16) or (k == 'M<=64' and 16 < M <= 64) or (k == 'M<=256' and 64 < M <= 256) or (k == 'M<=1024' and 256 < M <= 1024) or (k == 'M>1024' and M > 1024))} steps)"
+            res[f"gemm_replay range {k}"] = f"{v / 1e6:.3f} s {fl_range[k] / (v * 1e-6) / 1e12:6.0f} TFLOP/s ({sum(1 for M in Ms if (k == 'M<=16' and M <= 16) or (k == 'M<=64' and 16 < M <= 64) or (k == 'M<=256' and 64 < M <= 256) or (k == 'M<=1024' and 256 < M <= 1024) or (k == 'M>1024' and M > 1024))} steps)"
     if args.what == "decode_sweep":
         for B in (32, 48, 56, 64, 72, 96, 128):
             for ctxv in (1000, 3400):

@@ -277,6 +277,38 @@ def main():
             res[f"gemm_replay {k}"] = f"{v / 1e6:.3f} s over {len(Ms)} steps"
         for k, v in sorted(by_range.items()):
             res[f"gemm_replay range {k}"] = f"{v / 1e6:.3f} s {fl_range[k] / (v * 1e-6) / 1e12:6.0f} TFLOP/s ({sum(1 for M in Ms if (k == 'M<=16' and M <= 16) or (k == 'M<=64' and 16 < M <= 64) or (k == 'M<=256' and 64 < M <= 256) or (k == 'M<=1024' and 256 < M <= 1024) or (k == 'M>1024' and M > 1024))} steps)"
+    if args.what == "share_test":
+        # decode rows whose first L keys sit on the SAME pages in groups of G rows
+        # (cross-thread prefix sharing): does the current kernel already get those
+        # re-reads from L2 / MALL, i.e. does time track unique or total KV bytes?
+        B, ctxv = 125, 4700
+        nbs = (ctxv + BS - 1) // BS
+        for L, G in [(0, 1), (1024, 42), (1536, 42), (2048, 42), (1536, 4)]:
+            ls = L // BS
+            n_groups = (B + G - 1) // G
+            n_pages = n_groups * ls + B * (nbs - ls)
+            perm = torch.randperm(n_pages).int()
+            bt = torch.zeros(B, nbs, dtype=torch.int32)
+            u = n_groups * ls
+            for s_ in range(B):
+                g = s_ // G
+                bt[s_, :ls] = perm[g * ls:(g + 1) * ls]
+                bt[s_, ls:] = perm[u:u + nbs - ls]
+                u += nbs - ls
+            ctx = [ctxv] * B
+            meta, _ = make_meta(ctx, [1] * B, nq, nkv, BS, dev, True)
+            meta.block_tables = bt.to(dev)
+            kc = torch.empty(n_pages, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
+            vc = torch.empty(n_pages, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
+            q = torch.randn(B, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+            out = torch.empty(B, nq * 128, device=dev).bfloat16()
+            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out), iters=20)
+            tot_b = B * ctxv * nkv * 512
+            uniq_b = n_pages * BS * nkv * 512
+            res[f"share L{L} G{G}"] = (f"{us:.1f}us total {tot_b / us / 1e6:.2f} TB/s unique {uniq_b / us / 1e6:.2f} TB/s "
+                                       f"(unique/total {uniq_b / tot_b:.2f})")
+            del kc, vc
+            torch.cuda.empty_cache()
     if args.what == "decode_sweep":
         for B in (32, 48, 56, 64, 72, 96, 128):
             for ctxv in (1000, 3400):

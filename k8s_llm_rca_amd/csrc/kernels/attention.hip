@@ -422,8 +422,14 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
   }
 }
 
-// grid: (nq, S); block 128 (one thread per output column)
+// grid: (nq, S); block 128 (one thread per output column).  The (m, l) of the
+// row's partitions are loaded ONE PER THREAD and shared through LDS, and the
+// partial-O column loads of consecutive partitions are independent (unrolled),
+// so a row costs a few memory latencies instead of 2 * n_parts serial ones
+// (9.1 us per layer at one decode row with ~12 partitions before, c=1 profile).
+// Same max and the same summation order as the serial form.
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
+  __shared__ float sf[128], sl[128], scratch[16];
   const int qh = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
   const int ctx = a.ctx_lens[seq];
   const int part_size = a.d_n_items ? a.d_n_items[1] : a.part_size;
@@ -431,13 +437,28 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
   float M = -INFINITY;
-  for (int p = 0; p < np; ++p) M = fmaxf(M, a.part_ml[(base + p) * 2]);
+  for (int p = d; p < np; p += 128) M = fmaxf(M, a.part_ml[(base + p) * 2]);
+  M = block_max(M, scratch);
   float L = 0.f, acc = 0.f;
-  for (int p = 0; p < np; ++p) {
-    const float m = a.part_ml[(base + p) * 2];
-    const float f = (m == -INFINITY) ? 0.f : exp2f(m - M);
-    L += a.part_ml[(base + p) * 2 + 1] * f;
-    acc += a.part_o[(base + p) * D + d] * f;
+  for (int p0 = 0; p0 < np; p0 += 128) {
+    const int p = p0 + d;
+    float f = 0.f, lf = 0.f;
+    if (p < np) {
+      const float m = a.part_ml[(base + p) * 2];
+      f = (m == -INFINITY) ? 0.f : exp2f(m - M);
+      lf = a.part_ml[(base + p) * 2 + 1] * f;
+    }
+    __syncthreads();  // the previous chunk's readers are done with sf / sl
+    sf[d] = f;
+    sl[d] = lf;
+    __syncthreads();
+    const int n = min(128, np - p0);
+    const float* po = a.part_o + (base + p0) * D + d;
+#pragma unroll 8
+    for (int j = 0; j < n; ++j) {
+      L += sl[j];
+      acc += po[(size_t)j * D] * sf[j];
+    }
   }
   const int qrow = a.q_start[seq];
   a.out[(size_t)qrow * a.out_stride + qh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);

@@ -89,8 +89,10 @@ def build_hip(force: bool = False, jobs: int = 8) -> str:
         tmp = out + ".tmp"
         # -lhipblaslt resolves (SONAME libhipblaslt.so.1) to the copy torch already
         # mapped when the library is loaded after `import torch`: one hipBLASLt per process
+        # -z defs: an unresolved symbol (e.g. a kernel launch stub the host pass
+        # dropped) fails the build here, not the first dlopen on the GPU box
         _run([HIPCC, "-shared", "-fPIC", f"--offload-arch={ARCH}", *objs, "-L/opt/rocm/lib", "-lhipblaslt",
-              "-o", tmp])
+              "-Wl,-z,defs", "-o", tmp])
         os.replace(tmp, out)
     return out
 

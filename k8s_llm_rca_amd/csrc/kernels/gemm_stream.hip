@@ -14,8 +14,10 @@
 //     read of 16 rows hits 16 distinct bank slots) and read by the 4 waves:
 //     16 KB of LDS reads per 32-deep k-step whatever M is.
 //   * X (M x K, a few hundred KB: L2-resident) goes straight from L2 into each
-//     wave's own A-fragment registers, prefetched one chunk ahead: no LDS, no
-//     sharing needed since each wave owns its rows.
+//     wave's own A-fragment registers, in the same U-chunk ring as W (a
+//     chunk's W and X loads are issued together, so the in-order vmcnt wait
+//     for one chunk never drains the later ones): no LDS, no sharing needed
+//     since each wave owns its rows.
 //   * v_mfma_f32_16x16x32_bf16: A = X rows (16 m), B = W^T (16 n); one W
 //     fragment read from LDS feeds MTW MFMAs.
 //   * split-K over gridDim.y: fp32 partials [split][M][N] reduced by a
@@ -61,7 +63,9 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
     const int m = min(m_base + 16 * mt + r, M - 1);
     xrow[mt] = x + (size_t)m * ldx + kbeg + 8 * g;
   }
-  const bool active = m_base < M;  // waves past the last row only help stage W
+  // every wave computes (a wave past the last row works on clamped rows and
+  // stores nothing): no wave-dependent branch around a load, see below
+  const bool active = m_base < M;
 
   f32x4 acc[MTW][4];
 #pragma unroll
@@ -69,26 +73,28 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
 #pragma unroll
     for (int cf = 0; cf < 4; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // ring slot c % U holds chunk c: its W pieces (written to LDS one iteration
+  // before chunk c is computed) and this wave's X fragments of it (read
+  // straight from the registers by chunk c's MFMAs).  W and X of a chunk are
+  // issued together, U chunks ahead, so loads are consumed in issue order and
+  // the in-order vmcnt never drains the ring early: (U-1) chunks stay in flight
+  // while one is computed.
   u16x8 ring[U][2];
-  bf16x8 xr[2][2][MTW];
-  auto load_w = [&](int slot, int c) {
+  bf16x8 xq[U][2][MTW];
+  auto load_chunk = [&](int slot, int c) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) ring[slot][i] = *reinterpret_cast<const u16x8*>(wsrc[i] + c * kSC);
+#pragma unroll
+    for (int s = 0; s < 2; ++s)
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt)
+        xq[slot][s][mt] = *reinterpret_cast<const bf16x8*>(xrow[mt] + c * kSC + 32 * s);
   };
   auto store_w = [&](int slot, int buf) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) *reinterpret_cast<u16x8*>(&ws[buf][wdst[i]]) = ring[slot][i];
   };
-  auto load_x = [&](int set, int c) {
-    if (!active) return;
-#pragma unroll
-    for (int s = 0; s < 2; ++s)
-#pragma unroll
-      for (int mt = 0; mt < MTW; ++mt)
-        xr[set][s][mt] = *reinterpret_cast<const bf16x8*>(xrow[mt] + c * kSC + 32 * s);
-  };
-  auto compute = [&](int buf, int set) {
-    if (!active) return;
+  auto compute = [&](int buf, int slot) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -97,40 +103,172 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(&ws[buf][n * kSC + 8 * sswz(n, 4 * s + g)]);
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt)
-          acc[mt][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xr[set][s][mt], wf, acc[mt][cf], 0, 0, 0);
+          acc[mt][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xq[slot][s][mt], wf, acc[mt][cf], 0, 0, 0);
       }
   };
 
-  // ---- prologue: W chunks 0..U-1 in flight, X chunk 0, W chunk 0 -> LDS
+  // ---- prologue: chunks 0..U-1 in flight, chunk 0's W -> LDS
+  // (nch % U == 0 and nch >= U: checked at launch)
 #pragma unroll
-  for (int u = 0; u < U; ++u)
-    if (u < nch) load_w(u, u);
-  load_x(0, 0);
+  for (int u = 0; u < U; ++u) load_chunk(u, u);
   store_w(0, 0);
-  if (U < nch) load_w(0, U);
   __syncthreads();
 
-  // ---- main loop, unrolled by U (even): ring slots and X sets are compile-time
-  static_assert(U % 2 == 0, "U must be even");
+  // ---- main loop, unrolled by U (ring slots compile-time).  EVERY load is
+  // unconditional: one past the slice is clamped to the last chunk (an L2
+  // hit) -- a conditional load makes hipcc wait vmcnt(0) before every ring
+  // ds_write, which left ONE chunk in flight per workgroup (7.5 GB/s per
+  // workgroup: 0.95 TB/s at 128 workgroups, profiles/r2_gemm_probe_m128*.txt).
   for (int c0 = 0; c0 < nch; c0 += U) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int c = c0 + u;
-      if (c < nch) {
-        if (c + 1 < nch) load_x((u + 1) & 1, c + 1);
-        compute(c & 1, u & 1);
-        if (c + 1 < nch) {
-          const int slot = (u + 1) % U;
-          store_w(slot, (c + 1) & 1);
-          if (c + 1 + U < nch) load_w(slot, c + 1 + U);
-        }
-        __syncthreads();
-      }
+      compute(c & 1, u);
+      store_w((u + 1) % U, (c + 1) & 1);
+      load_chunk(u, min(c + U, nch - 1));
+      __syncthreads();
     }
   }
 
   // ---- epilogue: acc[mt][cf][v] = C[m = m_base + 16 mt + 4 g + v][n = n0 + 16 cf + r]
   if (!active) return;
+  if (gridDim.y == 1) {
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m_base + 16 * mt + 4 * g + v;
+        if (m < M) {
+#pragma unroll
+          for (int cf = 0; cf < 4; ++cf) y[(size_t)m * ldy + n0 + 16 * cf + r] = f2bf(acc[mt][cf][v]);
+        }
+      }
+  } else {
+    float* pp = part + (size_t)split * M * N;
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m_base + 16 * mt + 4 * g + v;
+        if (m < M) {
+#pragma unroll
+          for (int cf = 0; cf < 4; ++cf) pp[(size_t)m * N + n0 + 16 * cf + r] = acc[mt][cf][v];
+        }
+      }
+  }
+}
+
+// ---------------------------------------------------------------- LDS-DMA
+// Same decomposition (64-column strip x all M rows x one K slice per
+// workgroup, 4 waves splitting the rows), both operands staged by
+// global_load_lds (16-byte LDS-DMA, no VGPR round trip) into an NB-stage LDS
+// ring.  X arrives as full 128-byte row pieces instead of the fragment-shaped
+// L2 loads of the register-ring kernel (16 rows x 64 B per instruction, the
+// TA-bound pattern).  Both images are lane-linear per DMA instruction with
+// the XOR swizzle applied on the SOURCE address (piece j of row n lands in
+// slot j ^ (n & 7)), so every ds_read_b128 fragment read is the same as the
+// register-ring kernel's.  Synchronisation (cdna_hip_programming.md,
+// "Pipelining across barriers"): one __shared__ array, a counted
+// s_waitcnt vmcnt((NB-2) * DMAs per chunk) + raw s_barrier per chunk (never
+// __syncthreads, whose fence would drain the DMAs in flight), lgkmcnt(0)
+// after the fragment reads so the stage can be re-filled after the next
+// barrier.
+typedef __attribute__((address_space(3))) void lds_void_t;
+
+// a __device__ function: with the builtin written in the kernel template's own
+// body, hipcc's host pass silently dropped the kernels' launch stubs
+__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_dst, 16, 0, 0);
+}
+
+template <int MTW, int NB>
+__global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
+                                                        const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                        int ldy, float* __restrict__ part, int M, int N, int K,
+                                                        int kslice) {
+  constexpr int MP = 64 * MTW;        // X rows staged: 4 waves x MTW 16-row fragments
+  constexpr int WST = kSBN * kSC;     // W stage: 64 rows x 64 k
+  constexpr int STG = WST + MP * kSC;  // elements per stage
+  constexpr int XPT = MP * 8 / 256;   // X pieces (DMAs) per thread per chunk
+  constexpr int LPC = 2 + XPT;        // DMAs per thread per chunk
+  __shared__ __attribute__((aligned(16))) uint16_t sm[NB * STG];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int n0 = blockIdx.x * kSBN;
+  const int split = blockIdx.y;
+  const int kbeg = split * kslice;
+  const int nch = kslice / kSC;
+  const int m_base = wv * 16 * MTW;
+
+  const uint16_t* wsrc[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int p = 256 * i + tid, n = p >> 3, jl = p & 7;
+    wsrc[i] = w + (size_t)(n0 + n) * K + kbeg + 8 * (jl ^ (n & 7));
+  }
+  const uint16_t* xsrc[XPT];
+#pragma unroll
+  for (int i = 0; i < XPT; ++i) {
+    const int p = 256 * i + tid, m = p >> 3, jl = p & 7;
+    xsrc[i] = x + (size_t)min(m, M - 1) * ldx + kbeg + 8 * (jl ^ (m & 7));
+  }
+  auto issue = [&](int stage, int c) {
+    uint16_t* st = sm + stage * STG;
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+      glds16(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
+#pragma unroll
+    for (int i = 0; i < XPT; ++i)
+      glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
+  };
+
+  f32x4 acc[MTW][4];
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+    for (int cf = 0; cf < 4; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  auto compute = [&](int stage) {
+    const uint16_t* ws = sm + stage * STG;
+    const uint16_t* xs = ws + WST;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      bf16x8 xf[MTW];
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) {
+        const int m = m_base + 16 * mt + r;
+        xf[mt] = *reinterpret_cast<const bf16x8*>(xs + m * kSC + 8 * ((4 * s + g) ^ (m & 7)));
+      }
+#pragma unroll
+      for (int cf = 0; cf < 4; ++cf) {
+        const int n = 16 * cf + r;
+        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + n * kSC + 8 * ((4 * s + g) ^ (n & 7)));
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt)
+          acc[mt][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[mt], wf, acc[mt][cf], 0, 0, 0);
+      }
+    }
+  };
+
+  // prologue: chunks 0..NB-2 in flight (nch % NB == 0, nch >= NB: checked at launch)
+#pragma unroll
+  for (int c = 0; c < NB - 1; ++c) issue(c, c);
+  for (int c0 = 0; c0 < nch; c0 += NB) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int c = c0 + u;
+      // this wave's DMAs of chunk c are done when at most the NB-2 later chunks' remain
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * LPC) : "memory");
+      __builtin_amdgcn_s_barrier();  // every wave's chunk c landed; every wave is done reading chunk c-1
+      issue((u + NB - 1) % NB, min(c + NB - 1, nch - 1));  // re-fill chunk c-1's stage (clamped: an L2 hit)
+      compute(u);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+
+  // epilogue (the register-ring kernel's): acc[mt][cf][v] = C[m_base + 16 mt + 4 g + v][n0 + 16 cf + r]
+  if (m_base >= M) return;
   if (gridDim.y == 1) {
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt)
@@ -179,6 +317,13 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_kernel(const float* __
   *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + n) = o;
 }
 
+template <int MTW, int NB>
+static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
+                              int ldy, float* part, int M, int N, int K, int kslice) {
+  hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K, kslice);
+  return hipGetLastError();
+}
+
 template <int MTW, int U>
 static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
                                 int ldy, float* part, int M, int N, int K, int kslice) {
@@ -190,15 +335,21 @@ static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int
 
 using namespace k8s;
 
-// cfg: ring depth U (4 or 8).  splits > 1 needs `part` = splits * M * N fp32;
+// cfg: register-ring depth U (4 or 8), or 10 + NB for the LDS-DMA kernel (NB = 3 or 4
+// stages).  splits > 1 needs `part` = splits * M * N fp32;
 // reduce = 0 leaves the partials for a fused consumer.
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, bool reduce, hipStream_t s) {
   if (M <= 0 || M > 256 || N % kSBN || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
-      (cfg != 4 && cfg != 8) || ldx % 8 || (splits > 1 && (M * N) % 8) || (splits == 1 && ldy < N))
+      (cfg != 4 && cfg != 8 && cfg != 13 && cfg != 14) || ldx % 8 || (splits > 1 && (M * N) % 8) ||
+      (splits == 1 && ldy < N))
     return (int)hipErrorInvalidValue;
   const int kslice = K / splits;
+  const int unroll = cfg > 10 ? cfg - 10 : cfg;  // register ring depth U, or LDS-DMA stages NB (cfg = 10 + NB)
+  if ((kslice / kSC) % unroll) return (int)hipErrorInvalidValue;  // the kernel's loop is unrolled by that many chunks
   const int mtw = ((M + 15) / 16 + 3) / 4;  // 16-row fragments per wave (4 waves)
+  if (cfg == 14 && mtw > 3) return (int)hipErrorInvalidValue;  // 4 stages of 64 + 256 rows exceed the LDS
+  if (cfg == 8 && mtw > 2) return (int)hipErrorInvalidValue;  // an 8-deep X ring would not fit the VGPRs
   const dim3 grid(N / kSBN, splits);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
@@ -206,7 +357,21 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   float* pp = (float*)part;
   hipError_t e;
 #define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
-  if (cfg == 4) {
+#define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
+  if (cfg == 13) {
+    switch (mtw) {
+      case 1: K8S_GL(1, 3); break;
+      case 2: K8S_GL(2, 3); break;
+      case 3: K8S_GL(3, 3); break;
+      default: K8S_GL(4, 3); break;
+    }
+  } else if (cfg == 14) {
+    switch (mtw) {
+      case 1: K8S_GL(1, 4); break;
+      case 2: K8S_GL(2, 4); break;
+      default: K8S_GL(3, 4); break;
+    }
+  } else if (cfg == 4) {
     switch (mtw) {
       case 1: K8S_SL(1, 4); break;
       case 2: K8S_SL(2, 4); break;
@@ -217,11 +382,11 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
     switch (mtw) {
       case 1: K8S_SL(1, 8); break;
       case 2: K8S_SL(2, 8); break;
-      case 3: K8S_SL(3, 8); break;
-      default: K8S_SL(4, 8); break;
+      default: return (int)hipErrorInvalidValue;
     }
   }
 #undef K8S_SL
+#undef K8S_GL
   if (e != hipSuccess) return (int)e;
   if (splits > 1 && reduce) {
     const int blocks = (M * N / 8 + 255) / 256;

@@ -40,7 +40,7 @@ def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bo
                 return KIND_MID, cfg, splits
             if kind == "grp" and x_ok_layout and out_contig and N % 128 == 0 and K % (64 * splits) == 0:
                 return KIND_GRP, 0, splits
-            if kind == "stream" and x_ok_layout and out_contig and N % 64 == 0 and K % (64 * splits) == 0:
+            if kind == "stream" and x_ok_layout and out_contig and stream_shape_ok(M, N, K, cfg, splits):
                 return KIND_STREAM, cfg, splits
             if kind == "lib":
                 return KIND_LIB, 0, 1
@@ -314,14 +314,24 @@ def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
     return out
 
 
+def stream_shape_ok(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
+    """What csrc/kernels/gemm_stream.hip's launcher accepts: 64-column strips,
+    64-deep chunks, a slice of whole cfg-chunk loop trips, the 8-deep ring only
+    up to two 16-row fragments per wave (M <= 128)."""
+    unroll = cfg - 10 if cfg > 10 else cfg  # cfg 13 / 14: the LDS-DMA kernel with 3 / 4 stages
+    return (0 < M <= 256 and N % 64 == 0 and splits >= 1 and K % (64 * splits) == 0
+            and (K // splits // 64) % unroll == 0
+            and (cfg in (4, 13) or (cfg == 8 and M <= 128) or (cfg == 14 and M <= 192)))
+
+
 def stream_candidates(M: int, N: int, K: int):
     """(cfg, splits) of the stream kernel for (M, N, K): 128..2048 workgroups."""
     out = []
     if not (0 < M <= 256 and N % 64 == 0):
         return out
-    for cfg in (4, 8):
+    for cfg in (4, 8, 13, 14):
         for s in (1, 2, 4, 7, 8, 14, 16):
-            if K % (64 * s) or K // s < 64 * 2:
+            if not stream_shape_ok(M, N, K, cfg, s):
                 continue
             if 128 <= (N // 64) * s <= 2048:
                 out.append((cfg, s))

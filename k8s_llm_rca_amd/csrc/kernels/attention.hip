@@ -754,18 +754,27 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
   const int rows = a.m_len[mi] * a.G;
   if (row >= rows) return;
   const int tok0 = a.m_tok0[mi], slot0 = a.m_slot0[mi], np = a.m_np[mi];
-  float M = -INFINITY, L = 0.f, o0 = 0.f, o1 = 0.f;
+  // two passes (the row max, then the rescaled sums) whose per-part loads do
+  // not depend on each other, so they are in flight together: the online form
+  // chained every part's loads behind the previous part's rescale (11.4 us per
+  // merge launch, r2 headline profile)
+  float M = -INFINITY;
+#pragma unroll 4
+  for (int p = 0; p < np; ++p) {
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * PF_ROWS + row;
+    M = fmaxf(M, a.pf_ml[rb * 2]);
+  }
+  float L = 0.f, o0 = 0.f, o1 = 0.f;
+#pragma unroll 4
   for (int p = 0; p < np; ++p) {
     const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * PF_ROWS + row;
     const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
     const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
-    if (ml.x == -INFINITY) continue;  // this part saw no key of the row
-    const float Mn = fmaxf(M, ml.x);
-    const float fo = __builtin_amdgcn_exp2f(M - Mn), fp = __builtin_amdgcn_exp2f(ml.x - Mn);
-    L = L * fo + ml.y * fp;
-    o0 = o0 * fo + v.x * fp;
-    o1 = o1 * fo + v.y * fp;
-    M = Mn;
+    // a part that saw no key of the row has m = -inf: weight 0
+    const float f = (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
+    L += ml.y * f;
+    o0 += v.x * f;
+    o1 += v.y * f;
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   const int tt = row / a.G, g = row % a.G;

@@ -746,8 +746,8 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
 }
 
 // grid: (n_merge * nkv, PF_ROWS / 4); block 256: ONE WAVE PER ROW (a wave
-// walking many rows serialises np dependent loads per row).  Single online
-// pass: O = sum_p o_p 2^(m_p - M) / sum_p l_p 2^(m_p - M), 2 dims per lane.
+// walking many rows serialises np dependent loads per row).  Two passes:
+// M = max_p m_p, then O = sum_p o_p 2^(m_p - M) / sum_p l_p 2^(m_p - M), 2 dims per lane.
 __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
   const int kvh = blockIdx.x % a.nkv, mi = blockIdx.x / a.nkv;
   const int lane = threadIdx.x & 63, row = blockIdx.y * 4 + (threadIdx.x >> 6);

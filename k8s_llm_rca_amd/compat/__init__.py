@@ -48,3 +48,36 @@ def install(shims: bool = False) -> None:
         sys.path.insert(0, SHIMS_DIR)
         for mod in [m for m in sys.modules if m in ("openai", "neo4j") or m.startswith(("openai.", "neo4j."))]:
             del sys.modules[mod]
+
+
+def start_local(model: str = "llama3-8b", weights: str = None, tokenizer: str = None, device: str = None,
+                graphs: dict = None, kv_gb: float = None, shims: bool = True):
+    """One call for migrating drivers: start the in-process LLM engine on this
+    GPU (``weights``: an HF checkpoint dir; random init otherwise), make it the
+    default assistant service the ``openai`` shim talks to, register
+    ``graphs`` (``{"bolt://host:7687": graph or graph-file path, ...}`` -- the
+    URIs the driver hard-codes) for the ``neo4j`` shim, and :func:`install` the
+    reference's import paths.  Returns the engine (``engine.stop()`` when done).
+    """
+    import torch
+
+    from ..api.service import AssistantService, set_default_service
+    from ..engine.backend import EngineBackend
+    from ..engine.engine import EngineConfig, LLMEngine
+
+    install(shims=shims)
+    dev = device or ("cuda" if torch.cuda.is_available() else "cpu")
+    cfg = EngineConfig(model=model, device=dev, dtype=torch.bfloat16 if dev != "cpu" else torch.float32,
+                       kv_max_gb=kv_gb, num_blocks=None if dev != "cpu" else 1024, weights=weights,
+                       tokenizer=tokenizer)
+    eng = LLMEngine(cfg)
+    eng.start()
+    set_default_service(AssistantService(EngineBackend(eng)))
+    if graphs:
+        if not shims:
+            raise ValueError("graphs= binds bolt:// URIs in the neo4j shim: needs shims=True")
+        import neo4j  # the shim module install() put first on sys.path (the one driver code imports)
+        for uri, g in graphs.items():
+            neo4j.map_uri(uri, g)
+    return eng
+

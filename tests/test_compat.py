@@ -2,6 +2,7 @@
 the reference's ``test_all.py:54-131`` runs unchanged against this framework
 (scripted replies in place of GPT-4, a synthetic graph file in place of Neo4j)."""
 import json
+import time
 import os
 
 import pytest
@@ -151,3 +152,45 @@ def test_reference_test_all_runs_unchanged_on_shims(monkeypatch, capsys):
     out = capsys.readouterr().out
     assert "nfs path missing" in out  # check_statepath's summary report was printed
     assert "close connection" in out
+
+
+def test_start_local_serves_openai_shim_from_engine():
+    """``compat.start_local``: one call gives unchanged OpenAI-SDK-style code an
+    in-process engine (tiny Llama on CPU here) behind ``OpenAI().beta``, and
+    binds a hard-coded bolt:// URI to a graph for the neo4j shim."""
+    import sys
+
+    from k8s_llm_rca_amd import compat
+    from k8s_llm_rca_amd.graph.synth import generate_cluster
+
+    saved_path = list(sys.path)
+    saved_mods = {k: v for k, v in sys.modules.items() if k.split(".")[0] in ("openai", "neo4j")}
+    c = generate_cluster(300, 1, seed=1)
+    eng = compat.start_local(model="tiny-llama", device="cpu", graphs={"bolt://10.1.0.174:7687": c.stategraph})
+    try:
+        import neo4j
+        import openai
+        assert openai.__file__.startswith(compat.SHIMS_DIR) and neo4j.__file__.startswith(compat.SHIMS_DIR)
+        client = openai.OpenAI()
+        a = client.beta.assistants.create(instructions="You are terse.", name="t", model="gpt-4")
+        th = client.beta.threads.create()
+        client.beta.threads.messages.create(thread_id=th.id, role="user", content="hello")
+        run = client.beta.threads.runs.create(thread_id=th.id, assistant_id=a.id, max_completion_tokens=8)
+        for _ in range(600):
+            run = client.beta.threads.runs.retrieve(thread_id=th.id, run_id=run.id)
+            if run.status not in ("queued", "in_progress"):
+                break
+            time.sleep(0.05)
+        assert run.status == "completed"
+        msgs = client.beta.threads.messages.list(thread_id=th.id)
+        assert msgs.data[0].role == "assistant"
+        with neo4j.GraphDatabase.driver("bolt://10.1.0.174:7687", auth=("neo4j", "x")) as drv:
+            with drv.session() as sess:
+                n = list(sess.run("MATCH (n:Pod) RETURN count(n) AS c"))[0]["c"]
+        assert n > 0
+    finally:
+        eng.stop()
+        sys.path[:] = saved_path
+        for k in [k for k in sys.modules if k.split(".")[0] in ("openai", "neo4j")]:
+            del sys.modules[k]
+        sys.modules.update(saved_mods)

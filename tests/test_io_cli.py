@@ -142,3 +142,26 @@ def test_cli_stage_drivers(tmp_path, capsys):
     assert "MATCH (evt:EVENT)" in capsys.readouterr().out
     assert main(["state", *base, "--kind", "Pod", "--id", inc.involved_id, "--timestamp", inc.timestamp]) == 0
     assert capsys.readouterr().out.strip()
+
+
+@pytest.mark.slow
+def test_bench_tp2_cpu(tmp_path):
+    """``bench.py --gpus 2 --tp 2``: one TP=2 engine (rank 0 schedules, rank 1
+    serves the step channel) runs the whole RCA stream; parallelism reads tp2
+    and the aggregate counts ONE engine's analyses."""
+    import json as _json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--tp", "2", "--steps", "2", "--warmup", "1",
+           "--quantum", "1", "--device", "cpu", "--model", "tiny-llama-g8", "--incidents", "2", "--graph-nodes", "300",
+           "--no-hints-steps", "0"]
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(PYTHONPATH=root, OMP_NUM_THREADS="2")
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    d = _json.loads(lines[0])
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "tp2" and d["steps"] == 2
+    assert d["analyses_timed"] == 2 and d["errors"] == 0

@@ -107,7 +107,8 @@ def test_mixtral_engine_graphs_match_eager():
     assert outs[0] == outs[1]
 
 
-@pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True)])
+@pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True),
+                                           (False, "stream"), (True, "stream")])
 def test_layer_executor_bit_identical(graphs, splitk):
     """The native layer executor (one C call per forward) issues the same
     kernels in the same order as the Python layer loop: every step's logits
@@ -121,6 +122,8 @@ def test_layer_executor_bit_identical(graphs, splitk):
     from k8s_llm_rca_amd.ops import layer_exec as LX
     from k8s_llm_rca_amd.ops import linear as LIN
     split_rows = [(32, "mid", 0, 2), (64, "mid", 2, 4), (256, "grp", -1, 2)]  # tiny-llama o and down: [512, 1024]
+    if splitk == "stream":  # the register-ring and LDS-DMA stream kernels (dispatch kind 4)
+        split_rows = [(16, "stream", 4, 2), (64, "stream", 14, 2), (256, "stream", 14, 4)]
     runs = []
     try:
         for on in (False, True):
@@ -129,8 +132,12 @@ def test_layer_executor_bit_identical(graphs, splitk):
                                          temperature=0.0, max_batch_tokens=256, graph_batch_sizes=(1, 2, 4, 8)))
             if splitk:  # after the engine's own (absent) dispatch table was loaded
                 LIN._dispatch[(512, 1024)] = split_rows
-                assert LIN.select_gemm(6, 512, 1024)[0] == LIN.KIND_MID
-                assert LIN.select_gemm(100, 512, 1024)[0] == LIN.KIND_GRP
+                if splitk == "stream":
+                    assert LIN.select_gemm(6, 512, 1024)[0] == LIN.KIND_STREAM
+                    assert LIN.select_gemm(100, 512, 1024) == (LIN.KIND_STREAM, 14, 4)
+                else:
+                    assert LIN.select_gemm(6, 512, 1024)[0] == LIN.KIND_MID
+                    assert LIN.select_gemm(100, 512, 1024)[0] == LIN.KIND_GRP
             logs = []
             fwd = eng.model.forward
 

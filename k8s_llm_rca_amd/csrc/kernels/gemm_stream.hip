@@ -250,9 +250,9 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
     }
   };
 
-  // prologue: chunks 0..NB-2 in flight (nch % NB == 0, nch >= NB: checked at launch)
+  // prologue: chunks 0..NB-2 in flight (clamped to the slice's last chunk)
 #pragma unroll
-  for (int c = 0; c < NB - 1; ++c) issue(c, c);
+  for (int c = 0; c < NB - 1; ++c) issue(c, min(c, nch - 1));
   for (int c0 = 0; c0 < nch; c0 += NB) {
 #pragma unroll
     for (int u = 0; u < NB; ++u) {
@@ -261,7 +261,9 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * LPC) : "memory");
       __builtin_amdgcn_s_barrier();  // every wave's chunk c landed; every wave is done reading chunk c-1
       issue((u + NB - 1) % NB, min(c + NB - 1, nch - 1));  // re-fill chunk c-1's stage (clamped: an L2 hit)
-      compute(u);
+      // the last trip may run past the slice (nch % NB != 0): those steps skip
+      // only the MFMAs -- every DMA, wait and barrier stays unconditional
+      if (c < nch) compute(u);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
@@ -335,20 +337,21 @@ static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int
 
 using namespace k8s;
 
-// cfg: register-ring depth U (4 or 8), or 10 + NB for the LDS-DMA kernel (NB = 3 or 4
-// stages).  splits > 1 needs `part` = splits * M * N fp32;
+// cfg: register-ring depth U (4 or 8), or 10 + NB for the LDS-DMA kernel (NB = 3..6
+// stages; 5 and 6 for M <= 64).  splits > 1 needs `part` = splits * M * N fp32;
 // reduce = 0 leaves the partials for a fused consumer.
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, bool reduce, hipStream_t s) {
   if (M <= 0 || M > 256 || N % kSBN || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
-      (cfg != 4 && cfg != 8 && cfg != 13 && cfg != 14) || ldx % 8 || (splits > 1 && (M * N) % 8) ||
+      (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16)) || ldx % 8 || (splits > 1 && (M * N) % 8) ||
       (splits == 1 && ldy < N))
     return (int)hipErrorInvalidValue;
   const int kslice = K / splits;
-  const int unroll = cfg > 10 ? cfg - 10 : cfg;  // register ring depth U, or LDS-DMA stages NB (cfg = 10 + NB)
-  if ((kslice / kSC) % unroll) return (int)hipErrorInvalidValue;  // the kernel's loop is unrolled by that many chunks
+  // the register-ring loop is unrolled by U chunks with no partial trip
+  if (cfg < 10 && (kslice / kSC) % cfg) return (int)hipErrorInvalidValue;
   const int mtw = ((M + 15) / 16 + 3) / 4;  // 16-row fragments per wave (4 waves)
-  if (cfg == 14 && mtw > 3) return (int)hipErrorInvalidValue;  // 4 stages of 64 + 256 rows exceed the LDS
+  // LDS-DMA stages of (64 + 64 * mtw) x 64 bf16 must fit the 160 KB of LDS
+  if ((cfg == 14 && mtw > 3) || (cfg > 14 && mtw > 1)) return (int)hipErrorInvalidValue;
   if (cfg == 8 && mtw > 2) return (int)hipErrorInvalidValue;  // an 8-deep X ring would not fit the VGPRs
   const dim3 grid(N / kSBN, splits);
   const uint16_t* xx = (const uint16_t*)x;
@@ -371,6 +374,10 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
       case 2: K8S_GL(2, 4); break;
       default: K8S_GL(3, 4); break;
     }
+  } else if (cfg == 15) {
+    K8S_GL(1, 5);
+  } else if (cfg == 16) {
+    K8S_GL(1, 6);
   } else if (cfg == 4) {
     switch (mtw) {
       case 1: K8S_SL(1, 4); break;

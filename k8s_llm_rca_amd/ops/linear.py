@@ -318,10 +318,12 @@ def stream_shape_ok(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
     """What csrc/kernels/gemm_stream.hip's launcher accepts: 64-column strips,
     64-deep chunks, a slice of whole cfg-chunk loop trips, the 8-deep ring only
     up to two 16-row fragments per wave (M <= 128)."""
-    unroll = cfg - 10 if cfg > 10 else cfg  # cfg 13 / 14: the LDS-DMA kernel with 3 / 4 stages
-    return (0 < M <= 256 and N % 64 == 0 and splits >= 1 and K % (64 * splits) == 0
-            and (K // splits // 64) % unroll == 0
-            and (cfg in (4, 13) or (cfg == 8 and M <= 128) or (cfg == 14 and M <= 192)))
+    # cfg 13..16: the LDS-DMA kernel with 3..6 stages (any chunk count); 4 / 8:
+    # the register ring, whose loop has no partial trip
+    ok_cfg = (cfg == 4 or (cfg == 8 and M <= 128) or cfg == 13 or (cfg == 14 and M <= 192)
+              or (cfg in (15, 16) and M <= 64))
+    return (ok_cfg and 0 < M <= 256 and N % 64 == 0 and splits >= 1 and K % (64 * splits) == 0
+            and (cfg > 10 or (K // splits // 64) % cfg == 0))
 
 
 def stream_candidates(M: int, N: int, K: int):
@@ -329,7 +331,7 @@ def stream_candidates(M: int, N: int, K: int):
     out = []
     if not (0 < M <= 256 and N % 64 == 0):
         return out
-    for cfg in (4, 8, 13, 14):
+    for cfg in (4, 8, 13, 14, 15, 16):
         for s in (1, 2, 4, 7, 8, 14, 16):
             if not stream_shape_ok(M, N, K, cfg, s):
                 continue

@@ -55,6 +55,8 @@ class GraphBatcher:
         with self._cv:
             if self._dead is not None:
                 raise RuntimeError(f"graph batcher thread died: {self._dead!r}")
+            if self._stop:  # the worker drains what is queued, then exits: nothing would serve this
+                raise RuntimeError("graph batcher is closed")
             self._q.append(r)
             self._cv.notify()
         r.done.wait()

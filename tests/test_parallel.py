@@ -229,3 +229,41 @@ def test_ep_moe_matches_ep1(world):
         b = torch.load(o1, weights_only=True)
     for T in b:
         torch.testing.assert_close(a[T], b[T], atol=1e-5, rtol=1e-5)
+
+
+def _run_channel(rank, world, port, out_path):
+    import numpy as np
+    import torch.distributed as dist
+
+    from k8s_llm_rca_amd.parallel.channel import FWD_GRAPH, SAMPLE, STOP, StepChannel
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    ch = StepChannel(dist.group.WORLD, 0)
+    msgs = [(FWD_GRAPH, [np.arange(5, dtype=np.int32), np.array([1, -2, 3 << 40], dtype=np.int64),
+                         np.array([0.5, -1.25], dtype=np.float32)]),
+            (SAMPLE, [np.zeros(0, np.int32), np.arange(3, dtype=np.int64)]),
+            (STOP, [])]
+    got = []
+    if rank == 0:
+        for kind, arrs in msgs:
+            ch.send(kind, arrs)
+    else:
+        for _ in msgs:
+            kind, arrs = ch.recv()
+            got.append((kind, [(a.dtype.str, a.tolist()) for a in arrs]))
+        want = [(k, [(a.dtype.str, a.tolist()) for a in arrs]) for k, arrs in msgs]
+        assert got == want, (got, want)
+        with open(f"{out_path}.{rank}", "w") as f:
+            f.write("ok")
+    dist.destroy_process_group()
+
+
+def test_step_channel_roundtrip():
+    """The TP host step channel (parallel/channel.py) delivers every message's
+    kind and int32 / int64 / float32 arrays bit-exactly to every worker, in
+    order, including empty arrays and payload-free messages."""
+    world = 3
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "ch")
+        mp.spawn(_run_channel, args=(world, _free_port(), out), nprocs=world, join=True)
+        assert all(open(f"{out}.{r}").read() == "ok" for r in range(1, world))

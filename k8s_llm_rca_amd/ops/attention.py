@@ -8,6 +8,7 @@ MFMA operand is a contiguous load; see ``csrc/kernels/attention.hip``).
 from __future__ import annotations
 
 import math
+import os
 from dataclasses import dataclass
 from typing import List, Optional
 
@@ -246,7 +247,8 @@ def prefill_tile_tokens(G: int, block_size: int) -> int:
 
 PF_ROWS = 128               # (token, q-head) rows per paged-64 prefill workgroup
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
-PF_TARGET_WGS = 512         # split long key ranges until a prefill launch has about this many workgroups
+# split long key ranges until a prefill launch has about this many workgroups
+PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
 _NO_END = 1 << 30
 
 

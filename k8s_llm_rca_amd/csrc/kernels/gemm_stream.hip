@@ -182,52 +182,47 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_dst) {
 }
 
 template <int MTW, int NB>
-__global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
-                                                        const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                        int ldy, float* __restrict__ part, int M, int N, int K,
-                                                        int kslice) {
-  constexpr int MP = 64 * MTW;        // X rows staged: 4 waves x MTW 16-row fragments
-  constexpr int WST = kSBN * kSC;     // W stage: 64 rows x 64 k
+constexpr int glds_lds_elems() {
+  return NB * (kSBN * kSC + 64 * MTW * kSC);
+}
+
+// One workgroup's 64-column strip over one K slice: acc += X[0..M) . W[strip]^T.
+// x: the tile's first row (rows past M are clamped, never stored); wstrip: the
+// strip's first W row ([N][K] row-major, K-slice offset already applied);
+// nch: 64-deep chunks in the slice; sm: the kernel's one __shared__ array of
+// glds_lds_elems<MTW, NB>() elements.
+template <int MTW, int NB>
+__device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int ldx, int M,
+                                           const uint16_t* __restrict__ wstrip, int K, int nch, uint16_t* sm,
+                                           f32x4 (&acc)[MTW][4]) {
+  constexpr int MP = 64 * MTW;         // X rows staged: 4 waves x MTW 16-row fragments
+  constexpr int WST = kSBN * kSC;      // W stage: 64 rows x 64 k
   constexpr int STG = WST + MP * kSC;  // elements per stage
-  constexpr int XPT = MP * 8 / 256;   // X pieces (DMAs) per thread per chunk
-  constexpr int LPC = 2 + XPT;        // DMAs per thread per chunk
-  __shared__ __attribute__((aligned(16))) uint16_t sm[NB * STG];
+  constexpr int XPT = MP * 8 / 256;    // X pieces (DMAs) per thread per chunk
+  constexpr int LPC = 2 + XPT;         // DMAs per thread per chunk
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * kSBN;
-  const int split = blockIdx.y;
-  const int kbeg = split * kslice;
-  const int nch = kslice / kSC;
   const int m_base = wv * 16 * MTW;
 
   const uint16_t* wsrc[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int p = 256 * i + tid, n = p >> 3, jl = p & 7;
-    wsrc[i] = w + (size_t)(n0 + n) * K + kbeg + 8 * (jl ^ (n & 7));
+    wsrc[i] = wstrip + (size_t)n * K + 8 * (jl ^ (n & 7));
   }
   const uint16_t* xsrc[XPT];
 #pragma unroll
   for (int i = 0; i < XPT; ++i) {
     const int p = 256 * i + tid, m = p >> 3, jl = p & 7;
-    xsrc[i] = x + (size_t)min(m, M - 1) * ldx + kbeg + 8 * (jl ^ (m & 7));
+    xsrc[i] = x + (size_t)min(m, M - 1) * ldx + 8 * (jl ^ (m & 7));
   }
   auto issue = [&](int stage, int c) {
     uint16_t* st = sm + stage * STG;
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-      glds16(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
+    for (int i = 0; i < 2; ++i) glds16(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
 #pragma unroll
-    for (int i = 0; i < XPT; ++i)
-      glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
+    for (int i = 0; i < XPT; ++i) glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
   };
-
-  f32x4 acc[MTW][4];
-#pragma unroll
-  for (int mt = 0; mt < MTW; ++mt)
-#pragma unroll
-    for (int cf = 0; cf < 4; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-
   auto compute = [&](int stage) {
     const uint16_t* ws = sm + stage * STG;
     const uint16_t* xs = ws + WST;
@@ -268,33 +263,87 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+}
 
-  // epilogue (the register-ring kernel's): acc[mt][cf][v] = C[m_base + 16 mt + 4 g + v][n0 + 16 cf + r]
+// acc[mt][cf][v] = C[m_base + 16 mt + 4 g + v][16 cf + r] of the tile: bf16 rows
+// of y (final) or fp32 rows of `part` (split-K partial), rows < M only.
+template <int MTW>
+__device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][4], int M, uint16_t* __restrict__ y, int ldy,
+                                           float* __restrict__ pp, int ldp) {
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int m_base = wv * 16 * MTW;
   if (m_base >= M) return;
-  if (gridDim.y == 1) {
 #pragma unroll
-    for (int mt = 0; mt < MTW; ++mt)
+  for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = m_base + 16 * mt + 4 * g + v;
-        if (m < M) {
+    for (int v = 0; v < 4; ++v) {
+      const int m = m_base + 16 * mt + 4 * g + v;
+      if (m < M) {
 #pragma unroll
-          for (int cf = 0; cf < 4; ++cf) y[(size_t)m * ldy + n0 + 16 * cf + r] = f2bf(acc[mt][cf][v]);
+        for (int cf = 0; cf < 4; ++cf) {
+          if (pp)
+            pp[(size_t)m * ldp + 16 * cf + r] = acc[mt][cf][v];
+          else
+            y[(size_t)m * ldy + 16 * cf + r] = f2bf(acc[mt][cf][v]);
         }
       }
-  } else {
-    float* pp = part + (size_t)split * M * N;
+    }
+}
+
+template <int MTW, int NB>
+__global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
+                                                        const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                        int ldy, float* __restrict__ part, int M, int N, int K,
+                                                        int kslice) {
+  __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<MTW, NB>()];
+  const int n0 = blockIdx.x * kSBN, split = blockIdx.y, kbeg = split * kslice;
+  f32x4 acc[MTW][4];
 #pragma unroll
-    for (int mt = 0; mt < MTW; ++mt)
+  for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = m_base + 16 * mt + 4 * g + v;
-        if (m < M) {
-#pragma unroll
-          for (int cf = 0; cf < 4; ++cf) pp[(size_t)m * N + n0 + 16 * cf + r] = acc[mt][cf][v];
-        }
-      }
+    for (int cf = 0; cf < 4; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  glds_strip<MTW, NB>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc);
+  if (gridDim.y == 1)
+    glds_store<MTW>(acc, M, y + n0, ldy, nullptr, 0);
+  else
+    glds_store<MTW>(acc, M, nullptr, 0, part + (size_t)split * M * N + n0, N);
+}
+
+// MoE grouped form (B13, decode batches): rows offsets[e] .. offsets[e+1] of x
+// times W_e^T for every expert e in one launch (w [E][N][K]).  Grid (N / 64,
+// max_tiles, splits): workgroup (nb, j, z) walks the per-expert counts of
+// 64-row tiles to find its (expert, tile); surplus workgroups exit.  Split-K
+// partials are [splits][total_rows][N] (gemm_stream_reduce_kernel's layout).
+template <int NB>
+__global__ void __launch_bounds__(256) grouped_glds_kernel(const uint16_t* __restrict__ x, int ldx,
+                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                           int ldy, float* __restrict__ part,
+                                                           const int* __restrict__ offsets, int E, int N, int K,
+                                                           int kslice, int total_rows) {
+  __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<1, NB>()];
+  int j = blockIdx.y, e = 0, row0 = 0, rows = 0;
+  for (; e < E; ++e) {
+    const int a0 = offsets[e], a1 = offsets[e + 1];
+    const int t = (a1 - a0 + 63) / 64;
+    if (j < t) {
+      row0 = a0 + 64 * j;
+      rows = min(64, a1 - row0);
+      break;
+    }
+    j -= t;
   }
+  if (e >= E || rows <= 0) return;  // workgroup-uniform: before any DMA or barrier
+  const int n0 = blockIdx.x * kSBN, split = blockIdx.z, kbeg = split * kslice;
+  f32x4 acc[1][4];
+#pragma unroll
+  for (int cf = 0; cf < 4; ++cf) acc[0][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  glds_strip<1, NB>(x + (size_t)row0 * ldx + kbeg, ldx, rows, w + ((size_t)e * N + n0) * K + kbeg, K, kslice / kSC,
+                    sm, acc);
+  if (gridDim.z == 1)
+    glds_store<1>(acc, rows, y + (size_t)row0 * ldy + n0, ldy, nullptr, 0);
+  else
+    glds_store<1>(acc, rows, nullptr, 0, part + ((size_t)split * total_rows + row0) * N + n0, N);
 }
 
 // Y[m][n] = bf16(sum_s part[s][m][n]); 8 outputs per thread (M * N % 8 == 0).
@@ -411,4 +460,47 @@ K8S_API int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int 
 K8S_API int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                                  int splits, void* part, hipStream_t s) {
   return stream_launch(x, ldx, w, y, ldy, M, N, K, cfg, splits, part, false, s);
+}
+
+// MoE grouped GEMM on the LDS-DMA strip kernel (decode batches: every expert's
+// rows fit one or a few 64-row tiles).  cfg = 10 + NB (NB 3..6 stages);
+// max_tiles >= sum_e ceil(rows_e / 64) (ceil(total_rows / 64) + E always is);
+// splits > 1 needs `part` = splits * total_rows * N fp32 and reduces into y
+// unless reduce == 0.
+static int grouped_glds_launch(const void* x, int ldx, const void* w, void* y, int ldy, const int* offsets, int E,
+                               int N, int K, int max_tiles, int cfg, int splits, void* part, int total_rows,
+                               bool reduce, hipStream_t s) {
+  if (total_rows <= 0) return (int)hipSuccess;
+  if (E <= 0 || N % kSBN || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) || cfg < 13 ||
+      cfg > 16 || ldx % 8 || max_tiles <= 0 || (splits > 1 && ((size_t)total_rows * N) % 8))
+    return (int)hipErrorInvalidValue;
+  const int kslice = K / splits;
+  const dim3 grid(N / kSBN, max_tiles, splits);
+  const uint16_t* xx = (const uint16_t*)x;
+  const uint16_t* ww = (const uint16_t*)w;
+  uint16_t* yy = (uint16_t*)y;
+  float* pp = (float*)part;
+#define K8S_GG(NB)                                                                                               \
+  hipLaunchKernelGGL((grouped_glds_kernel<NB>), grid, dim3(256), 0, s, xx, ldx, ww, yy, ldy, pp, offsets, E, N, K, \
+                     kslice, total_rows)
+  switch (cfg) {
+    case 13: K8S_GG(3); break;
+    case 14: K8S_GG(4); break;
+    case 15: K8S_GG(5); break;
+    default: K8S_GG(6); break;
+  }
+#undef K8S_GG
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (splits > 1 && reduce) {
+    const int blocks = (int)(((size_t)total_rows * N / 8 + 255) / 256);
+    hipLaunchKernelGGL(gemm_stream_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, splits, yy, ldy,
+                       total_rows, N);
+  }
+  return (int)hipGetLastError();
+}
+
+K8S_API int k8s_grouped_glds(const void* x, int ldx, const void* w, void* y, int ldy, const int* offsets, int E, int N,
+                             int K, int max_tiles, int cfg, int splits, void* part, int total_rows, hipStream_t s) {
+  return grouped_glds_launch(x, ldx, w, y, ldy, offsets, E, N, K, max_tiles, cfg, splits, part, total_rows, true, s);
 }

@@ -74,6 +74,12 @@ class MoELayerSet:
     # 264 -> 305 / 485 -> 442 us at 1024 / 2048 rows with 2 slices
     DOWN_SPLITS = 2
     SPLIT_MAX_ROWS = 2048
+    # the LDS-DMA strip kernel (ops/moe.py grouped_gemm(glds=...)) for decode-
+    # sized batches: (cfg, splits) per projection, 0 = the grouped kernel
+    # (tools/bench_kernels.py --what moe_glds)
+    GLDS_MAX_ROWS = 0
+    GLDS_UP = (14, 1)
+    GLDS_DOWN = (14, 2)
 
     def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
         """Grouped SwiGLU over contiguous expert slices offsets[e]..offsets[e+1]
@@ -90,11 +96,15 @@ class MoELayerSet:
                     gu = lib_gemm(x_perm[a:b], self.w13[li][e])
                     lib_gemm(N.silu_mul(gu), self.w2[li][e], out=out[a:b])
             return out
+        rows = x_perm.shape[0]
+        if x_perm.is_cuda and rows <= self.GLDS_MAX_ROWS:
+            gu = M.grouped_gemm(x_perm, self.w13[li], offsets, glds=self.GLDS_UP[0], splits=self.GLDS_UP[1])
+            return M.grouped_gemm(N.silu_mul(gu), self.w2[li], offsets, glds=self.GLDS_DOWN[0],
+                                  splits=self.GLDS_DOWN[1])
         gu = M.grouped_gemm(x_perm, self.w13[li], offsets)
         # measured (tools/bench_kernels.py --what moe_split): silu_mul + the
         # un-fused down GEMM beats the SwiGLU-fused operand load (244 vs 287-305
         # us per layer at decode sizes), and splitting K (only 32 column tiles
         # per expert) fills the chip: 168-192 us
-        rows = x_perm.shape[0]
         splits = self.DOWN_SPLITS if rows <= self.SPLIT_MAX_ROWS else 1
         return M.grouped_gemm(N.silu_mul(gu), self.w2[li], offsets, splits=splits)

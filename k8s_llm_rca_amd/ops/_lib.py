@@ -36,6 +36,7 @@ _SIGS = {
     "k8s_gemm_mid_part": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_stream": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_stream_part": [P, I, P, P, I, I, I, I, I, I, P, P],
+    "k8s_grouped_glds": [P, I, P, P, I, P, I, I, I, I, I, I, P, I, P],
     "k8s_splitk_addnorm": [P, I, P, P, P, I, I, I, F, P],
     "k8s_gemm_mid_num_cfgs": [],
     "k8s_blaslt_gemm": [P, I, P, P, I, I, I, I, P, ctypes.c_size_t, P],

@@ -57,17 +57,27 @@ def combine(y_perm: torch.Tensor, inv: torch.Tensor, w: torch.Tensor, T: int, k:
 
 
 def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, fuse_silu: bool = False,
-                 out: Optional[torch.Tensor] = None, splits: int = 1) -> torch.Tensor:
+                 out: Optional[torch.Tensor] = None, splits: int = 1, glds: int = 0) -> torch.Tensor:
     """B13: rows offsets[e]..offsets[e+1] of ``a`` times ``w[e]^T`` for every
     expert in one launch (``w`` [E, N, K]).  ``fuse_silu``: ``a`` is the
     gate_up output [rows, 2K] and the activation silu(gate) * up is formed on
     the fly.  ``splits`` > 1 splits K over workgroups (fp32 partials + a
-    reduce; see grouped_gemm.hip).  Offsets stay on the device (no host sync)."""
+    reduce; see grouped_gemm.hip).  ``glds`` = 10 + NB runs the LDS-DMA strip
+    kernel with NB stages instead (64-row tiles: decode batches).  Offsets stay
+    on the device (no host sync)."""
     E, N, K = w.shape
     rows = a.shape[0]
     if out is None:
         out = torch.empty(rows, N, dtype=a.dtype, device=a.device)
     if rows == 0:
+        return out
+    if glds and use_hip(a) and not fuse_silu and N % 64 == 0 and K % (64 * splits) == 0:
+        # the LDS-DMA strip kernel (csrc/kernels/gemm_stream.hip grouped_glds_kernel)
+        assert a.dtype == torch.bfloat16 and w.is_contiguous() and a.stride(1) == 1 and out.is_contiguous()
+        max_tiles = (rows + 63) // 64 + E
+        part = _split_scratch(a.device, splits * rows * N) if splits > 1 else None
+        check(lib().k8s_grouped_glds(ptr(a), a.stride(0), ptr(w), ptr(out), out.stride(0), ptr(offsets), E, N, K,
+                                     max_tiles, glds, splits, ptr(part), rows, stream_ptr(a)), "grouped_glds")
         return out
     if use_hip(a) and N % 128 == 0 and K % (64 * splits) == 0:
         assert a.dtype == torch.bfloat16 and w.is_contiguous() and a.stride(1) == 1 and out.is_contiguous()

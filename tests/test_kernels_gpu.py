@@ -528,3 +528,24 @@ def test_gemm_stream_vs_fp32(M, N, K, splits, cfg):
     e[torch.arange(M, device=dev), idx] = 1.0
     ye = LIN.gemm_stream(e, w, cfg, splits)
     assert torch.equal(ye, w[:, idx].t().contiguous())
+
+
+@pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])
+@pytest.mark.parametrize("cfg", [13, 14, 16])
+@pytest.mark.parametrize("splits", [1, 2, 4])
+def test_grouped_glds_matches_per_expert(E, N, K, cfg, splits):
+    """The LDS-DMA strip kernel in its grouped form (gemm_stream.hip
+    grouped_glds_kernel): device offsets, empty experts, experts spanning
+    several 64-row tiles, split-K partials + reduce == per-expert fp32."""
+    from k8s_llm_rca_amd.ops import moe as MO
+    _need_gpu()
+    torch.manual_seed(6)
+    counts = torch.tensor([0, 70, 1, 130, 64, 0, 5, 200][:E])
+    offs = torch.zeros(E + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(counts, 0)
+    rows = int(offs[-1])
+    a = (torch.randn(rows, K) * 0.5).bfloat16()
+    w = (torch.randn(E, N, K) / K ** 0.5).bfloat16()
+    got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), splits=splits, glds=cfg).float().cpu()
+    ref = MO.grouped_gemm(a, w, offs).float()
+    torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)

@@ -224,6 +224,38 @@ def main():
                 + " ".join(f"x{z} {t:.0f}" for z, t in sp13.items())
                 + f" | w2 fused {t2f:.0f}us | silu {tsl:.0f}us + w2 {t2u:.0f}us "
                 f"({w2.numel() * 2 / t2u / 1e6:.2f} TB/s) " + " ".join(f"x{z} {t:.0f}" for z, t in sp.items()))
+    if args.what == "moe_glds":  # Mixtral expert GEMMs: grouped kernel vs the LDS-DMA strip kernel
+        from k8s_llm_rca_amd.ops import moe as MO
+        E, H, I = 8, 4096, 14336
+        w13 = (torch.randn(E, 2 * I, H, device=dev) * 0.02).bfloat16()
+        w2 = (torch.randn(E, H, I, device=dev) * 0.02).bfloat16()
+        for rows in (64, 128, 250, 512):
+            g = torch.Generator().manual_seed(rows)
+            counts = torch.bincount(torch.randint(0, E, (rows,), generator=g), minlength=E)
+            offs = torch.zeros(E + 1, dtype=torch.int32)
+            offs[1:] = torch.cumsum(counts, 0)
+            offs_d = offs.to(dev)
+            x = torch.randn(rows, H, device=dev).bfloat16()
+            act = torch.randn(rows, I, device=dev).bfloat16()
+            ref13, ref2 = MO.grouped_gemm(x, w13, offs_d), MO.grouped_gemm(act, w2, offs_d, splits=2)
+            line = []
+            for name, wt, inp, ref, base in (("w13", w13, x, ref13, dict()), ("w2", w2, act, ref2, dict(splits=2))):
+                tb = timeit(lambda: MO.grouped_gemm(inp, wt, offs_d, **base), iters=10)
+                best = (tb, "grouped")
+                for cfg in (13, 14, 15, 16):
+                    for z in (1, 2, 4):
+                        if (wt.shape[2] // z) % 64:
+                            continue
+                        y = MO.grouped_gemm(inp, wt, offs_d, splits=z, glds=cfg)
+                        err = (y.float() - ref.float()).abs().max().item() / (ref.float().abs().max().item() + 1e-6)
+                        if err > 2e-2:
+                            line.append(f"!!{name} glds{cfg}x{z} err {err:.2e}")
+                            continue
+                        t = timeit(lambda: MO.grouped_gemm(inp, wt, offs_d, splits=z, glds=cfg), iters=10)
+                        best = min(best, (t, f"glds{cfg}x{z}"))
+                line.append(f"{name} grouped {tb:.0f}us ({wt.numel() * 2 / tb / 1e6:.2f} TB/s) best {best[1]} "
+                            f"{best[0]:.0f}us ({wt.numel() * 2 / best[0] / 1e6:.2f} TB/s)")
+            res[f"moe_glds rows{rows}"] = " | ".join(line)
     if args.what == "gemm_big":
         for M in (512, 1024, 2048, 4096, 8192):
             for (n, k) in [(6144, 4096), (4096, 4096), (28672, 4096), (4096, 14336)]:

@@ -11,6 +11,8 @@ on ``E / ep`` ranks and tokens travel by all-to-all (:mod:`..parallel.ep`).
 """
 from __future__ import annotations
 
+import os
+
 from typing import List, Optional
 
 import torch
@@ -74,12 +76,13 @@ class MoELayerSet:
     # 264 -> 305 / 485 -> 442 us at 1024 / 2048 rows with 2 slices
     DOWN_SPLITS = 2
     SPLIT_MAX_ROWS = 2048
-    # the LDS-DMA strip kernel (ops/moe.py grouped_gemm(glds=...)) for decode-
-    # sized batches: (cfg, splits) per projection, 0 = the grouped kernel
-    # (tools/bench_kernels.py --what moe_glds)
-    GLDS_MAX_ROWS = 0
-    GLDS_UP = (14, 1)
-    GLDS_DOWN = (14, 2)
+    # gate_up on the LDS-DMA strip kernel (ops/moe.py grouped_gemm(glds=...))
+    # for decode-sized batches, (cfg, splits): 343-365 vs 383-391 us per layer
+    # at 64-250 rows (5.2-5.5 TB/s); the down projection measured equal to the
+    # split-K grouped kernel and stays there; at 512 rows the grouped kernel wins
+    # (tools/bench_kernels.py --what moe_glds, profiles/r2_moe_glds.txt)
+    GLDS_MAX_ROWS = int(os.environ.get("K8S_MOE_GLDS_MAX_ROWS", "384"))  # 0 disables (A/B)
+    GLDS_UP = (13, 1)
 
     def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
         """Grouped SwiGLU over contiguous expert slices offsets[e]..offsets[e+1]
@@ -99,9 +102,8 @@ class MoELayerSet:
         rows = x_perm.shape[0]
         if x_perm.is_cuda and rows <= self.GLDS_MAX_ROWS:
             gu = M.grouped_gemm(x_perm, self.w13[li], offsets, glds=self.GLDS_UP[0], splits=self.GLDS_UP[1])
-            return M.grouped_gemm(N.silu_mul(gu), self.w2[li], offsets, glds=self.GLDS_DOWN[0],
-                                  splits=self.GLDS_DOWN[1])
-        gu = M.grouped_gemm(x_perm, self.w13[li], offsets)
+        else:
+            gu = M.grouped_gemm(x_perm, self.w13[li], offsets)
         # measured (tools/bench_kernels.py --what moe_split): silu_mul + the
         # un-fused down GEMM beats the SwiGLU-fused operand load (244 vs 287-305
         # us per layer at decode sizes), and splitting K (only 32 column tiles

@@ -30,6 +30,8 @@ def main():
     steps = [s for s in steps if s]
     g = torch.Generator().manual_seed(0)
     idx = torch.randperm(len(steps), generator=g)[: a.samples].tolist()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    tot_ms = 0.0
     for i in idx:
         ctx = [c for c, q in steps[i]]
         ql = [q for c, q in steps[i]]
@@ -39,10 +41,14 @@ def main():
         T = sum(ql)
         q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
         out = torch.empty(T, nq * 128, device=dev).bfloat16()
+        A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out)
+        e0.record()
         for _ in range(a.iters):
             A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out)
-    torch.cuda.synchronize()
-    print("ok", len(idx))
+        e1.record()
+        torch.cuda.synchronize()
+        tot_ms += e0.elapsed_time(e1) / a.iters
+    print(f"ok {len(idx)} steps, q in [{a.min_q}, {a.max_q or 'inf'}]: {tot_ms * 1e3 / len(idx):.1f} us per step")
 
 
 if __name__ == "__main__":

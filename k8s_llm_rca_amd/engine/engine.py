@@ -105,6 +105,11 @@ class EngineConfig:
     # (profiles/r1_blaslt_tune_8b.txt)
     tune_lib_gemms: bool = field(default_factory=lambda: os.environ.get("K8SRCA_BLASLT_TUNE", "0") == "1")
     max_decode_seqs: int = 256
+    # prefill chunks of at most this many tokens (grammar jump-forward runs) are
+    # run as rows of the decode-attention work list (one row per token, its own
+    # causal key count) instead of a prefill tile that walks every page for a
+    # few rows and then needs a split-KV merge; 0 disables
+    tiny_chunk_tokens: int = field(default_factory=lambda: int(os.environ.get("K8S_TINY_CHUNK_TOKENS", "8")))
     max_context: Optional[int] = None
     use_graphs: bool = True
     # overlap the host's token processing of step n with the GPU's forward of
@@ -271,7 +276,8 @@ class LLMEngine:
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
                       "prefix_hit_tokens": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0,
-                      "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0}
+                      "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
+                      "tiny_chunk_tokens": 0}
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
 
@@ -621,11 +627,18 @@ class LLMEngine:
             if young:
                 self._fail_req(young[-1].req, "KV pool exhausted")
             return True
-        rows = [(s, 1) for s in decode] + chunks
+        tiny = [(s, q) for s, q in chunks if q <= self.cfg.tiny_chunk_tokens]
+        big = [(s, q) for s, q in chunks if q > self.cfg.tiny_chunk_tokens]
+        if len(decode) + sum(q for _, q in tiny) > max(self.cfg.max_decode_seqs, 1):
+            tiny, big = [], chunks
+        # decode-attention rows (sequence, token offset past n_cached): the decode
+        # rows, then every token of the tiny chunks; token order = decode, tiny, big
+        drows = [(s, 0) for s in decode] + [(s, j) for s, q in tiny for j in range(q)]
+        rows = [(s, 1) for s in decode] + tiny + big
         if self._shape_trace:
             with open(self._shape_trace, "a") as f:
-                f.write(json.dumps({"d": [s.n_cached + 1 for s in decode],
-                                    "p": [[s.n_cached + q, q] for s, q in chunks]}) + "\n")
+                f.write(json.dumps({"d": [s.n_cached + j + 1 for s, j in drows],
+                                    "p": [[s.n_cached + q, q] for s, q in big]}) + "\n")
         sample_rows = []  # (row index in batch, seq)
         off = 0
         for s, q in rows:
@@ -639,12 +652,12 @@ class LLMEngine:
             # its first kernel: the GPU goes sample(k) -> forward(k+1) with no
             # host packing time between them
             pos_in = {s.id: j for j, s in enumerate(ps[1])}
-            src = np.array([pos_in.get(s.id, -1) if s.tokens[s.n_cached] == SPEC else -1 for s in decode],
-                           dtype=np.int32)
+            src = np.array([pos_in.get(s.id, -1) if s.tokens[s.n_cached] == SPEC else -1 for s in decode]
+                           + [-1] * (len(drows) - len(decode)), dtype=np.int32)
             lazy = _LazySample(self, ps)
             spec = (src, lazy)
         self.stats["host_s"] += time.perf_counter() - t_host0
-        logits = self._forward(decode, chunks, [i for i, _ in sample_rows], spec)
+        logits = self._forward(drows, big, [i for i, _ in sample_rows], spec)
         infl = lazy.launch() if lazy is not None else None
         spec_pos = {}
         for s, q in rows:
@@ -657,6 +670,7 @@ class LLMEngine:
                 self._register_blocks(s)
         self.stats["steps"] += 1
         self.stats["prefill_tokens"] += sum(q for _, q in chunks)
+        self.stats["tiny_chunk_tokens"] += len(drows) - len(decode)
         self.stats["decode_tokens"] += len(decode)
         self.stats["decode_ctx_tokens"] += sum(s.n_cached for s in decode)
         self.stats["prefill_ctx_tokens"] += sum(s.n_cached * q for s, q in chunks)
@@ -750,6 +764,9 @@ class LLMEngine:
 
     def _token_arrays(self, rows: List[Tuple[Sequence, int]]):
         BS = self.kv.block_size
+        if not rows:
+            e = np.zeros(0, np.int32)
+            return e, e, e
         ids, pos, slots = [], [], []
         for s, q in rows:
             a = s.n_cached
@@ -761,8 +778,33 @@ class LLMEngine:
         return (np.asarray(ids, dtype=np.int32), np.concatenate(pos).astype(np.int32),
                 np.concatenate(slots).astype(np.int32))
 
-    def _forward(self, decode: List[Sequence], chunks: List[Tuple[Sequence, int]], sample_idx: List[int],
-                 spec=None):
+    def _decode_token_arrays(self, drows: List[Tuple[Sequence, int]]):
+        BS = self.kv.block_size
+        n = len(drows)
+        ids = np.empty(n, np.int32)
+        pos = np.empty(n, np.int32)
+        slots = np.empty(n, np.int32)
+        for i, (s, j) in enumerate(drows):
+            p = s.n_cached + j
+            ids[i] = s.tokens[p]
+            pos[i] = p
+            slots[i] = s.blocks[p // BS] * BS + p % BS
+        return ids, pos, slots
+
+    def _decode_meta(self, drows: List[Tuple[Sequence, int]]):
+        """Block tables / context lengths / q_start of decode-attention rows:
+        row (s, j) is the token at n_cached + j and sees keys 0..n_cached + j."""
+        n = len(drows)
+        maxb = max(len(s.blocks) for s, _ in drows)
+        bt = np.zeros((n, maxb), dtype=np.int32)
+        ctx = np.zeros(n, dtype=np.int32)
+        for i, (s, j) in enumerate(drows):
+            bt[i, : len(s.blocks)] = s.blocks
+            ctx[i] = s.n_cached + j + 1
+        return bt, ctx, np.arange(n + 1, dtype=np.int32)
+
+    def _forward(self, decode: List[Tuple[Sequence, int]], chunks: List[Tuple[Sequence, int]],
+                 sample_idx: List[int], spec=None):
         """``spec`` = (src[nd], tok): decode row i takes its input id from the
         device tensor ``tok[src[i]]`` when ``src[i] >= 0`` (tokens sampled by
         the in-flight step, not yet on the host)."""
@@ -775,7 +817,7 @@ class LLMEngine:
             _spec_tok(spec)  # TP: sample(k) -- a message + an all-gather -- goes before forward(k+1) on every rank
         if (not chunks and self.cfg.use_graphs and self.device.type == "cuda" and decode and self._graphs_ok()
                 and self.kv.block_size % 64 == 0):
-            out = self._forward_graph(decode, spec)
+            out = self._forward_graph(decode, spec, sample_idx)
             self.stats["graph_steps"] += 1
             self.stats["decode_steps"] += 1
             kind = "graph"
@@ -833,14 +875,16 @@ class LLMEngine:
     HDR = 14
 
     def _pack_step(self, decode, chunks, sample_idx):
-        rows = [(s, 1) for s in decode] + list(chunks)
-        ids, pos, slots = self._token_arrays(rows)
+        """``decode``: decode-attention rows (sequence, token offset past n_cached)."""
+        ids_d, pos_d, slots_d = self._decode_token_arrays(decode)
+        ids, pos, slots = self._token_arrays(list(chunks))
+        ids, pos, slots = np.concatenate([ids_d, ids]), np.concatenate([pos_d, pos]), np.concatenate([slots_d, slots])
         arrays = [ids, pos, slots, np.asarray(sample_idx, dtype=np.int32)]
         nd = len(decode)
         maxb_d = maxb_p = n_tiles = n_merge = n_items = 0
         n_parts, part = 1, PART_MIN
         if decode:
-            bt_d, ctx_d, qs_d = self._meta_arrays([(s, 1) for s in decode])
+            bt_d, ctx_d, qs_d = self._decode_meta(decode)
             maxb_d = bt_d.shape[1]
             n_parts, part = A.plan_decode_split(ctx_d, self.model.nkv)
             arrays += [bt_d, ctx_d, qs_d]
@@ -1052,10 +1096,10 @@ class LLMEngine:
                 spec = (arrs[2], self._last_tok) if len(arrs) > 2 else None
                 logits = self._run_eager(arrs[0], arrs[1], spec)
             elif kind == FWD_GRAPH:
-                meta, flat = arrs[0], arrs[1]
-                spec = (arrs[2], self._last_tok) if len(arrs) > 2 else None
+                meta, flat, sel = arrs[0], arrs[1], arrs[2]
+                spec = (arrs[3], self._last_tok) if len(arrs) > 3 else None
                 logits = self._graph_run(int(meta[0]), int(meta[1]), int(meta[2]), int(meta[3]), int(meta[4]),
-                                         flat, spec)
+                                         flat, spec, sel)
             else:
                 raise RuntimeError(f"unknown step message {kind}")
 
@@ -1146,12 +1190,17 @@ class LLMEngine:
         self.stats["capture_s"] += time.perf_counter() - t0
         return self._graphs[key]
 
-    def _forward_graph(self, decode: List[Sequence], spec=None):
+    def _forward_graph(self, decode: List[Tuple[Sequence, int]], spec=None, sample_idx: Optional[List[int]] = None):
+        """``decode``: decode-attention rows (sequence, token offset past
+        n_cached); the logits of the ``sample_idx`` rows are returned (all rows
+        when every row samples)."""
         st = self._ensure_static()
         B = len(decode)
+        if sample_idx is None:
+            sample_idx = list(range(B))
         Bb = self._bucket(B)
         if Bb > max(self.cfg.graph_batch_sizes):
-            return self._forward_eager(decode, [], list(range(B)), spec)
+            return self._forward_eager(decode, [], sample_idx, spec)
         BS = self.kv.block_size
         mb = self.max_blocks_per_seq
         ctx = np.ones(Bb, dtype=np.int32)
@@ -1159,8 +1208,8 @@ class LLMEngine:
         pos = np.zeros(Bb, dtype=np.int32)
         slots = np.full(Bb, -1, dtype=np.int32)
         bt = np.zeros((Bb, mb), dtype=np.int32)
-        for i, s in enumerate(decode):
-            p = s.n_cached
+        for i, (s, j) in enumerate(decode):
+            p = s.n_cached + j
             ids[i] = s.tokens[p]
             pos[i] = p
             slots[i] = s.blocks[p // BS] * BS + p % BS
@@ -1170,7 +1219,7 @@ class LLMEngine:
         # (sorted last) so every output row the graph produces is finite
         _, part = A.plan_decode_split(ctx[:B], self.model.nkv)
         if self.stats["graph_steps"] % 32 == 0:  # how often decode attention re-reads a shared KV block
-            used = np.concatenate([s.blocks[: (s.n_cached + BS) // BS] for s in decode])
+            used = np.concatenate([s.blocks[: (s.n_cached + j + BS) // BS] for s, j in decode])
             self.stats["kv_read_blocks_sampled"] += used.size
             self.stats["kv_unique_blocks_sampled"] += np.unique(used).size
         items = A.build_decode_items(ctx, np.arange(Bb), part)
@@ -1178,13 +1227,15 @@ class LLMEngine:
         assert n_items <= self._max_items
         flat = np.concatenate([ids, pos, slots, ctx, bt.reshape(-1), np.array([n_items, part], np.int32),
                                items.reshape(-1).astype(np.int32)])
+        sel = np.asarray(sample_idx if len(sample_idx) != B else [], dtype=np.int32)
         if self._chan is not None:
             from ..parallel.channel import FWD_GRAPH
             meta = np.array([B, Bb, part, n_items, mb], dtype=np.int32)
-            self._chan.send(FWD_GRAPH, [meta, flat] + ([spec[0]] if spec is not None else []))
-        return self._graph_run(B, Bb, part, n_items, mb, flat, spec)
+            self._chan.send(FWD_GRAPH, [meta, flat, sel] + ([spec[0]] if spec is not None else []))
+        return self._graph_run(B, Bb, part, n_items, mb, flat, spec, sel)
 
-    def _graph_run(self, B: int, Bb: int, part: int, n_items: int, mb: int, flat: np.ndarray, spec=None):
+    def _graph_run(self, B: int, Bb: int, part: int, n_items: int, mb: int, flat: np.ndarray, spec=None,
+                   sel: Optional[np.ndarray] = None):
         """Upload a packed decode step into the static graph inputs (pinned
         staging, one async copy) and replay bucket ``Bb``'s graph (rank 0, and
         every TP worker from the channel's message).  ``spec`` = (src[B], tok):
@@ -1203,6 +1254,11 @@ class LLMEngine:
             hv[n:n + B] = spec[0]
             n_src = n
             n += B
+        n_sel = 0 if sel is None else sel.size
+        if n_sel:  # rows that sample (tiny-chunk rows other than a chunk's last do not)
+            hv[n:n + n_sel] = sel
+            o_sel = n
+            n += n_sel
         dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
         dev_flat.copy_(host[:n], non_blocking=True)
         ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event()
@@ -1218,6 +1274,8 @@ class LLMEngine:
             self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], _spec_tok(spec))
         graph, out = self._capture(Bb, part)  # one graph per bucket: the plan's part size is read on the device
         graph.replay()
+        if n_sel:
+            return out.index_select(0, dev_flat[o_sel:o_sel + n_sel].long())
         return out[:B]
 
     # ------------------------------------------------------------ sampling

@@ -427,3 +427,32 @@ def test_service_wait_timeout_cancels_engine_request():
         assert a.wait_get_last_k_message(1, timeout=60) is not None
     finally:
         eng.stop()
+
+
+def test_tiny_chunks_as_decode_rows_match_prefill_path():
+    """Short prefill chunks (grammar jump-forward literals, short follow-up
+    messages) run as decode-attention rows -- one row per token with its own
+    causal key count -- and generate what the prefill path generates (greedy,
+    fp32), including a chunk's last row feeding the sampler."""
+    outs, tiny = [], []
+    for t in (0, 64):  # 64: every prompt / follow-up chunk of this toy tokenizer runs as decode rows
+        eng = _engine(temperature=0.0, tiny_chunk_tokens=t, num_blocks=128)
+        res = {}
+        for i in range(6):
+            sid = eng.new_sequence()
+            g = Grammar([Lit('{"k": '), Choice(['"aa"', '"b"', '"cccc"'], "c"), Lit(', "t": "'),
+                         Free(4 + i, name="t"), Lit('"}')]) if i % 2 else None
+            p = eng.tok.system_prefix("s") + eng.tok.message("user", "req %d " % i * (3 + 4 * i)) + \
+                eng.tok.header("assistant")
+            eng.submit(sid, p, g, 6 + 3 * i, temperature=0.0, on_done=lambda gen, st, i=i: res.__setitem__(i, gen))
+        eng.run_until_idle()
+        for i, sid in enumerate(list(eng.seqs)):
+            s = eng.seqs[sid]
+            eng.submit(sid, s.tokens + eng.tok.message("user", "m%d" % i) + eng.tok.header("assistant"),
+                       None, 5, temperature=0.0, on_done=lambda gen, st, i=i: res.__setitem__(100 + i, gen))
+        eng.run_until_idle()
+        assert len(res) == 12
+        outs.append(res)
+        tiny.append(eng.stats["tiny_chunk_tokens"])
+    assert tiny[0] == 0 and tiny[1] > 0
+    assert outs[0] == outs[1]

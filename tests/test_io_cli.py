@@ -80,7 +80,7 @@ def test_bench_dp2_torchrun_cpu_contract(tmp_path):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2", "--master-addr",
            "127.0.0.1", "--master-port", str(port), os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "1",
            "--warmup", "0", "--device", "cpu", "--model", "tiny-llama", "--incidents", "2", "--graph-nodes", "300",
-           "--quantum", "1", "--no-hints-steps", "0"]
+           "--quantum", "1", "--no-hints-steps", "0", "--time-budget", "0"]
     env = dict(os.environ, PYTHONPATH=root, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
     assert r.returncode == 0, r.stderr[-3000:]
@@ -101,7 +101,7 @@ def test_bench_self_spawns_ranks_cpu(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "2", "--warmup", "1",
            "--quantum", "1", "--device", "cpu", "--model", "tiny-llama", "--incidents", "2", "--graph-nodes", "300",
-           "--no-hints-steps", "0"]
+           "--no-hints-steps", "0", "--time-budget", "0"]  # no budget: a loaded CI box must not truncate
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(PYTHONPATH=root, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))
@@ -155,7 +155,7 @@ def test_bench_tp2_cpu(tmp_path):
     root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
     cmd = [sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--tp", "2", "--steps", "2", "--warmup", "1",
            "--quantum", "1", "--device", "cpu", "--model", "tiny-llama-g8", "--incidents", "2", "--graph-nodes", "300",
-           "--no-hints-steps", "0"]
+           "--no-hints-steps", "0", "--time-budget", "0"]
     env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
     env.update(PYTHONPATH=root, OMP_NUM_THREADS="2")
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=900, env=env, cwd=str(tmp_path))

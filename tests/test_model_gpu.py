@@ -164,3 +164,32 @@ def test_layer_executor_bit_identical(graphs, splitk):
     assert len(l0) == len(l1) and len(l0) > 2
     for a, b in zip(l0, l1):
         assert torch.equal(a, b)
+
+
+@pytest.mark.parametrize("graphs", [False, True])
+def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
+    """A short prefill chunk run as decode-attention rows (one row per token,
+    each with its own causal key count; the HIP-graph decode path when the
+    step has no other chunk) gives the logits of the prefill-attention path."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=64, use_graphs=graphs,
+                                 temperature=0.0, graph_batch_sizes=(1, 2, 4, 8, 16)))
+    g = torch.Generator().manual_seed(3)
+    outs = []
+    for n0, q in ((40, 6), (63, 5), (64, 8)):  # chunks that stay in a page / cross a page boundary
+        s = eng.seqs[eng.new_sequence()]
+        s.tokens = torch.randint(5, 1000, (n0 + q,), generator=g).tolist()
+        assert eng._ensure_blocks(s, n0 + q, set())
+        eng._forward([], [(s, n0)], [n0 - 1])
+        s.n_cached = n0
+        big = eng._forward([], [(s, q)], list(range(q))).float()
+        rows = eng._forward([(s, j) for j in range(q)], [], list(range(q))).float()
+        torch.cuda.synchronize()
+        err = (big - rows).abs().max().item() / big.abs().max().item()
+        assert err < 3e-2, (n0, q, err)
+        assert (big.argmax(-1) == rows.argmax(-1)).float().mean().item() >= 0.8
+        outs.append(err)
+    if graphs:
+        assert eng.stats["graph_steps"] == 3

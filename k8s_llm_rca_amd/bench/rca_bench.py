@@ -33,6 +33,26 @@ METRIC = "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-nod
 REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
 
 
+def _thread_cpu() -> Dict[str, float]:
+    """CPU seconds per thread group of this process (engine / graph batcher /
+    RCA pipelines / other): which Python threads compete with the engine
+    thread for the interpreter lock over the timed window."""
+    import threading
+    try:
+        import psutil
+        per = {t.id: t.user_time + t.system_time for t in psutil.Process().threads()}
+    except Exception:
+        return {}
+    names = {t.native_id: t.name for t in threading.enumerate()}
+    out: Dict[str, float] = {}
+    for tid, cpu in per.items():
+        n = names.get(tid, "other")
+        g = "engine" if n == "llm-engine" else "graph_batcher" if n == "graph-batcher" else \
+            "pipelines" if n == "rca-stream" else "main" if n == "MainThread" else "other"
+        out[g] = out.get(g, 0.0) + cpu
+    return out
+
+
 def _dist_init():
     import torch.distributed as dist
 
@@ -169,10 +189,12 @@ def run(args) -> Optional[Dict[str, Any]]:
     stats0 = dict(eng.stats)
     eng.kv.reset_peak()
     t_wall0 = time.time()
+    cpu0 = _thread_cpu()
     t0 = time.perf_counter()
     base = stream.n_ok
     done_all = stream.wait_ok(base + n_steps * quantum, deadline, _poll)
     t_end = time.perf_counter()
+    cpu1 = _thread_cpu()
     n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
@@ -269,6 +291,8 @@ def run(args) -> Optional[Dict[str, Any]]:
             "runs": len(ttft),
             "ttft_p50_s": round(ttft[len(ttft) // 2], 4) if ttft else None,
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
+        # CPU seconds per thread group over the timed window (GIL competition with the engine thread)
+        "host_cpu_s": {k: round(v - cpu0.get(k, 0.0), 2) for k, v in cpu1.items()},
         "setup_s": round(setup_s, 1),
         "wall_s": round(time.perf_counter() - t_start, 1),
         "clean_shutdown": clean,

@@ -213,8 +213,11 @@ __device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a
 // `blkv`: lane j holds the block id of the partition's j-th page (fetched
 // once per work item: a per-chunk block-table load would put a dependent
 // memory latency in front of every chunk's K/V loads).
+// `k1`: end key of the item (wave-uniform); `lim`: this lane's row sees keys
+// < lim (== k1 except for the earlier tokens of a multi-token item);
+// `kmin`: the smallest row limit of the wave (tail masking starts there).
 __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a, int blkv, int kvh, int k0,
-                                                int k1, int lane) {
+                                                int k1, int kmin, int lim, int lane) {
   const int h = lane >> 4;
   const int nch = (k1 - k0 + 63) >> 6;
   const int pg0 = k0 / a.BS;
@@ -240,14 +243,14 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
       }
     dec_load_k(kf, a, bn, kvh, kbn, lane);
     float cmax = -INFINITY;
-    if (kb + 64 > k1) {  // tail chunk: keys >= k1 are not part of this partition
+    if (kb + 64 > kmin) {  // tail chunk: keys >= the row's limit are not visible to it
 #pragma unroll
       for (int u = 0; u < 2; ++u)
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
           for (int i = 0; i < 4; ++i)
-            if (kb + 32 * u + 8 * h + 4 * t + i >= k1) sc[u][t][i] = -INFINITY;
+            if (kb + 32 * u + 8 * h + 4 * t + i >= lim) sc[u][t][i] = -INFINITY;
     }
 #pragma unroll
     for (int u = 0; u < 2; ++u)
@@ -362,8 +365,10 @@ __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
 // LPT scheduling, and no wave is ever launched for an empty partition (a
 // (seq, parts) grid with the partition count of the longest sequence spent
 // most of its waves on nothing when context lengths vary 1k..6k).
+// MFMA row rho = qi * G + g: token qi of the item (decode row seq + qi, q row
+// qrow + qi), q head g of the kv group.
 __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnArgs& a, int seq, int part, int qrow,
-                                                int kvh, bool whole, int lane) {
+                                                int kvh, bool whole, int nt, int lane) {
   const int r = lane & 15, h = lane >> 4;
   float l = st.l + __shfl_xor(st.l, 16, 64);
   l += __shfl_xor(l, 32, 64);
@@ -376,15 +381,16 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
     const int row = 4 * h + i;
-    if (row >= a.G) continue;
-    const int qh = kvh * a.G + row;
+    if (row >= nt * a.G) continue;
+    const int qi = row / a.G;
+    const int qh = kvh * a.G + (row - qi * a.G);
     if (whole) {
       const float inv = lr[i] > 0.f ? 1.f / lr[i] : 0.f;
-      uint16_t* dst = a.out + (size_t)qrow * a.out_stride + qh * D;
+      uint16_t* dst = a.out + (size_t)(qrow + qi) * a.out_stride + qh * D;
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) dst[16 * dt + r] = f2bf(st.o[dt][i] * inv);
     } else {
-      const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts + part;
+      const size_t base = ((size_t)(seq + qi) * a.nq + qh) * a.n_parts + part;
       float* po = a.part_o + base * D;
 #pragma unroll
       for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
@@ -404,21 +410,30 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
   const int n_items = a.d_n_items ? __builtin_amdgcn_readfirstlane(a.d_n_items[0]) : a.n_items;
   const int part_size = a.d_n_items ? __builtin_amdgcn_readfirstlane(a.d_n_items[1]) : a.part_size;
   const int total = n_items * a.nkv;
-  const bool valid = r < a.G;
   for (int w = blockIdx.x; w < total; w += gridDim.x) {
     const int it = w / a.nkv, kvh = w - it * a.nkv;
     const int4 item = a.items[it];
-    const int seq = item.x, k1 = item.z, qrow = item.w;
+    // item.w = q row | (tokens - 1) << 24: a multi-token item holds up to 16 / G
+    // consecutive tokens of one sequence (decode rows seq .. seq + nt - 1, one
+    // block table) in the MFMA's 16 rows, so their shared keys are read ONCE
+    const int seq = item.x, k1 = item.z, qrow = item.w & 0xFFFFFF, nt = (item.w >> 24) + 1;
     const bool whole = item.y < 0;
     const int part = whole ? 0 : item.y;
     const int k0 = part * part_size;
     const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
     const int pg0 = k0 / a.BS, npg = (k1 - 1) / a.BS - pg0 + 1;
     const int blkv = lane < npg ? bt[pg0 + lane] : 0;
+    const int qi = r / a.G;
+    const bool valid = qi < nt;
+    int lim = k1, kmin = k1;
+    if (nt > 1) {  // token qi sees keys < its own context length
+      lim = min(k1, a.ctx_lens[seq + min(qi, nt - 1)]);
+      kmin = min(k1, __builtin_amdgcn_readfirstlane(a.ctx_lens[seq]));
+    }
     RowState st;
-    init_state(st, a, qrow, kvh * a.G + (valid ? r : 0), valid, lane);
-    decode_stream64(st, a, blkv, kvh, k0, k1, lane);
-    decode_epilogue(st, a, seq, part, qrow, kvh, whole, lane);
+    init_state(st, a, qrow + (valid ? qi : 0), kvh * a.G + (valid ? r - qi * a.G : 0), valid, lane);
+    decode_stream64(st, a, blkv, kvh, k0, k1, kmin, lim, lane);
+    decode_epilogue(st, a, seq, part, qrow, kvh, whole, nt, lane);
   }
 }
 

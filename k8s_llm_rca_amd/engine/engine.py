@@ -249,6 +249,10 @@ class LLMEngine:
         self._graph_pool = None
         self._static = None
         self._pf_ws = None  # prefill split-KV partials (allocated on first split step)
+        # multi-token decode items (a short chunk's tokens read their shared keys
+        # once): the decode MFMA's 16 rows hold G q heads per token
+        G = getattr(self.model, "nq", 1) // max(1, getattr(self.model, "nkv", 1))
+        self._dec_gmax = max(1, 16 // G) if A.DECODE_GROUP_TOKENS and G <= 16 else 1
         self._pending_sample = None  # (logits, seqs, rows): sampled at the start of the next step
         # TP: the leader's host work of step n overlaps step n+1 on every rank too
         # (the workers take the sampled tokens from their own device copy)
@@ -791,6 +795,24 @@ class LLMEngine:
             slots[i] = s.blocks[p // BS] * BS + p % BS
         return ids, pos, slots
 
+    def _decode_chain(self, drows: List[Tuple[Sequence, int]]) -> Optional[np.ndarray]:
+        """chain[i]: decode row i is the token after row i-1's (same sequence):
+        such rows share multi-token decode-attention items.  None when no row
+        continues its predecessor (plain decode steps)."""
+        if self._dec_gmax <= 1 or len(drows) == len(set(id(s) for s, _ in drows)):
+            return None
+        ch = np.zeros(len(drows), dtype=bool)
+        for i in range(1, len(drows)):
+            ch[i] = drows[i][0] is drows[i - 1][0] and drows[i][1] == drows[i - 1][1] + 1
+        return ch
+
+    def _plan_ctx(self, ctx: np.ndarray, chain: Optional[np.ndarray]) -> np.ndarray:
+        """Context lengths the split planner sees: one per multi-token item."""
+        if chain is None:
+            return ctx
+        lead, nt = A.decode_groups(ctx, np.arange(ctx.size), chain, self._dec_gmax)
+        return ctx[lead + nt - 1]
+
     def _decode_meta(self, drows: List[Tuple[Sequence, int]]):
         """Block tables / context lengths / q_start of decode-attention rows:
         row (s, j) is the token at n_cached + j and sees keys 0..n_cached + j."""
@@ -886,10 +908,12 @@ class LLMEngine:
         if decode:
             bt_d, ctx_d, qs_d = self._decode_meta(decode)
             maxb_d = bt_d.shape[1]
-            n_parts, part = A.plan_decode_split(ctx_d, self.model.nkv)
+            chain = self._decode_chain(decode)
+            n_parts, part = A.plan_decode_split(self._plan_ctx(ctx_d, chain), self.model.nkv)
+            n_parts = max(n_parts, -(-int(ctx_d.max()) // part))
             arrays += [bt_d, ctx_d, qs_d]
             if self.kv.block_size % 64 == 0:
-                items = A.build_decode_items(ctx_d, np.arange(nd), part)
+                items = A.build_decode_items(ctx_d, np.arange(nd), part, chain, self._dec_gmax)
                 n_items = items.shape[0]
                 arrays.append(items)
             else:
@@ -1217,12 +1241,15 @@ class LLMEngine:
             bt[i, : len(s.blocks)] = s.blocks
         # plan on the real rows; padded rows (ctx 1) still get a one-key item
         # (sorted last) so every output row the graph produces is finite
-        _, part = A.plan_decode_split(ctx[:B], self.model.nkv)
+        chain = self._decode_chain(decode)
+        _, part = A.plan_decode_split(self._plan_ctx(ctx[:B], chain), self.model.nkv)
         if self.stats["graph_steps"] % 32 == 0:  # how often decode attention re-reads a shared KV block
             used = np.concatenate([s.blocks[: (s.n_cached + j + BS) // BS] for s, j in decode])
             self.stats["kv_read_blocks_sampled"] += used.size
             self.stats["kv_unique_blocks_sampled"] += np.unique(used).size
-        items = A.build_decode_items(ctx, np.arange(Bb), part)
+        if chain is not None:
+            chain = np.concatenate([chain, np.zeros(Bb - B, dtype=bool)])
+        items = A.build_decode_items(ctx, np.arange(Bb), part, chain, self._dec_gmax)
         n_items = items.shape[0]
         assert n_items <= self._max_items
         flat = np.concatenate([ids, pos, slots, ctx, bt.reshape(-1), np.array([n_items, part], np.int32),

@@ -131,6 +131,8 @@ class AttnMeta:
 
 DECODE_PARTS = tuple(range(256, 1537, 64))  # candidate keys per decode work item (64-key aligned)
 DECODE_PARTS_V1 = (512, 768, 1024)
+# consecutive tokens of one sequence in a decode step share multi-token work items
+DECODE_GROUP_TOKENS = os.environ.get("K8S_DECODE_GROUP", "1") == "1"
 DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (<= 256 VGPRs)
 DECODE_ITEM_OVERHEAD = 256               # per-item start cost in key-equivalents (replay-calibrated)
 _DECODE_PLANNER = "makespan"
@@ -193,7 +195,7 @@ def set_decode_planner(name: str) -> None:
 
 
 def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size: int, device,
-                       q_rows=None, part: Optional[int] = None) -> "AttnMeta":
+                       q_rows=None, part: Optional[int] = None, chain=None) -> "AttnMeta":
     """Plan + upload the decode split for ``meta`` (tests / tools; the engine
     ships the same arrays in its step buffer).  Paged-64 caches use the
     persistent work-list kernel; other page sizes the (seq, part) grid."""
@@ -205,7 +207,9 @@ def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size
         if part is not None:
             P = part
             n_parts = max(1, -(-max(ctx_host) // P))
-        items = build_decode_items(ctx_host, q_rows if q_rows is not None else np.arange(S), P)
+        G = nq // nkv
+        items = build_decode_items(ctx_host, q_rows if q_rows is not None else np.arange(S), P, chain,
+                                   max(1, 16 // G) if G <= 16 else 1)
         meta.items = torch.from_numpy(items).to(device)
         meta.n_items = items.shape[0]
     else:
@@ -219,22 +223,55 @@ def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size
     return meta
 
 
-def build_decode_items(ctx_lens, q_rows, part: int):
-    """Work list [n_items, 4] int32 = (seq, part | -1 for a one-item row, end
-    key, q row), longest first."""
+def decode_groups(ctx_lens, q_rows, chain, gmax: int, part: Optional[int] = None):
+    """Multi-token decode items: ``chain[i]`` = row i is the next token of row
+    i-1's sequence (a short prefill chunk run as decode rows).  Runs of chained
+    rows are cut into groups of at most ``gmax`` (= 16 // G: the decode MFMA's
+    16 rows hold G q heads per token) consecutive q rows; with ``part`` a group
+    also never mixes rows of different partition counts (each row's split-KV
+    reduce reads its own count).  Returns (first row, tokens) per group."""
     import numpy as np
     c = np.asarray(ctx_lens, dtype=np.int64)
-    n = (c + part - 1) // part
-    seq = np.repeat(np.arange(c.size), n)
+    S = c.size
+    idx = np.arange(S)
+    ok = np.zeros(S, dtype=bool)
+    if chain is not None and gmax > 1 and S > 1:
+        qr = np.asarray(q_rows, dtype=np.int64)
+        ok[1:] = np.asarray(chain[1:], dtype=bool) & (qr[1:] == qr[:-1] + 1)
+        if part is not None:
+            n = (c + part - 1) // part
+            ok[1:] &= n[1:] == n[:-1]
+    brk = ~ok
+    start = np.maximum.accumulate(np.where(brk, idx, 0))
+    lead = np.nonzero(brk | ((idx - start) % max(gmax, 1) == 0))[0]
+    nt = np.diff(np.append(lead, S))
+    return lead, nt
+
+
+def build_decode_items(ctx_lens, q_rows, part: int, chain=None, gmax: int = 1):
+    """Work list [n_items, 4] int32 = (seq, part | -1 for a one-item row, end
+    key, q row | (tokens - 1) << 24), longest first.  With ``chain`` rows of
+    one sequence's consecutive tokens share items (``decode_groups``): the
+    item's seq / q row are its first token's, its key range its last token's."""
+    import numpy as np
+    c = np.asarray(ctx_lens, dtype=np.int64)
+    qr = np.asarray(q_rows, dtype=np.int64)
+    if chain is not None and gmax > 1:
+        lead, nt = decode_groups(c, qr, chain, gmax, part)
+    else:
+        lead, nt = np.arange(c.size), np.ones(c.size, dtype=np.int64)
+    cl = c[lead + nt - 1]
+    n = (cl + part - 1) // part
+    g = np.repeat(np.arange(lead.size), n)
     first = np.repeat(np.cumsum(n) - n, n)
-    pidx = np.arange(seq.size) - first
+    pidx = np.arange(g.size) - first
     k0 = pidx * part
-    k1 = np.minimum(c[seq], k0 + part)
-    out = np.empty((seq.size, 4), dtype=np.int32)
-    out[:, 0] = seq
-    out[:, 1] = np.where(n[seq] == 1, -1, pidx)
+    k1 = np.minimum(cl[g], k0 + part)
+    out = np.empty((g.size, 4), dtype=np.int32)
+    out[:, 0] = lead[g]
+    out[:, 1] = np.where(n[g] == 1, -1, pidx)
     out[:, 2] = k1
-    out[:, 3] = np.asarray(q_rows, dtype=np.int64)[seq]
+    out[:, 3] = qr[lead[g]] | ((nt[g] - 1) << 24)
     order = np.argsort(-(k1 - k0), kind="stable")
     return out[order]
 

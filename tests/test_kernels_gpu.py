@@ -1,6 +1,8 @@
 """HIP kernel numerics vs fp32 PyTorch references (run on the MI355X via gpurun)."""
 import math
 
+import numpy as np
+
 import pytest
 import torch
 
@@ -136,6 +138,52 @@ def test_paged_decode(nq, nkv, ctx, BS):
     out = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
     ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (64, 8), (8, 1)])
+def test_paged_decode_multi_token_items(nq, nkv):
+    """Consecutive tokens of one sequence as decode rows (a short chunk):
+    multi-token work items (16 // G tokens share one MFMA, keys read once)
+    match the fp32 reference per row and are bit-identical to one item per
+    row -- incl. groups split where a row's partition count changes."""
+    _need_gpu()
+    torch.manual_seed(4)
+    BS = 64
+    runs = [(1000, 6), (254, 6), (60, 3), (5000, 4), (17, 1), (1535, 5)]
+    ctx, seq_of, chain = [], [], []
+    for i, (c0, q) in enumerate(runs):
+        for j in range(q):
+            ctx.append(c0 + j + 1)
+            seq_of.append(i)
+            chain.append(j > 0)
+    S = len(ctx)
+    NB = sum((c0 + q + BS - 1) // BS for c0, q in runs) + 4
+    kc, vc = _setup_cache(nkv, BS, NB, dev)
+    perm = torch.randperm(NB)
+    maxb = max((c + BS - 1) // BS for c in ctx)
+    bt_seq, used = [], 0
+    for c0, q in runs:
+        nb = (c0 + q + BS - 1) // BS
+        row = torch.zeros(maxb, dtype=torch.int32)
+        row[:nb] = perm[used:used + nb].int()
+        used += nb
+        bt_seq.append(row)
+    bt = torch.stack([bt_seq[i] for i in seq_of])
+    q = torch.randn(S, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+    scale = 1 / math.sqrt(128)
+    outs = []
+    for ch in (None, np.asarray(chain)):
+        meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
+                          q_start=torch.arange(S + 1, dtype=torch.int32, device=dev), num_seqs=S, decode=True,
+                          ctx_lens_host=list(ctx), q_start_host=list(range(S + 1)))
+        A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev, part=256, chain=ch)
+        if ch is not None:
+            assert meta.n_items < outs[0][1]  # the chunks' rows share items
+        outs.append((A.paged_attention(q, kc, vc, meta, nq, nkv, scale), meta.n_items))
+        cpu_meta = _cpu_meta(meta)
+    ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), cpu_meta, nq, nkv, scale)
+    torch.testing.assert_close(outs[1][0].cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    assert torch.equal(outs[0][0], outs[1][0])
 
 
 @pytest.mark.parametrize("BS", [64, 32])  # 64: paged-64 32x32x16 kernel; 32: generic kernel

@@ -178,7 +178,10 @@ def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
                                  temperature=0.0, graph_batch_sizes=(1, 2, 4, 8, 16)))
     g = torch.Generator().manual_seed(3)
     outs = []
-    for n0, q in ((40, 6), (63, 5), (64, 8)):  # chunks that stay in a page / cross a page boundary
+    gmax = eng._dec_gmax
+    assert gmax > 1
+    # chunks inside a page / across a page boundary / across a decode partition boundary
+    for n0, q in ((40, 6), (63, 5), (64, 8), (254, 6), (1000, 7)):
         s = eng.seqs[eng.new_sequence()]
         s.tokens = torch.randint(5, 1000, (n0 + q,), generator=g).tolist()
         assert eng._ensure_blocks(s, n0 + q, set())
@@ -186,10 +189,14 @@ def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
         s.n_cached = n0
         big = eng._forward([], [(s, q)], list(range(q))).float()
         rows = eng._forward([(s, j) for j in range(q)], [], list(range(q))).float()
+        eng._dec_gmax = 1  # one decode item per row: the multi-token items are bit-identical
+        rows1 = eng._forward([(s, j) for j in range(q)], [], list(range(q))).float()
+        eng._dec_gmax = gmax
         torch.cuda.synchronize()
+        assert torch.equal(rows, rows1), (n0, q)
         err = (big - rows).abs().max().item() / big.abs().max().item()
         assert err < 3e-2, (n0, q, err)
         assert (big.argmax(-1) == rows.argmax(-1)).float().mean().item() >= 0.8
         outs.append(err)
     if graphs:
-        assert eng.stats["graph_steps"] == 3
+        assert eng.stats["graph_steps"] == 10

@@ -28,6 +28,7 @@
 #include <hipblaslt/hipblaslt.h>
 #include <hipblaslt/hipblaslt-ext.hpp>
 
+#include <algorithm>
 #include <iterator>
 #include <map>
 #include <mutex>
@@ -226,6 +227,95 @@ K8S_API int k8s_blaslt_tune(const void* x, int ldx, const void* w, void* y, int 
     times[1] = best_us;
   }
   return best;
+}
+
+// Time EVERY solution the library has for this problem (getAllAlgos +
+// matmulIsAlgoSupported), not only the heuristic's list: at mid M (256..2048)
+// with N = 4096 the heuristic's solutions use 256x256 macro tiles that leave
+// most CUs idle, and smaller-tile / split-K solutions it ranks low are what
+// fills the chip.  Writes the `max_out` fastest (solution index, us) pairs,
+// fastest first, and returns how many it wrote (< 0: error).  times[0] = the
+// heuristic's first choice (us).  A tool / init-time call (not capturable).
+// `nw` weight copies `w_stride` elements apart are rotated (cold weights, as
+// the engine's per-layer calls see them).
+K8S_API int k8s_blaslt_sweep(const void* x, int ldx, const void* w, int nw, size_t w_stride, void* y, int ldy, int M,
+                             int N, int K, void* ws, size_t ws_bytes, int iters, hipStream_t s, int max_out,
+                             int* out_idx, float* out_us, float* times) {
+  if (M <= 0 || N <= 0 || K <= 0 || ldx < K || ldy < N || iters < 1 || max_out < 1 || nw < 1)
+    return -(int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return -900;
+  const Key key{M, N, K, ldx, ldy, 0};
+  Plan p;
+  int rc = make_desc(key, &p);
+  if (rc) return -rc;
+  auto wk = [&](int r) { return (const void*)((const uint16_t*)w + (size_t)(r % nw) * w_stride); };
+  std::vector<hipblasLtMatmulHeuristicResult_t> all;
+  if (hipblaslt_ext::getAllAlgos(g_handle, hipblaslt_ext::GemmType::HIPBLASLT_GEMM, HIPBLAS_OP_T, HIPBLAS_OP_N,
+                                 HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIP_R_16BF, HIPBLAS_COMPUTE_32F,
+                                 all) != HIPBLAS_STATUS_SUCCESS)
+    return -1600;
+  hipEvent_t e0, e1;
+  if (hipEventCreate(&e0) != hipSuccess || hipEventCreate(&e1) != hipSuccess) return -901;
+  const float alpha = 1.f, beta = 0.f;
+  auto time_algo = [&](hipblasLtMatmulAlgo_t& algo, size_t wsz) -> float {
+    for (int r = 0; r < 2; ++r)
+      if (hipblasLtMatmul(g_handle, p.desc, &alpha, wk(r), p.a, x, p.b, &beta, y, p.c, y, p.c, &algo, ws, wsz, s) !=
+          HIPBLAS_STATUS_SUCCESS)
+        return -1.f;
+    if (hipStreamSynchronize(s) != hipSuccess) return -1.f;
+    hipEventRecord(e0, s);
+    for (int r = 0; r < iters; ++r)
+      hipblasLtMatmul(g_handle, p.desc, &alpha, wk(r), p.a, x, p.b, &beta, y, p.c, y, p.c, &algo, ws, wsz, s);
+    hipEventRecord(e1, s);
+    if (hipEventSynchronize(e1) != hipSuccess) return -1.f;
+    float ms = 0.f;
+    hipEventElapsedTime(&ms, e0, e1);
+    return 1000.f * ms / iters;
+  };
+  if (times) {
+    hipblasLtMatmulHeuristicResult_t h[1];
+    int n = 0;
+    times[0] = heuristic(p, ws_bytes, 1, h, &n) == 0 ? time_algo(h[0].algo, h[0].workspaceSize) : -1.f;
+  }
+  std::vector<std::pair<float, int>> best;
+  for (auto& r : all) {
+    size_t wsz = 0;
+    if (hipblaslt_ext::matmulIsAlgoSupported(g_handle, p.desc, &alpha, p.a, p.b, &beta, p.c, p.c, r.algo, wsz) !=
+            HIPBLAS_STATUS_SUCCESS ||
+        wsz > ws_bytes)
+      continue;
+    const float us = time_algo(r.algo, wsz);
+    if (us > 0.f) best.emplace_back(us, hipblaslt_ext::getIndexFromAlgo(r.algo));
+  }
+  hipEventDestroy(e0);
+  hipEventDestroy(e1);
+  std::sort(best.begin(), best.end());
+  const int n = std::min<int>(max_out, (int)best.size());
+  for (int i = 0; i < n; ++i) {
+    out_us[i] = best[i].first;
+    out_idx[i] = best[i].second;
+  }
+  return n;
+}
+
+// Register solution `idx` (from k8s_blaslt_sweep, kept in a data file) for
+// (N, K) from ladder point M up: plans built afterwards use it where the
+// library confirms it supports the problem (build_plan), else the heuristic.
+K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return 900;
+  std::vector<int> ids{idx};
+  std::vector<hipblasLtMatmulHeuristicResult_t> res;
+  if (hipblaslt_ext::getAlgosFromIndex(g_handle, ids, res) != HIPBLAS_STATUS_SUCCESS || res.empty()) return 1700;
+  g_tuned[{N, K}][M] = res[0].algo;
+  for (auto it = g_plans.begin(); it != g_plans.end();) {
+    if (it->first.N == N && it->first.K == K)
+      it = g_plans.erase(it);
+    else
+      ++it;
+  }
+  return 0;
 }
 
 K8S_API void k8s_blaslt_clear_tuning() {

@@ -202,6 +202,7 @@ class LLMEngine:
             from ..ops import linear as LIN
             gemm_tuning.load(self.mc.name, self.pc.tp_size)
             LIN.reserve_lib_workspace(self.device)
+            self.lib_algos = LIN.load_lib_algos(LIN.lib_algos_path(self.mc.name, self.pc.tp_size))
             if cfg.tune_lib_gemms:  # measured hipBLASLt solutions for prefill-sized M
                 t_tune = time.perf_counter()
                 self.gemm_tuning = LIN.tune_lib_gemms(self.device, LIN.projection_shapes(self.mc, self.pc.tp_size),

@@ -185,6 +185,34 @@ def tune_lib_gemms(dev: torch.device, shapes, max_m: int = 8192, max_algos: int 
     return out
 
 
+def lib_algos_path(model: str, tp: int = 1) -> str:
+    return os.path.join(DATA_DIR, f"blaslt_algos_{model}" + (f"-tp{tp}" if tp > 1 else "") + ".json")
+
+
+def load_lib_algos(path: str) -> int:
+    """Register the measured hipBLASLt solutions of ``path``
+    (tools/blaslt_sweep.py --emit: solution index per (N, K) per ladder M,
+    the fastest of ALL the library's solutions where it beat the heuristic's
+    first choice) with the native front end.  Returns how many were accepted.
+    OFF by default (K8S_BLASLT_ALGOS=1 enables it): per-shape the swept
+    winners are 1.0-1.6x faster at their ladder M (profiles/r2_blaslt_sweep.txt)
+    but the engine's M falls between ladder points and the headline measured
+    9.33 / 9.40 -> 8.89 / 8.83 analyses/s with the table (interleaved A/B), the
+    same loss the round-1 top-24 tuning showed.  No-op without the native
+    library GEMM."""
+    if not _native_lib_gemm or os.environ.get("K8S_BLASLT_ALGOS", "0") != "1" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        d = json.load(f)
+    n = 0
+    for key, ladder in d.get("algos", {}).items():
+        N, K = (int(v) for v in key.split(","))
+        for M, idx in sorted(ladder.items(), key=lambda kv: int(kv[0])):
+            if lib().k8s_blaslt_set_algo(int(M), N, K, int(idx)) == 0:
+                n += 1
+    return n
+
+
 def clear_lib_tuning() -> None:
     lib().k8s_blaslt_clear_tuning()
     _tuned_report.clear()

@@ -31,6 +31,8 @@ int k8s_splitk_addnorm(const void* part, int splits, void* res, const void* w, v
 int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s);
 int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc, int T,
                 int nq, int nkv, int BS, hipStream_t s);
+int k8s_splitk_rope_kv(const void* part, int splits, void* qkv, int ld, const int* pos, const float* cos_sin,
+                       const int* slots, void* kc, void* vc, int T, int nq, int nkv, int BS, hipStream_t s);
 int k8s_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                     int bt_stride, const int* ctx_lens, const int* q_start, int S, int nq, int nkv, int BS,
                     float scale, void* out, int out_stride, float* part_o, float* part_ml, int n_parts,
@@ -167,7 +169,9 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
 // are the inputs of the final norm (exactly as after the Python loop).
 // Where the step's dispatch picked a split-K kernel for the o or down
 // projection, its partials are reduced inside the following residual-add +
-// RMSNorm (k8s_splitk_addnorm): bit-identical, one launch fewer per GEMM.
+// RMSNorm (k8s_splitk_addnorm), and a split-K qkv projection's inside the
+// RoPE / KV-write kernel (k8s_splitk_rope_kv): bit-identical, one launch fewer
+// per GEMM.
 K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   const K8sLlamaStep& s = *sp;
   const int T = s.T, H = s.H, nd = s.nd;
@@ -185,8 +189,16 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                                  s.eps, st));
     else
       K8S_TRY(k8s_rmsnorm(s.prev, s.residual, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
-    K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
-    K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    // a split-K qkv projection leaves its partials to the RoPE / KV-write kernel,
+    // which reduces them first (k8s_splitk_rope_kv: bit-identical, one launch fewer)
+    if (deferred(s.sel[0], true)) {
+      K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st, true));
+      K8S_TRY(k8s_splitk_rope_kv(part_of(s, s.sel[0]), s.sel[0].splits, qkv, ld_qkv, s.pos, s.cos_sin, s.slots,
+                                 s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    } else {
+      K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
+      K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    }
     if (nd > 0 && s.d_bt)
       K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
                               s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,

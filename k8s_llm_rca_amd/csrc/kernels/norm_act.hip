@@ -115,12 +115,46 @@ __global__ void __launch_bounds__(256) silu_mul_kernel(const uint16_t* __restric
 // Rotates q and k in place (rotate-half / NeoX pairing i <-> i+64), writes
 // k -> K page [blk][h][off][:], v -> transposed V page [blk][h][:][off].
 // cos_sin: [max_pos][128] fp32 = cos[0..63] | sin[0..63].
+//
+// PART: the qkv projection was a split-K GEMM whose fp32 partials
+// part[s][t][0..ld) (gemm_stream / gemm_mid / grouped layout, s < splits) are
+// still unreduced.  Each 8-column piece is summed here in the reduce kernel's
+// order (split 0, then += 1, 2, ...) and rounded to bf16 before the rotation,
+// and the reduced (then rotated) row is stored back into qkv, so qkv, the K
+// page and the V page are bit-identical to reduce kernel + this kernel -- one
+// launch and one [T][ld] bf16 round trip fewer per layer of a decode step
+// (SURVEY B3 "fuse into the QKV-GEMM epilogue").
+template <bool PART>
+__device__ __forceinline__ u16x8 qkv_piece(const uint16_t* row, const float* prow, int col, int splits, size_t MN) {
+  if constexpr (!PART) {
+    return *reinterpret_cast<const u16x8*>(row + col);
+  } else {
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(prow + col);
+    f32x4 a1 = *reinterpret_cast<const f32x4*>(prow + col + 4);
+    for (int s = 1; s < splits; ++s) {
+      a0 += *reinterpret_cast<const f32x4*>(prow + s * MN + col);
+      a1 += *reinterpret_cast<const f32x4*>(prow + s * MN + col + 4);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      o[v] = f2bf(a0[v]);
+      o[v + 4] = f2bf(a1[v]);
+    }
+    return o;
+  }
+}
+
+template <bool PART>
 __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv, int ld, const int* __restrict__ pos,
                                                       const float* __restrict__ cos_sin,
                                                       const int* __restrict__ slots, uint16_t* __restrict__ kc,
-                                                      uint16_t* __restrict__ vc, int nq, int nkv, int BS) {
+                                                      uint16_t* __restrict__ vc, int nq, int nkv, int BS,
+                                                      const float* __restrict__ part, int splits, int T) {
   const int t = blockIdx.x;
   uint16_t* row = qkv + (size_t)t * ld;
+  const size_t MN = (size_t)T * ld;
+  const float* prow = PART ? part + (size_t)t * ld : nullptr;
   const int p = pos[t];
   const float* cs = cos_sin + (size_t)p * 128;
   const int slot = slots ? slots[t] : -1;
@@ -129,8 +163,8 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv
   for (int i = threadIdx.x; i < nrot; i += blockDim.x) {
     const int hd = i >> 3, c = (i & 7) * 8;
     uint16_t* xp = row + hd * 128;
-    u16x8 lo = *reinterpret_cast<u16x8*>(xp + c);
-    u16x8 hi = *reinterpret_cast<u16x8*>(xp + 64 + c);
+    const u16x8 lo = qkv_piece<PART>(row, prow, hd * 128 + c, splits, MN);
+    const u16x8 hi = qkv_piece<PART>(row, prow, hd * 128 + 64 + c, splits, MN);
     u16x8 olo, ohi;
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -148,12 +182,15 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv
       *reinterpret_cast<u16x8*>(kp + 64 + c) = ohi;
     }
   }
-  if (slot < 0) return;
-  // V: nkv*128 values, transposed scatter into the page
-  const uint16_t* vrow = row + (nq + nkv) * 128;
+  if (!PART && slot < 0) return;
+  // V: nkv*128 values, transposed scatter into the page (PART: reduced and
+  // stored back into qkv first, as the reduce kernel would have)
+  uint16_t* vrow = row + (nq + nkv) * 128;
   for (int i = threadIdx.x; i < nkv * 16; i += blockDim.x) {
     const int kh = i >> 4, d0 = (i & 15) * 8;
-    u16x8 v = *reinterpret_cast<const u16x8*>(vrow + kh * 128 + d0);
+    const u16x8 v = qkv_piece<PART>(row, prow, (nq + nkv) * 128 + kh * 128 + d0, splits, MN);
+    if (PART) *reinterpret_cast<u16x8*>(vrow + kh * 128 + d0) = v;
+    if (slot < 0) continue;
     uint16_t* vp = vc + ((size_t)blk * nkv + kh) * 128 * BS + off;
 #pragma unroll
     for (int j = 0; j < 8; ++j) vp[(size_t)(d0 + j) * BS] = v[j];
@@ -221,7 +258,19 @@ K8S_API int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s)
 K8S_API int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc,
                         int T, int nq, int nkv, int BS, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(rope_kv_kernel, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
-                     (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS);
+  hipLaunchKernelGGL(rope_kv_kernel<false>, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
+                     (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS, (const float*)nullptr, 0, T);
+  return (int)hipGetLastError();
+}
+
+// qkv = bf16(sum_s part[s]) with q, k rotated and k, v written to their pages:
+// reduce kernel + k8s_rope_kv in one launch, bit-identical.  part =
+// [splits][T][ld] fp32 (the split-K GEMM's partials, ld = (nq + 2 nkv) * 128).
+K8S_API int k8s_splitk_rope_kv(const void* part, int splits, void* qkv, int ld, const int* pos, const float* cos_sin,
+                               const int* slots, void* kc, void* vc, int T, int nq, int nkv, int BS, hipStream_t s) {
+  if (T <= 0) return 0;
+  if (!part || splits < 1 || ld % 8 || ld < (nq + 2 * nkv) * 128) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rope_kv_kernel<true>, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
+                     (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS, (const float*)part, splits, T);
   return (int)hipGetLastError();
 }

@@ -178,8 +178,8 @@ class LlamaModel:
                 N.rmsnorm(residual, L["in_norm"], cfg.rms_eps, out=y)
             else:
                 N.rmsnorm(prev, L["in_norm"], cfg.rms_eps, residual=residual, out=y)
-            qkv = linear(y, L["wqkv"])
-            A.rope_kv_write(qkv, inp.positions, self.cos_sin, inp.slots, k_cache[li], v_cache[li], self.nq, self.nkv)
+            qkv = A.linear_rope_kv(y, L["wqkv"], inp.positions, self.cos_sin, inp.slots, k_cache[li], v_cache[li],
+                                   self.nq, self.nkv)
             if inp.meta_decode is not None and nd > 0:
                 A.paged_attention(qkv[:nd], k_cache[li], v_cache[li], inp.meta_decode, self.nq, self.nkv, self.scale,
                                   out=attn[:nd])

@@ -28,6 +28,7 @@ _SIGS = {
     "k8s_rmsnorm": [P, P, P, P, I, I, I, I, F, P],
     "k8s_silu_mul": [P, P, I, I, P],
     "k8s_rope_kv": [P, I, P, P, P, P, P, I, I, I, I, P],
+    "k8s_splitk_rope_kv": [P, I, P, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_attn_decode": [P, I, P, P, P, I, P, P, I, I, I, I, F, P, I, P, P, I, I, P, I, P, I, P],
     "k8s_attn_prefill": [P, I, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P, P, I, I, I, F, P, I, P],
     "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, I, P, P, P, I],

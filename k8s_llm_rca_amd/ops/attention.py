@@ -83,6 +83,42 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
     v_cache[blk, :, :, off] = v[ok]
 
 
+_fuse_qkv = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
+
+
+def linear_rope_kv(y: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                   slots: Optional[torch.Tensor], k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int,
+                   nkv: int) -> torch.Tensor:
+    """``qkv = y @ w.T`` followed by :func:`rope_kv_write`.  When the measured
+    dispatch picks a split-K kernel for this M, its fp32 partials go straight
+    to ``k8s_splitk_rope_kv``, which reduces them in the reduce kernel's order
+    before rotating: bit-identical to ``linear`` + ``rope_kv_write`` with one
+    launch fewer (csrc/kernels/norm_act.hip, PART form of rope_kv_kernel)."""
+    from . import linear as LIN
+    M, K = y.shape
+    N = w.shape[0]
+    if _fuse_qkv and use_hip(y) and y.dtype == torch.bfloat16 and slots is not None:
+        layout = y.stride(1) == 1 and y.stride(0) % 8 == 0 and w.is_contiguous()
+        kind, cfg, splits = LIN.select_gemm(M, N, K, layout, True)
+        if kind in (LIN.KIND_STREAM, LIN.KIND_MID) and splits > 1:
+            qkv = torch.empty((M, N), dtype=y.dtype, device=y.device)
+            part = LIN._scratch(y.device, splits * M * N)
+            fn = lib().k8s_gemm_stream_part if kind == LIN.KIND_STREAM else lib().k8s_gemm_mid_part
+            check(fn(ptr(y), y.stride(0), ptr(w), ptr(qkv), N, M, N, K, cfg, splits, ptr(part), stream_ptr(y)),
+                  "qkv gemm (split-K partials)")
+            BS = k_cache.shape[2]
+            assert positions.dtype == torch.int32 and cos_sin.dtype == torch.float32 and slots.dtype == torch.int32
+            assert k_cache.shape[1] == nkv and v_cache.shape[2] == HEAD_DIM and v_cache.shape[3] == BS
+            assert N >= (nq + 2 * nkv) * HEAD_DIM
+            check(lib().k8s_splitk_rope_kv(ptr(part), splits, ptr(qkv), N, ptr(positions), ptr(cos_sin), ptr(slots),
+                                           ptr(k_cache), ptr(v_cache), M, nq, nkv, BS, stream_ptr(y)),
+                  "splitk_rope_kv")
+            return qkv
+    qkv = LIN.linear(y, w)
+    rope_kv_write(qkv, positions, cos_sin, slots, k_cache, v_cache, nq, nkv)
+    return qkv
+
+
 @dataclass
 class AttnMeta:
     """Per-step attention metadata (device tensors, int32)."""

@@ -94,6 +94,67 @@ def test_rope_kv_write(nq, nkv):
     torch.testing.assert_close(vc.cpu().float(), vc_r.float(), atol=0, rtol=0)
 
 
+@pytest.mark.parametrize("S,T", [(2, 96), (4, 5), (3, 130)])
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1)])
+def test_splitk_rope_kv_bit_identical(S, T, nq, nkv):
+    """Fused split-K reduce + RoPE + paged KV write (k8s_splitk_rope_kv) ==
+    reduce in split order, bf16 round, then rope_kv_write -- bit for bit (qkv,
+    K pages, V pages), incl. a row with no slot."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops._lib import check, lib, ptr, stream_ptr
+    torch.manual_seed(S * 131 + T)
+    BS, NB = 64, 8
+    ld = (nq + 2 * nkv) * 128
+    cs = A.rope_cos_sin(4096, 500000.0, device=dev)
+    part = torch.randn(S, T, ld, device=dev) * 0.5
+    pos = torch.randint(0, 4000, (T,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=dev)[:T].int()
+    slots[min(3, T - 1)] = -1
+    kc0 = torch.randn(NB, nkv, BS, 128, device=dev).bfloat16()
+    vc0 = torch.randn(NB, nkv, 128, BS, device=dev).bfloat16()
+    acc = part[0].clone()
+    for s in range(1, S):
+        acc += part[s]
+    qkv_u, kc_u, vc_u = acc.bfloat16(), kc0.clone(), vc0.clone()
+    A.rope_kv_write(qkv_u, pos, cs, slots, kc_u, vc_u, nq, nkv)
+    qkv_f = torch.empty(T, ld, device=dev, dtype=torch.bfloat16)
+    kc_f, vc_f = kc0.clone(), vc0.clone()
+    check(lib().k8s_splitk_rope_kv(ptr(part), S, ptr(qkv_f), ld, ptr(pos), ptr(cs), ptr(slots), ptr(kc_f), ptr(vc_f),
+                                   T, nq, nkv, BS, stream_ptr(part)), "splitk_rope_kv")
+    torch.cuda.synchronize()
+    assert torch.equal(qkv_f, qkv_u) and torch.equal(kc_f, kc_u) and torch.equal(vc_f, vc_u)
+
+
+@pytest.mark.parametrize("M", [24, 96, 128, 200])
+def test_linear_rope_kv_matches_unfused(M, monkeypatch):
+    """The model's qkv path (ops.attention.linear_rope_kv) with the 8B dispatch
+    table loaded: where it picks a split-K kernel the fused reduce+RoPE output
+    equals linear() + rope_kv_write() exactly."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    saved = LIN._dispatch
+    assert LIN.load_dispatch(LIN.dispatch_path("llama3-8b"))
+    try:
+        torch.manual_seed(M)
+        nq, nkv, BS, NB = 32, 8, 64, 8
+        N, K = (nq + 2 * nkv) * 128, 4096
+        y = torch.randn(M, K, device=dev).bfloat16()
+        w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+        cs = A.rope_cos_sin(8192, 500000.0, device=dev)
+        pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
+        slots = torch.randperm(NB * BS, device=dev)[:M].int()
+        kc0 = torch.zeros(NB, nkv, BS, 128, device=dev).bfloat16()
+        vc0 = torch.zeros(NB, nkv, 128, BS, device=dev).bfloat16()
+        kc_f, vc_f = kc0.clone(), vc0.clone()
+        qkv_f = A.linear_rope_kv(y, w, pos, cs, slots, kc_f, vc_f, nq, nkv)
+        qkv_u = LIN.linear(y, w)
+        kc_u, vc_u = kc0.clone(), vc0.clone()
+        A.rope_kv_write(qkv_u, pos, cs, slots, kc_u, vc_u, nq, nkv)
+        assert torch.equal(qkv_f, qkv_u) and torch.equal(kc_f, kc_u) and torch.equal(vc_f, vc_u)
+    finally:
+        LIN._dispatch = saved
+
+
 def _meta(ctx, qlen, nq, nkv, BS, nblocks_total, device, decode):
     S = len(ctx)
     maxb = max((c + BS - 1) // BS for c in ctx)

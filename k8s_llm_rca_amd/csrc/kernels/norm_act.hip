@@ -145,23 +145,31 @@ __device__ __forceinline__ u16x8 qkv_piece(const uint16_t* row, const float* pro
   }
 }
 
+// Grid (T, units / block), ONE unit per lane: unit u <
+// (nq + nkv) * 8 rotates 8 (i, i + 64) pairs of head u / 8; the next nkv * 16
+// units move 8 dims of one v head.  (A block per token looping over its 448
+// units left a decode step with ~125 blocks: 9.4 us of serial latency per
+// layer at M = 125; spread over ~900 one-wave blocks each lane pays one round
+// trip.  Long prefill steps use 256-lane blocks: 64-lane ones measured 7 %
+// slower there, dispatch-bound at T x 7 blocks.)
 template <bool PART>
 __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv, int ld, const int* __restrict__ pos,
-                                                      const float* __restrict__ cos_sin,
-                                                      const int* __restrict__ slots, uint16_t* __restrict__ kc,
-                                                      uint16_t* __restrict__ vc, int nq, int nkv, int BS,
-                                                      const float* __restrict__ part, int splits, int T) {
+                                                     const float* __restrict__ cos_sin,
+                                                     const int* __restrict__ slots, uint16_t* __restrict__ kc,
+                                                     uint16_t* __restrict__ vc, int nq, int nkv, int BS,
+                                                     const float* __restrict__ part, int splits, int T) {
   const int t = blockIdx.x;
+  const int u = blockIdx.y * blockDim.x + threadIdx.x;
+  const int nrot = (nq + nkv) * 8;  // 8 lanes per head, 8 pairs each
+  if (u >= nrot + nkv * 16) return;
   uint16_t* row = qkv + (size_t)t * ld;
   const size_t MN = (size_t)T * ld;
   const float* prow = PART ? part + (size_t)t * ld : nullptr;
-  const int p = pos[t];
-  const float* cs = cos_sin + (size_t)p * 128;
   const int slot = slots ? slots[t] : -1;
   const int blk = slot >= 0 ? slot / BS : 0, off = slot >= 0 ? slot % BS : 0;
-  const int nrot = (nq + nkv) * 8;  // 8 threads per head, 8 pairs each
-  for (int i = threadIdx.x; i < nrot; i += blockDim.x) {
-    const int hd = i >> 3, c = (i & 7) * 8;
+  if (u < nrot) {
+    const int hd = u >> 3, c = (u & 7) * 8;
+    const float* cs = cos_sin + (size_t)pos[t] * 128;
     uint16_t* xp = row + hd * 128;
     const u16x8 lo = qkv_piece<PART>(row, prow, hd * 128 + c, splits, MN);
     const u16x8 hi = qkv_piece<PART>(row, prow, hd * 128 + 64 + c, splits, MN);
@@ -181,20 +189,19 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv
       *reinterpret_cast<u16x8*>(kp + c) = olo;
       *reinterpret_cast<u16x8*>(kp + 64 + c) = ohi;
     }
+    return;
   }
-  if (!PART && slot < 0) return;
-  // V: nkv*128 values, transposed scatter into the page (PART: reduced and
+  // V: 8 dims of one head, transposed scatter into the page (PART: reduced and
   // stored back into qkv first, as the reduce kernel would have)
-  uint16_t* vrow = row + (nq + nkv) * 128;
-  for (int i = threadIdx.x; i < nkv * 16; i += blockDim.x) {
-    const int kh = i >> 4, d0 = (i & 15) * 8;
-    const u16x8 v = qkv_piece<PART>(row, prow, (nq + nkv) * 128 + kh * 128 + d0, splits, MN);
-    if (PART) *reinterpret_cast<u16x8*>(vrow + kh * 128 + d0) = v;
-    if (slot < 0) continue;
-    uint16_t* vp = vc + ((size_t)blk * nkv + kh) * 128 * BS + off;
+  if (!PART && slot < 0) return;
+  const int i = u - nrot, kh = i >> 4, d0 = (i & 15) * 8;
+  const int col = (nq + nkv) * 128 + kh * 128 + d0;
+  const u16x8 v = qkv_piece<PART>(row, prow, col, splits, MN);
+  if (PART) *reinterpret_cast<u16x8*>(row + col) = v;
+  if (slot < 0) return;
+  uint16_t* vp = vc + ((size_t)blk * nkv + kh) * 128 * BS + off;
 #pragma unroll
-    for (int j = 0; j < 8; ++j) vp[(size_t)(d0 + j) * BS] = v[j];
-  }
+  for (int j = 0; j < 8; ++j) vp[(size_t)(d0 + j) * BS] = v[j];
 }
 
 }  // namespace k8s
@@ -255,10 +262,13 @@ K8S_API int k8s_silu_mul(const void* gu, void* out, int T, int I, hipStream_t s)
   return (int)hipGetLastError();
 }
 
+static int rope_block(int T) { return T >= 512 ? 256 : 64; }
+
 K8S_API int k8s_rope_kv(void* qkv, int ld, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc,
                         int T, int nq, int nkv, int BS, hipStream_t s) {
   if (T <= 0) return 0;
-  hipLaunchKernelGGL(rope_kv_kernel<false>, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
+  const int bs = rope_block(T), units = (nq + nkv) * 8 + nkv * 16;
+  hipLaunchKernelGGL(rope_kv_kernel<false>, dim3(T, (units + bs - 1) / bs), dim3(bs), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
                      (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS, (const float*)nullptr, 0, T);
   return (int)hipGetLastError();
 }
@@ -270,7 +280,8 @@ K8S_API int k8s_splitk_rope_kv(const void* part, int splits, void* qkv, int ld, 
                                const int* slots, void* kc, void* vc, int T, int nq, int nkv, int BS, hipStream_t s) {
   if (T <= 0) return 0;
   if (!part || splits < 1 || ld % 8 || ld < (nq + 2 * nkv) * 128) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(rope_kv_kernel<true>, dim3(T), dim3(256), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
+  const int bs = rope_block(T), units = (nq + nkv) * 8 + nkv * 16;
+  hipLaunchKernelGGL(rope_kv_kernel<true>, dim3(T, (units + bs - 1) / bs), dim3(bs), 0, s, (uint16_t*)qkv, ld, pos, cos_sin, slots,
                      (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS, (const float*)part, splits, T);
   return (int)hipGetLastError();
 }

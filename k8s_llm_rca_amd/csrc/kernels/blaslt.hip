@@ -68,8 +68,12 @@ struct Plan {
 std::mutex g_mu;
 hipblasLtHandle_t g_handle = nullptr;
 std::unordered_map<Key, Plan, KeyHash> g_plans;
-// (N, K) -> ladder M -> tuned algorithm
-std::map<std::pair<int, int>, std::map<int, hipblasLtMatmulAlgo_t>> g_tuned;
+// (N, K) -> ladder M -> tuned algorithm, used for M in [ladder M, hi]
+struct Tuned {
+  hipblasLtMatmulAlgo_t algo;
+  int hi;
+};
+std::map<std::pair<int, int>, std::map<int, Tuned>> g_tuned;
 
 int make_desc(const Key& k, Plan* p) {
   hipblasStatus_t st = hipblasLtMatmulDescCreate(&p->desc, HIPBLAS_COMPUTE_32F, HIP_R_32F);
@@ -105,7 +109,7 @@ int build_plan(const Key& k, size_t ws_limit, Plan* out) {
     hipblasLtMatmulAlgo_t algo;
     size_t wsz = 0;
     const float alpha = 1.f, beta = 0.f;
-    if (it != t->second.begin() && (algo = std::prev(it)->second, true) &&
+    if (it != t->second.begin() && k.M <= std::prev(it)->second.hi && (algo = std::prev(it)->second.algo, true) &&
         hipblaslt_ext::matmulIsAlgoSupported(g_handle, p.desc, &alpha, p.a, p.b, &beta, p.c, p.c, algo, wsz) ==
             HIPBLAS_STATUS_SUCCESS &&
         wsz <= ws_limit) {
@@ -215,7 +219,7 @@ K8S_API int k8s_blaslt_tune(const void* x, int ldx, const void* w, void* y, int 
   hipEventDestroy(e0);
   hipEventDestroy(e1);
   if (best < 0) return -1500;
-  g_tuned[{N, K}][M] = res[best].algo;
+  g_tuned[{N, K}][M] = Tuned{res[best].algo, 1 << 30};
   for (auto it = g_plans.begin(); it != g_plans.end();) {
     if (it->first.N == N && it->first.K == K)
       it = g_plans.erase(it);  // descriptors intentionally not destroyed (see above)
@@ -302,13 +306,13 @@ K8S_API int k8s_blaslt_sweep(const void* x, int ldx, const void* w, int nw, size
 // Register solution `idx` (from k8s_blaslt_sweep, kept in a data file) for
 // (N, K) from ladder point M up: plans built afterwards use it where the
 // library confirms it supports the problem (build_plan), else the heuristic.
-K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) {
+static int set_algo_range(int M, int hi, int N, int K, int idx) {
   std::lock_guard<std::mutex> g(g_mu);
   if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return 900;
   std::vector<int> ids{idx};
   std::vector<hipblasLtMatmulHeuristicResult_t> res;
   if (hipblaslt_ext::getAlgosFromIndex(g_handle, ids, res) != HIPBLAS_STATUS_SUCCESS || res.empty()) return 1700;
-  g_tuned[{N, K}][M] = res[0].algo;
+  g_tuned[{N, K}][M] = Tuned{res[0].algo, hi};
   for (auto it = g_plans.begin(); it != g_plans.end();) {
     if (it->first.N == N && it->first.K == K)
       it = g_plans.erase(it);
@@ -316,6 +320,14 @@ K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) {
       ++it;
   }
   return 0;
+}
+
+K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) { return set_algo_range(M, 1 << 30, N, K, idx); }
+
+// Bucketed form (tools/blaslt_tune_buckets.py): solution `idx` for M in [lo, hi]
+// only; M outside every registered bucket keeps the heuristic's choice.
+K8S_API int k8s_blaslt_set_algo_range(int lo, int hi, int N, int K, int idx) {
+  return set_algo_range(lo, hi, N, K, idx);
 }
 
 K8S_API void k8s_blaslt_clear_tuning() {

@@ -210,6 +210,13 @@ def load_lib_algos(path: str) -> int:
         for M, idx in sorted(ladder.items(), key=lambda kv: int(kv[0])):
             if lib().k8s_blaslt_set_algo(int(M), N, K, int(idx)) == 0:
                 n += 1
+    # bucketed form (tools/blaslt_tune_buckets.py): [lo, hi, solution] per (N, K),
+    # each verified on the engine's own call path at the bucket's ends and middle
+    for key, rows in d.get("buckets", {}).items():
+        N, K = (int(v) for v in key.split(","))
+        for lo, hi, idx in rows:
+            if lib().k8s_blaslt_set_algo_range(int(lo), int(hi), N, K, int(idx)) == 0:
+                n += 1
     return n
 
 

@@ -40,7 +40,7 @@ def main():
     dev = torch.device("cuda")
     L.reserve_lib_workspace(dev)
     n_alg = L.load_lib_algos(L.lib_algos_path(a.model))
-    table = json.load(open(L.lib_algos_path(a.model)))["algos"]
+    table = json.load(open(L.lib_algos_path(a.model))).get("algos", {})
     steps = [json.loads(l) for l in open(a.trace)]
     Ms = [len(s["d"]) + sum(q for _, q in s["p"]) for s in steps]
     freq = Counter(bucket(M) for M in Ms if M > 256)

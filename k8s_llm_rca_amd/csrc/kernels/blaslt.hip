@@ -322,6 +322,20 @@ static int set_algo_range(int M, int hi, int N, int K, int idx) {
   return 0;
 }
 
+// The heuristic's first-choice solution index for (M, N, K) (x / y dense,
+// ldx = K, ldy = N): candidates for a neighbouring M's bucket
+// (tools/blaslt_tune_buckets.py), where the heuristic's own pick misfires.
+K8S_API int k8s_blaslt_heuristic_index(int M, int N, int K, size_t ws_bytes) {
+  std::lock_guard<std::mutex> g(g_mu);
+  if (g_handle == nullptr && hipblasLtCreate(&g_handle) != HIPBLAS_STATUS_SUCCESS) return -900;
+  Plan p;
+  if (make_desc(Key{M, N, K, K, N, 0}, &p)) return -1100;
+  hipblasLtMatmulHeuristicResult_t res[1];
+  int n = 0;
+  if (heuristic(p, ws_bytes, 1, res, &n) || n < 1) return -1200;
+  return hipblaslt_ext::getIndexFromAlgo(res[0].algo);
+}
+
 K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) { return set_algo_range(M, 1 << 30, N, K, idx); }
 
 // Bucketed form (tools/blaslt_tune_buckets.py): solution `idx` for M in [lo, hi]

@@ -48,6 +48,7 @@ _SIGS = {
     "k8s_blaslt_sweep": [P, I, P, I, ctypes.c_size_t, P, I, I, I, I, P, ctypes.c_size_t, I, P, I, P, P, P],
     "k8s_blaslt_set_algo": [I, I, I, I],
     "k8s_blaslt_set_algo_range": [I, I, I, I, I],
+    "k8s_blaslt_heuristic_index": [I, I, I, ctypes.c_size_t],
     "k8s_gemm_mid_cfg": [I, P],
     "k8s_moe_route": [P, I, I, I, P, P, P],
     "k8s_moe_align": [P, I, I, I, P, P, P, P],

@@ -190,17 +190,23 @@ def lib_algos_path(model: str, tp: int = 1) -> str:
 
 
 def load_lib_algos(path: str) -> int:
-    """Register the measured hipBLASLt solutions of ``path``
-    (tools/blaslt_sweep.py --emit: solution index per (N, K) per ladder M,
-    the fastest of ALL the library's solutions where it beat the heuristic's
-    first choice) with the native front end.  Returns how many were accepted.
-    OFF by default (K8S_BLASLT_ALGOS=1 enables it): per-shape the swept
-    winners are 1.0-1.6x faster at their ladder M (profiles/r2_blaslt_sweep.txt)
-    but the engine's M falls between ladder points and the headline measured
-    9.33 / 9.40 -> 8.89 / 8.83 analyses/s with the table (interleaved A/B), the
-    same loss the round-1 top-24 tuning showed.  No-op without the native
+    """Register the measured hipBLASLt solutions of ``path`` with the native
+    front end; returns how many were accepted.  ON by default
+    (K8S_BLASLT_ALGOS=0 disables it).
+
+    The file's ``buckets`` (tools/blaslt_tune_buckets.py) hold, per (N, K),
+    ``[lo, hi, solution]`` rows: a solution is used for M in [lo, hi] only,
+    and was kept only where, registered and re-timed on this call path with
+    cold weights, it was no slower than the heuristic's own choice at lo, mid
+    and hi and >= 3 % faster over the three -- 14 of 76 buckets, mostly where
+    the heuristic's pick misfires just above a tile boundary (down M = 1537:
+    328 -> 177 us).  Replayed on 811 recorded prefill-size steps: 11.68 ->
+    11.46 s (profiles/r2_blaslt_buckets/).  The older one-point ``algos``
+    ladder (tools/blaslt_sweep.py) picked winners of noisy sweeps and applied
+    them up to the next ladder point; it measured slower (profiles/r2_blaslt_ab/)
+    and is still read for other models' files.  No-op without the native
     library GEMM."""
-    if not _native_lib_gemm or os.environ.get("K8S_BLASLT_ALGOS", "0") != "1" or not os.path.exists(path):
+    if not _native_lib_gemm or os.environ.get("K8S_BLASLT_ALGOS", "1") != "1" or not os.path.exists(path):
         return 0
     with open(path) as f:
         d = json.load(f)

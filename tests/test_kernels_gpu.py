@@ -615,6 +615,32 @@ def test_blaslt_tuned_solutions():
         LIN.clear_lib_tuning()
 
 
+def test_blaslt_bucket_registration(monkeypatch):
+    """A solution registered for M in [lo, hi] (k8s_blaslt_set_algo_range: the
+    heuristic's own pick at another M) serves that range only; results inside
+    and outside the bucket match fp32; the shipped 8B table registers."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops._lib import lib
+    torch.manual_seed(12)
+    N, K = 4096, 4096
+    LIN.reserve_lib_workspace(torch.device(dev))
+    idx = lib().k8s_blaslt_heuristic_index(1024, N, K, LIN.BLASLT_WS_BYTES)
+    assert idx >= 0
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    try:
+        LIN.clear_lib_tuning()
+        assert lib().k8s_blaslt_set_algo_range(300, 400, N, K, idx) == 0
+        for M in (299, 300, 350, 400, 401, 777):
+            x = torch.randn(M, K, device=dev).bfloat16()
+            torch.testing.assert_close(LIN.lib_gemm(x, w).float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+        LIN.clear_lib_tuning()
+        monkeypatch.setenv("K8S_BLASLT_ALGOS", "1")
+        assert LIN.load_lib_algos(LIN.lib_algos_path("llama3-8b")) > 0
+    finally:
+        LIN.clear_lib_tuning()
+
+
 @pytest.mark.parametrize("M", [1, 17, 64, 96, 128, 200, 256])
 @pytest.mark.parametrize("N,K,splits", [(4096, 4096, 8), (6144, 4096, 4), (512, 14336, 7), (1280, 8192, 1)])
 @pytest.mark.parametrize("cfg", [4, 8, 13, 14, 16])

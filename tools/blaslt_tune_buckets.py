@@ -47,9 +47,11 @@ def timed(x, w, y, nw, reps=3, iters=6):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--model", default="llama3-8b")
-    ap.add_argument("--edges", default="257,321,385,449,513,641,769,897,1025,1281,1537,2049,3073,4097")
+    ap.add_argument("--edges", default="257,321,385,449,513,641,769,897,1025,1281,1537,1793,2049,2561,3073,3585,"
+                    "4097,5121,6145,8449")
     ap.add_argument("--cands", type=int, default=4)
-    ap.add_argument("--min-gain", type=float, default=1.05)
+    ap.add_argument("--min-gain", type=float, default=1.03)
+    ap.add_argument("--tol", type=float, default=1.02, help="a candidate may not be slower than this at any point")
     ap.add_argument("--emit", action="store_true")
     ap.add_argument("--out", default=None, help="also write the table here (e.g. under gpurun_out/)")
     a = ap.parse_args()
@@ -74,20 +76,27 @@ def main():
             us = (ctypes.c_float * a.cands)()
             n = lib().k8s_blaslt_sweep(ptr(xs[mid]), K, ptr(w), nw, N * K, ptr(ys[mid]), N, mid, N, K, ptr(ws),
                                        L.BLASLT_WS_BYTES, 6, stream_ptr(w), a.cands, idx, us, None)
+            # candidates: the sweep's top solutions at mid, and the heuristic's own
+            # picks at M inside / just above the bucket (its choice is not monotone in M)
+            cands = [int(idx[c]) for c in range(max(n, 0))]
+            for m in sorted({lo, mid, hi, hi + 64, hi + 128, hi + (hi - lo + 1) // 2}):
+                hi_idx = lib().k8s_blaslt_heuristic_index(m, N, K, L.BLASLT_WS_BYTES)
+                if hi_idx >= 0 and hi_idx not in cands:
+                    cands.append(hi_idx)
             best = None
-            for c in range(max(n, 0)):
+            for cid in cands:
                 L.clear_lib_tuning()
-                if lib().k8s_blaslt_set_algo_range(lo, hi, N, K, int(idx[c])) != 0:
+                if lib().k8s_blaslt_set_algo_range(lo, hi, N, K, cid) != 0:
                     continue
                 tc = [timed(xs[m], w, ys[m], nw) for m in pts]
-                if all(t < h for t, h in zip(tc, th)) and (best is None or sum(tc) < sum(best[1])):
-                    best = (int(idx[c]), tc)
+                if all(t <= h * a.tol for t, h in zip(tc, th)) and (best is None or sum(tc) < sum(best[1])):
+                    best = (cid, tc)
             L.clear_lib_tuning()
             keep = best is not None and sum(th) / sum(best[1]) > a.min_gain
             tot_h += sum(th)
             tot_b += sum(best[1]) if keep else sum(th)
             print(f"N {N:6d} K {K:6d} M [{lo:5d},{hi:5d}] heuristic {' / '.join(f'{t:.1f}' for t in th)} us"
-                  + (f"  cand {best[0]} {' / '.join(f'{t:.1f}' for t in best[1])} us ({sum(th) / sum(best[1]):.2f}x)"
+                  + (f"  cand {best[0]} of {len(cands)} {' / '.join(f'{t:.1f}' for t in best[1])} us ({sum(th) / sum(best[1]):.2f}x)"
                      if best else "  no candidate beats it everywhere") + ("  KEEP" if keep else ""), flush=True)
             if keep:
                 table.setdefault(f"{N},{K}", []).append([lo, hi, best[0]])

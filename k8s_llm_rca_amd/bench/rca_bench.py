@@ -279,9 +279,17 @@ def run(args) -> Optional[Dict[str, Any]]:
                    # decode-attention KV blocks read per distinct block (sampled every 32nd graph step)
                    "kv_block_reuse": round(d["kv_read_blocks_sampled"] / max(1, d["kv_unique_blocks_sampled"]), 2),
                    "admit_s": round(d["admit_s"], 3), "post_s": round(d["post_s"], 3),
+                   # measured GEMM tables in use (decode dispatch; hipBLASLt solution buckets registered)
+                   "gemm_dispatch": bool(getattr(eng, "gemm_dispatch", False)),
+                   "blaslt_buckets": int(getattr(eng, "lib_algos", 0) or 0),
                    # K8S_RCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
                    **({k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}
                       if d["eager_gpu_s"] or d["graph_gpu_s"] else {})},
+        # the work behind each timed analysis (sampling varies it run to run by a few %:
+        # compare A/B runs per unit of it, not by the headline alone)
+        "work_per_analysis": {"decode_ctx_ktokens": round(d["decode_ctx_tokens"] / 1e3 / max(1, n_done), 1),
+                              "prefill_tokens": round(d["prefill_tokens"] / max(1, n_done), 1),
+                              "sampled_tokens": round(d["sampled_tokens"] / max(1, n_done), 1)},
         "throughput": {  # rank 0's engine over the timed window
             "prefill_tok_per_s": round(d["prefill_tokens"] / elapsed, 1),
             "decode_tok_per_s": round(d["decode_tokens"] / elapsed, 1),

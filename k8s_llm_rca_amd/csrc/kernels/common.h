@@ -19,6 +19,25 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef uint16_t u16x8 __attribute__((ext_vector_type(8)));
 typedef uint16_t u16x4 __attribute__((ext_vector_type(4)));
 
+// Weight-stream loads into VGPRs: every weight byte is read once per step and
+// never re-read by the launch, so they carry the non-temporal policy (nt), as
+// MI355X_MICROARCH.md measures for weight-streaming decode kernels (34.5 ->
+// 30.6-30.8 us per Llama-3.2-1B layer).  Measured here, interleaved A/B
+// (profiles/r2_nt_ab/): Llama-3-8B per-layer projections at M = 8 / 16 / 32
+// 91.8-93.4 / 93.7-95.9 / 98.7-100.1 us vs 98.1-103.6 / 99.6-100.0 /
+// 103.5-104.3 us with the default policy.  Activations keep the default policy.
+#ifndef K8S_W_NT
+#define K8S_W_NT 1
+#endif
+template <typename V>
+__device__ __forceinline__ V ldw_nt(const void* p) {
+#if K8S_W_NT
+  return __builtin_nontemporal_load(reinterpret_cast<const V*>(p));
+#else
+  return *reinterpret_cast<const V*>(p);
+#endif
+}
+
 __device__ __forceinline__ float bf2f(uint16_t b) { return __uint_as_float(((uint32_t)b) << 16); }
 
 __device__ __forceinline__ uint16_t f2bf(float f) {

@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_mid_kernel(const uint16_t* __res
     for (int nt = 0; nt < NT; ++nt)
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
-        ring[slot][nt][ks] = *reinterpret_cast<const bf16x8*>(wrow[nt] + c * kChunk + 32 * ks);
+        ring[slot][nt][ks] = ldw_nt<bf16x8>(wrow[nt] + c * kChunk + 32 * ks);
   };
   // X: register double buffer, loaded two chunks ahead of its MFMAs (one
   // whole iteration of latency slack before the LDS write that needs it)

@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __
   bf16x8 xa[U][MT], xb[U][MT];
   auto load = [&](bf16x8 (&wf)[U], bf16x8 (&xf)[U][MT], int s0) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) wf[u] = *reinterpret_cast<const bf16x8*>(wrow + (s0 + u) * 32);
+    for (int u = 0; u < U; ++u) wf[u] = ldw_nt<bf16x8>(wrow + (s0 + u) * 32);
 #pragma unroll
     for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __
     s = nblk * U;
   }
   for (; s < nsteps; ++s) {
-    const bf16x8 wf = *reinterpret_cast<const bf16x8*>(wrow + s * 32);
+    const bf16x8 wf = ldw_nt<bf16x8>(wrow + s * 32);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       const bf16x8 xf = *reinterpret_cast<const bf16x8*>(xrow[mt] + s * 32);

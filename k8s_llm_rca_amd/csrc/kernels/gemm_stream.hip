@@ -83,7 +83,7 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
   bf16x8 xq[U][2][MTW];
   auto load_chunk = [&](int slot, int c) {
 #pragma unroll
-    for (int i = 0; i < 2; ++i) ring[slot][i] = *reinterpret_cast<const u16x8*>(wsrc[i] + c * kSC);
+    for (int i = 0; i < 2; ++i) ring[slot][i] = ldw_nt<u16x8>(wsrc[i] + c * kSC);
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
@@ -181,6 +181,17 @@ __device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
+// Weight stream of the LDS-DMA kernel: default cache policy.  The non-temporal
+// policy (nt, bit 2) that speeds the register-path weight loads (ldw_nt, M <= 32:
+// 4-6 % per layer) made this kernel 2-3 % SLOWER at M = 96-192, measured
+// interleaved nt / off / nt / off (profiles/r2_nt_ab/).  K8S_GLDS_W_NT=1 restores it.
+#ifndef K8S_GLDS_W_NT
+#define K8S_GLDS_W_NT 0
+#endif
+__device__ __forceinline__ void glds16_w(const uint16_t* src, uint16_t* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_dst, 16, 0, K8S_GLDS_W_NT ? 2 : 0);
+}
+
 template <int MTW, int NB>
 constexpr int glds_lds_elems() {
   return NB * (kSBN * kSC + 64 * MTW * kSC);
@@ -219,7 +230,7 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
   auto issue = [&](int stage, int c) {
     uint16_t* st = sm + stage * STG;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
+    for (int i = 0; i < 2; ++i) glds16_w(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
 #pragma unroll
     for (int i = 0; i < XPT; ++i) glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
   };

@@ -75,7 +75,7 @@ __global__ void __launch_bounds__(256, 2) grouped_gemm_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int q = tid + 256 * i, row = q >> 3, c = q & 7;
-      sb[i] = *reinterpret_cast<const bf16x8*>(we + (size_t)row * K + k0 + 8 * c);
+      sb[i] = ldw_nt<bf16x8>(we + (size_t)row * K + k0 + 8 * c);
     }
   };
   auto store = [&](int buf) {

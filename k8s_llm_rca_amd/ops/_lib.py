@@ -69,7 +69,9 @@ def lib():
         return _lib
     with _lock:
         if _lib is None:
-            path = _build.hip_lib_path()
+            # K8SRCA_HIP_LIB: an alternate build of the same sources (compile-time
+            # A/Bs, e.g. tools/_nt_ab.sh); the in-tree library otherwise
+            path = os.environ.get("K8SRCA_HIP_LIB") or _build.hip_lib_path()
             if not os.path.exists(path):
                 if os.environ.get("K8SRCA_AUTOBUILD", "1") == "1":
                     _build.build_hip()

@@ -192,9 +192,13 @@ __device__ __forceinline__ void glds16_w(const uint16_t* src, uint16_t* lds_dst)
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_dst, 16, 0, K8S_GLDS_W_NT ? 2 : 0);
 }
 
-template <int MTW, int NB>
+// NF: 16-column fragments per strip (4: 64-column strips, 8: 128-column strips,
+// which halve the X re-reads per weight byte at M ~ 100-256: every workgroup
+// stages all M rows of X for its strip, so X -- not W -- was the larger
+// stream through L2 -> LDS there).
+template <int MTW, int NB, int NF = 4>
 constexpr int glds_lds_elems() {
-  return NB * (kSBN * kSC + 64 * MTW * kSC);
+  return NB * (16 * NF * kSC + 64 * MTW * kSC);
 }
 
 // One workgroup's 64-column strip over one K slice: acc += X[0..M) . W[strip]^T.
@@ -202,22 +206,23 @@ constexpr int glds_lds_elems() {
 // strip's first W row ([N][K] row-major, K-slice offset already applied);
 // nch: 64-deep chunks in the slice; sm: the kernel's one __shared__ array of
 // glds_lds_elems<MTW, NB>() elements.
-template <int MTW, int NB>
+template <int MTW, int NB, int NF = 4>
 __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int ldx, int M,
                                            const uint16_t* __restrict__ wstrip, int K, int nch, uint16_t* sm,
-                                           f32x4 (&acc)[MTW][4]) {
+                                           f32x4 (&acc)[MTW][NF]) {
   constexpr int MP = 64 * MTW;         // X rows staged: 4 waves x MTW 16-row fragments
-  constexpr int WST = kSBN * kSC;      // W stage: 64 rows x 64 k
+  constexpr int WST = 16 * NF * kSC;   // W stage: 16 NF rows x 64 k
   constexpr int STG = WST + MP * kSC;  // elements per stage
   constexpr int XPT = MP * 8 / 256;    // X pieces (DMAs) per thread per chunk
-  constexpr int LPC = 2 + XPT;         // DMAs per thread per chunk
+  constexpr int WPT = NF / 2;          // W pieces (DMAs) per thread per chunk
+  constexpr int LPC = WPT + XPT;       // DMAs per thread per chunk
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int m_base = wv * 16 * MTW;
 
-  const uint16_t* wsrc[2];
+  const uint16_t* wsrc[WPT];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
+  for (int i = 0; i < WPT; ++i) {
     const int p = 256 * i + tid, n = p >> 3, jl = p & 7;
     wsrc[i] = wstrip + (size_t)n * K + 8 * (jl ^ (n & 7));
   }
@@ -230,7 +235,7 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
   auto issue = [&](int stage, int c) {
     uint16_t* st = sm + stage * STG;
 #pragma unroll
-    for (int i = 0; i < 2; ++i) glds16_w(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
+    for (int i = 0; i < WPT; ++i) glds16_w(wsrc[i] + c * kSC, st + (256 * i + 64 * wv) * 8);
 #pragma unroll
     for (int i = 0; i < XPT; ++i) glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
   };
@@ -246,7 +251,7 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
         xf[mt] = *reinterpret_cast<const bf16x8*>(xs + m * kSC + 8 * ((4 * s + g) ^ (m & 7)));
       }
 #pragma unroll
-      for (int cf = 0; cf < 4; ++cf) {
+      for (int cf = 0; cf < NF; ++cf) {
         const int n = 16 * cf + r;
         const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + n * kSC + 8 * ((4 * s + g) ^ (n & 7)));
 #pragma unroll
@@ -278,8 +283,8 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
 
 // acc[mt][cf][v] = C[m_base + 16 mt + 4 g + v][16 cf + r] of the tile: bf16 rows
 // of y (final) or fp32 rows of `part` (split-K partial), rows < M only.
-template <int MTW>
-__device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][4], int M, uint16_t* __restrict__ y, int ldy,
+template <int MTW, int NF = 4>
+__device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][NF], int M, uint16_t* __restrict__ y, int ldy,
                                            float* __restrict__ pp, int ldp) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -292,7 +297,7 @@ __device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][4], int M, ui
       const int m = m_base + 16 * mt + 4 * g + v;
       if (m < M) {
 #pragma unroll
-        for (int cf = 0; cf < 4; ++cf) {
+        for (int cf = 0; cf < NF; ++cf) {
           if (pp)
             pp[(size_t)m * ldp + 16 * cf + r] = acc[mt][cf][v];
           else
@@ -302,23 +307,23 @@ __device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][4], int M, ui
     }
 }
 
-template <int MTW, int NB>
+template <int MTW, int NB, int NF>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                         int ldy, float* __restrict__ part, int M, int N, int K,
                                                         int kslice) {
-  __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<MTW, NB>()];
-  const int n0 = blockIdx.x * kSBN, split = blockIdx.y, kbeg = split * kslice;
-  f32x4 acc[MTW][4];
+  __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<MTW, NB, NF>()];
+  const int n0 = blockIdx.x * 16 * NF, split = blockIdx.y, kbeg = split * kslice;
+  f32x4 acc[MTW][NF];
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
-    for (int cf = 0; cf < 4; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  glds_strip<MTW, NB>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc);
+    for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
+  glds_strip<MTW, NB, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc);
   if (gridDim.y == 1)
-    glds_store<MTW>(acc, M, y + n0, ldy, nullptr, 0);
+    glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0);
   else
-    glds_store<MTW>(acc, M, nullptr, 0, part + (size_t)split * M * N + n0, N);
+    glds_store<MTW, NF>(acc, M, nullptr, 0, part + (size_t)split * M * N + n0, N);
 }
 
 // MoE grouped form (B13, decode batches): rows offsets[e] .. offsets[e+1] of x
@@ -379,10 +384,11 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_kernel(const float* __
   *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + n) = o;
 }
 
-template <int MTW, int NB>
+template <int MTW, int NB, int NF = 4>
 static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
                               int ldy, float* part, int M, int N, int K, int kslice) {
-  hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K, kslice);
+  hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K,
+                     kslice);
   return hipGetLastError();
 }
 
@@ -398,22 +404,25 @@ static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int
 using namespace k8s;
 
 // cfg: register-ring depth U (4 or 8), or 10 + NB for the LDS-DMA kernel (NB = 3..6
-// stages; 5 and 6 for M <= 64).  splits > 1 needs `part` = splits * M * N fp32;
-// reduce = 0 leaves the partials for a fused consumer.
+// stages; 5 and 6 for M <= 64), or 20 + NB for the LDS-DMA kernel on 128-column
+// strips (NB = 3, or 4 for M <= 192; N % 128 == 0).  splits > 1 needs `part` =
+// splits * M * N fp32; reduce = 0 leaves the partials for a fused consumer.
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, bool reduce, hipStream_t s) {
-  if (M <= 0 || M > 256 || N % kSBN || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
-      (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16)) || ldx % 8 || (splits > 1 && (M * N) % 8) ||
-      (splits == 1 && ldy < N))
+  const int bn = cfg > 20 ? 128 : kSBN;  // strip width
+  if (M <= 0 || M > 256 || N % bn || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
+      (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24) || ldx % 8 ||
+      (splits > 1 && (M * N) % 8) || (splits == 1 && ldy < N))
     return (int)hipErrorInvalidValue;
   const int kslice = K / splits;
   // the register-ring loop is unrolled by U chunks with no partial trip
   if (cfg < 10 && (kslice / kSC) % cfg) return (int)hipErrorInvalidValue;
   const int mtw = ((M + 15) / 16 + 3) / 4;  // 16-row fragments per wave (4 waves)
   // LDS-DMA stages of (64 + 64 * mtw) x 64 bf16 must fit the 160 KB of LDS
-  if ((cfg == 14 && mtw > 3) || (cfg > 14 && mtw > 1)) return (int)hipErrorInvalidValue;
+  if ((cfg == 14 && mtw > 3) || (cfg > 14 && cfg < 20 && mtw > 1) || (cfg == 24 && mtw > 3))
+    return (int)hipErrorInvalidValue;
   if (cfg == 8 && mtw > 2) return (int)hipErrorInvalidValue;  // an 8-deep X ring would not fit the VGPRs
-  const dim3 grid(N / kSBN, splits);
+  const dim3 grid(N / bn, splits);
   const uint16_t* xx = (const uint16_t*)x;
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
@@ -421,7 +430,21 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   hipError_t e;
 #define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
 #define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
-  if (cfg == 13) {
+#define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
+  if (cfg == 23) {
+    switch (mtw) {
+      case 1: K8S_GW(1, 3); break;
+      case 2: K8S_GW(2, 3); break;
+      case 3: K8S_GW(3, 3); break;
+      default: K8S_GW(4, 3); break;
+    }
+  } else if (cfg == 24) {
+    switch (mtw) {
+      case 1: K8S_GW(1, 4); break;
+      case 2: K8S_GW(2, 4); break;
+      default: K8S_GW(3, 4); break;
+    }
+  } else if (cfg == 13) {
     switch (mtw) {
       case 1: K8S_GL(1, 3); break;
       case 2: K8S_GL(2, 3); break;
@@ -454,6 +477,7 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   }
 #undef K8S_SL
 #undef K8S_GL
+#undef K8S_GW
   if (e != hipSuccess) return (int)e;
   if (splits > 1 && reduce) {
     const int blocks = (M * N / 8 + 255) / 256;

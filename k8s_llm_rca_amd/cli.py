@@ -139,7 +139,8 @@ def cmd_run(args) -> int:
     wall = time.time() - t0
     if eng is not None:
         eng.stop()
-    summary = {"analyses": len(st.results), "wall_s": round(wall, 2), "analyses_per_s": round(st.analyses_per_s, 3),
+    summary = {"analyses": len(st.results), "completed": st.n_ok, "wall_s": round(wall, 2),
+               "analyses_per_s": round(st.analyses_per_s, 3),
                "p50_latency_s": round(st.pct(0.5), 3), "p90_latency_s": round(st.pct(0.9), 3),
                "errors": len(st.errors), "output": args.output}
     if args.output:  # per-stage spans (and engine counters) next to the result file

@@ -225,8 +225,15 @@ class BatchStats:
     errors: List[str]
 
     @property
+    def n_ok(self) -> int:
+        """Analyses that completed; an incident that raised is in ``results`` as
+        an ``{"error": ...}`` record (the batch output keeps one line per input)
+        but is not throughput."""
+        return sum(1 for r in self.results if "error" not in r)
+
+    @property
     def analyses_per_s(self) -> float:
-        return len(self.results) / self.wall_s if self.wall_s > 0 else 0.0
+        return self.n_ok / self.wall_s if self.wall_s > 0 else 0.0
 
     def pct(self, q: float) -> float:
         if not self.latencies:

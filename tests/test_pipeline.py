@@ -102,3 +102,26 @@ def test_failed_run_counts_as_attempt(small_cluster):
     inc = small_cluster.incidents[0]
     r = p.analyze(inc.message, inc)
     assert r["locator_attempts"] == 3 and r["analysis"] == []
+
+
+def test_batch_failed_incidents_are_not_throughput(small_cluster):
+    """An incident whose analysis raises keeps its ``{"error": ...}`` record in
+    the batch output but is not counted as a completed analysis (ADVICE r1:
+    failures that end fast must not inflate analyses/s)."""
+    msgs = list(small_cluster.messages[:4])
+
+    class Boom(RCAPipeline):
+        def analyze(self, message, truth=None):
+            if message == msgs[1]:
+                raise RuntimeError("injected")
+            return super().analyze(message, truth)
+
+    def mk():
+        base = make(small_cluster, oracle)
+        base.__class__ = Boom
+        return base
+
+    st = run_batch(mk, msgs, concurrency=2, truths=small_cluster.incidents[:4])
+    assert len(st.results) == 4 and len(st.errors) == 1
+    assert st.n_ok == 3
+    assert st.analyses_per_s == pytest.approx(3 / st.wall_s)

@@ -16,7 +16,7 @@ from k8s_llm_rca_amd.ops import attention as A  # noqa: E402
 nq, nkv, BS, D = 32, 8, 64, 128
 
 
-def meta_for(ctx, contiguous, dev):
+def meta_for(ctx, contiguous, dev, part=None):
     S = len(ctx)
     nbs = [(c + BS - 1) // BS for c in ctx]
     total = sum(nbs)
@@ -31,7 +31,7 @@ def meta_for(ctx, contiguous, dev):
     meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
                       q_start=torch.tensor(qs, dtype=torch.int32, device=dev), num_seqs=S, decode=True,
                       ctx_lens_host=list(ctx), q_start_host=qs)
-    A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev)
+    A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev, part=part)
     return meta, total
 
 
@@ -39,8 +39,9 @@ def main():
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(0)
     ctx = (torch.randint(3000, 6400, (125,), generator=g)).tolist()
-    for contiguous in (False, True):
-        meta, nb = meta_for(ctx, contiguous, dev)
+    parts = [None] + [int(v) for v in os.environ.get("PROBE_PARTS", "").split(",") if v]
+    for contiguous, part in [(False, None), (True, None)] + [(False, p) for p in parts[1:]]:
+        meta, nb = meta_for(ctx, contiguous, dev, part)
         kc = torch.empty(nb, nkv, BS, D, device=dev, dtype=torch.bfloat16).normal_()
         vc = torch.empty(nb, nkv, D, BS, device=dev, dtype=torch.bfloat16).normal_()
         q = torch.randn(len(ctx), (nq + 2 * nkv) * D, device=dev).bfloat16()
@@ -57,7 +58,7 @@ def main():
         torch.cuda.synchronize()
         us = e0.elapsed_time(e1) / n * 1e3
         by = sum(ctx) * nkv * 512
-        print(f"{'contiguous' if contiguous else 'scattered'}: {us:.1f} us per call (decode + reduce), "
+        print(f"{'contiguous' if contiguous else 'scattered'} part={part}: {us:.1f} us per call (decode + reduce), "
               f"{by / us / 1e6:.2f} TB/s, part {meta.part_size}, items {meta.n_items}", flush=True)
         del kc, vc
 

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstddef>
+#include <cstdlib>
 
 #include "common.h"
 
@@ -157,6 +158,45 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
   }
 }
 
+// Mixed steps (decode rows + prefill chunks): the prefill attention (MFMA-heavy)
+// may run on a side stream concurrently with the decode attention (HBM-bound),
+// both after the layer's RoPE / KV write and before its o projection; the
+// decode kernel then gets at most `overlap_grid` waves (one per SIMD at 1024)
+// so prefill waves can be resident beside it.  K8SRCA_ATTN_OVERLAP=1 enables it
+// (tools/overlap_probe.py measures the pair both ways).  Same kernels, same
+// work items, disjoint outputs: results are bit-identical either way.
+struct Overlap {
+  bool on = false;
+  int grid = 1024;
+  int dev = -1;
+  hipStream_t side = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+};
+
+Overlap& overlap_state() {
+  static thread_local Overlap o;
+  const char* v = std::getenv("K8SRCA_ATTN_OVERLAP");  // read per step: A/B-able in one process
+  o.on = v && v[0] == '1';
+  const char* g = std::getenv("K8SRCA_ATTN_OVERLAP_GRID");
+  o.grid = g && std::atoi(g) > 0 ? std::atoi(g) : 1024;
+  return o;
+}
+
+// side stream + fork/join events of the calling thread's current device
+bool overlap_ready(Overlap& o) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (o.dev == dev && o.side) return true;
+  if (hipStreamCreateWithFlags(&o.side, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&o.fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&o.join, hipEventDisableTiming) != hipSuccess) {
+    o.side = nullptr;
+    return false;
+  }
+  o.dev = dev;
+  return true;
+}
+
 }  // namespace
 
 #define K8S_TRY(call)          \
@@ -181,6 +221,11 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   bool pend = false;  // the previous layer's down projection is still split-K partials
   const bool tp = s.ar_id >= 0;  // row-parallel outputs are partial sums: all-reduce, never defer split-K
   const long n_out = (long)T * H;
+  Overlap& ov = overlap_state();
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  // never inside a graph capture (decode-only steps are the captured ones anyway)
+  const bool ov_ok = ov.on && nd > 0 && nd < T && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+                     cap == hipStreamCaptureStatusNone && overlap_ready(ov);
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
@@ -199,15 +244,24 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
       K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
     }
-    if (nd > 0 && s.d_bt)
-      K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
-                              s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,
-                              s.d_items, s.d_n_items, s.d_n_items_dev, s.d_grid, st));
-    if (nd < T && s.p_bt)
+    const bool dec = nd > 0 && s.d_bt, pre = nd < T && s.p_bt;
+    const bool conc = dec && pre && ov.on && ov_ok;
+    if (conc) {  // prefill attention on the side stream, joined before the o projection
+      K8S_TRY((int)hipEventRecord(ov.fork, st));
+      K8S_TRY((int)hipStreamWaitEvent(ov.side, ov.fork, 0));
+    }
+    if (pre)
       K8S_TRY(k8s_attn_prefill(qkv + (size_t)nd * ld_qkv, ld_qkv, s.kc[l], s.vc[l], s.p_bt, s.p_bt_stride, s.p_ctx,
                                s.p_qs, s.tile[0], s.tile[1], s.tile[2], s.tile[3], s.tile[4], s.tile[5], s.n_tiles,
                                s.merge[0], s.merge[1], s.merge[2], s.merge[3], s.n_merge, s.pf_o, s.pf_ml, s.nq,
-                               s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, st));
+                               s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, conc ? ov.side : st));
+    if (conc) K8S_TRY((int)hipEventRecord(ov.join, ov.side));
+    if (dec)
+      K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
+                              s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,
+                              s.d_items, s.d_n_items, s.d_n_items_dev,
+                              conc ? (s.d_grid < ov.grid ? s.d_grid : ov.grid) : s.d_grid, st));
+    if (conc) K8S_TRY((int)hipStreamWaitEvent(st, ov.join, 0));
     K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
     if (tp) K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
     if (!tp && deferred(s.sel[1], true))

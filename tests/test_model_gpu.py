@@ -166,6 +166,43 @@ def test_layer_executor_bit_identical(graphs, splitk):
         assert torch.equal(a, b)
 
 
+def test_attention_overlap_bit_identical(monkeypatch):
+    """K8SRCA_ATTN_OVERLAP=1: in mixed steps the native executor runs the
+    prefill attention on a side stream beside the decode attention (decode at
+    a capped grid).  Same kernels and work items, disjoint outputs: every
+    step's logits are bit-identical to the serial order."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    runs = []
+    for on in ("0", "1"):
+        monkeypatch.setenv("K8SRCA_ATTN_OVERLAP", on)
+        monkeypatch.setenv("K8SRCA_ATTN_OVERLAP_GRID", "64")  # a small grid: many items per wave
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=512, use_graphs=False,
+                                     temperature=0.0, max_batch_tokens=256))
+        logs = []
+        fwd = eng.model.forward
+
+        def rec(*a, **k):
+            out = fwd(*a, **k)
+            logs.append(out.float().cpu())
+            return out
+        eng.model.forward = rec
+        res = {}
+        for i in range(6):
+            sid = eng.new_sequence()
+            p = eng.tok.system_prefix("s") + eng.tok.message("user", "w%d " % i * (20 + 40 * i)) + \
+                eng.tok.header("assistant")
+            eng.submit(sid, p, None, 12, temperature=0.0, on_done=lambda g, st, i=i: res.__setitem__(i, g))
+        eng.run_until_idle()
+        assert eng.model._exec is not None
+        runs.append((res, logs))
+    (r0, l0), (r1, l1) = runs
+    assert r0 == r1 and len(l0) == len(l1) and len(l0) > 2
+    for a, b in zip(l0, l1):
+        assert torch.equal(a, b)
+
+
 @pytest.mark.parametrize("graphs", [False, True])
 def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
     """A short prefill chunk run as decode-attention rows (one row per token,

@@ -332,8 +332,14 @@ K8S_API int k8s_blaslt_heuristic_index(int M, int N, int K, size_t ws_bytes) {
   if (make_desc(Key{M, N, K, K, N, 0}, &p)) return -1100;
   hipblasLtMatmulHeuristicResult_t res[1];
   int n = 0;
-  if (heuristic(p, ws_bytes, 1, res, &n) || n < 1) return -1200;
-  return hipblaslt_ext::getIndexFromAlgo(res[0].algo);
+  const int rc = heuristic(p, ws_bytes, 1, res, &n);
+  const int idx = (rc || n < 1) ? -1200 : hipblaslt_ext::getIndexFromAlgo(res[0].algo);
+  // a throw-away plan (no kernel was enqueued with it): release its descriptors
+  hipblasLtMatrixLayoutDestroy(p.a);
+  hipblasLtMatrixLayoutDestroy(p.b);
+  hipblasLtMatrixLayoutDestroy(p.c);
+  hipblasLtMatmulDescDestroy(p.desc);
+  return idx;
 }
 
 K8S_API int k8s_blaslt_set_algo(int M, int N, int K, int idx) { return set_algo_range(M, 1 << 30, N, K, idx); }

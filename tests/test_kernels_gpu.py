@@ -247,6 +247,55 @@ def test_paged_decode_multi_token_items(nq, nkv):
     assert torch.equal(outs[0][0], outs[1][0])
 
 
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (64, 8), (8, 1)])
+def test_decode_in_kernel_merge_bit_identical(nq, nkv, monkeypatch):
+    """K8SRCA_DECODE_MERGE=1: the last wave of each (row group, kv head) merges
+    the split-KV partials inside the decode kernel instead of the reduce
+    launch -- bit-identical rows (single rows and multi-token groups), over
+    repeated launches (the arrival counters reset themselves)."""
+    _need_gpu()
+    torch.manual_seed(5)
+    BS = 64
+    runs = [(1000, 6), (254, 6), (60, 3), (5000, 4), (17, 1), (1535, 5), (4700, 1), (3100, 1)]
+    ctx, seq_of, chain = [], [], []
+    for i, (c0, q) in enumerate(runs):
+        for j in range(q):
+            ctx.append(c0 + j + 1)
+            seq_of.append(i)
+            chain.append(j > 0)
+    S = len(ctx)
+    NB = sum((c0 + q + BS - 1) // BS for c0, q in runs) + 4
+    kc, vc = _setup_cache(nkv, BS, NB, dev)
+    perm = torch.randperm(NB)
+    maxb = max((c + BS - 1) // BS for c in ctx)
+    bt_seq, used = [], 0
+    for c0, q in runs:
+        nb = (c0 + q + BS - 1) // BS
+        row = torch.zeros(maxb, dtype=torch.int32)
+        row[:nb] = perm[used:used + nb].int()
+        used += nb
+        bt_seq.append(row)
+    bt = torch.stack([bt_seq[i] for i in seq_of])
+    q = torch.randn(S, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+    scale = 1 / math.sqrt(128)
+    for ch, part in ((None, 256), (np.asarray(chain), 256), (None, None)):
+        meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
+                          q_start=torch.arange(S + 1, dtype=torch.int32, device=dev), num_seqs=S, decode=True,
+                          ctx_lens_host=list(ctx), q_start_host=list(range(S + 1)))
+        A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev, part=part, chain=ch)
+        assert meta.n_parts > 1
+        monkeypatch.setenv("K8SRCA_DECODE_MERGE", "0")
+        ref = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
+        monkeypatch.setenv("K8SRCA_DECODE_MERGE", "1")
+        for grid in (None, 64):  # 64 waves: many items (and tickets) per wave
+            meta.grid_waves = grid or 0
+            for _ in range(3):
+                got = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
+                torch.cuda.synchronize()
+                assert torch.equal(got, ref)
+    monkeypatch.setenv("K8SRCA_DECODE_MERGE", "0")
+
+
 @pytest.mark.parametrize("BS", [64, 32])  # 64: paged-64 32x32x16 kernel; 32: generic kernel
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
 @pytest.mark.parametrize("ctx,qlen", [([7], [7]), ([300, 40], [300, 13]), ([1500, 90, 33], [64, 90, 1]),

@@ -455,7 +455,9 @@ __device__ __forceinline__ void decode_merge_rows(const AttnArgs& a, int seq, in
     for (int p = 0; p < np; ++p) {
       const float m = a.part_ml[(base + p) * 2];
       const float f = (m == -INFINITY) ? 0.f : exp2f(m - M);
-      L += a.part_ml[(base + p) * 2 + 1] * f;
+      // l * f rounded on its own, then added: attn_reduce_kernel stages l * f
+      // through LDS before summing (a contracted fma here would round once less)
+      L += __fmul_rn(a.part_ml[(base + p) * 2 + 1], f);
       const float* po = a.part_o + (base + p) * D + d0;
       const f32x4 v0 = *reinterpret_cast<const f32x4*>(po);
       const f32x4 v1 = *reinterpret_cast<const f32x4*>(po + 4);

@@ -372,6 +372,9 @@ __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
 // most of its waves on nothing when context lengths vary 1k..6k).
 // MFMA row rho = qi * G + g: token qi of the item (decode row seq + qi, q row
 // qrow + qi), q head g of the kv group.
+// SC1: partials stored write-through at agent scope (the in-kernel merge's
+// hand-off needs no release fence then: cdna_hip_programming.md Guideline 16 R1)
+template <bool SC1 = false>
 __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnArgs& a, int seq, int part, int qrow,
                                                 int kvh, bool whole, int nt, int lane) {
   const int r = lane & 15, h = lane >> 4;
@@ -397,11 +400,21 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
     } else {
       const size_t base = ((size_t)(seq + qi) * a.nq + qh) * a.n_parts + part;
       float* po = a.part_o + base * D;
+      if constexpr (SC1) {
 #pragma unroll
-      for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
-      if (r == 0) {
-        a.part_ml[base * 2 + 0] = mr[i];
-        a.part_ml[base * 2 + 1] = lr[i];
+        for (int dt = 0; dt < 8; ++dt)
+          __hip_atomic_store(po + 16 * dt + r, st.o[dt][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (r == 0) {
+          __hip_atomic_store(a.part_ml + base * 2 + 0, mr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_store(a.part_ml + base * 2 + 1, lr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
+        if (r == 0) {
+          a.part_ml[base * 2 + 0] = mr[i];
+          a.part_ml[base * 2 + 1] = lr[i];
+        }
       }
     }
   }
@@ -411,20 +424,24 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
 // seq .. seq + nt - 1, q heads kvh * G .. + G - 1.  Same arithmetic in the same
 // order as attn_reduce_kernel (exact max, then sequential sums over the
 // partitions), so the rows are bit-identical to the separate launch.
-// Hand-off (cdna_hip_programming.md Guideline 16, counter form): every
-// partial-writing wave drains its stores, releases at agent scope and takes a
-// ticket; the wave that draws the last one acquires at agent scope and reads
-// the partials with vector loads (lane-varying addresses); it resets the
-// counter for the next launch.  Four (row, head) pairs per pass, 16 lanes x 8
+// Hand-off (cdna_hip_programming.md Guideline 16, R1 counter form): every
+// partial-writing wave stores its partials write-through (agent-scope atomic
+// stores), drains them and takes a ticket; the wave that draws the last one
+// reads every partial with agent-scope loads (no release or acquire fence: a
+// per-wave release -- an L2 write-back -- made the first form 36 % slower,
+// profiles/r2_decode_merge/); it resets the counter for the next launch.  Four (row, head) pairs per pass, 16 lanes x 8
 // dims each.
+// agent-scope load that bypasses this CU's L1 (reads what other XCDs' write-through stores left)
+__device__ __forceinline__ float ld_sc1(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // Publish this wave's partials and take a ticket: true for the last arriver
 // of the (row group, kv head), which then owes its merge.
 __device__ __forceinline__ bool decode_merge_ticket(const AttnArgs& a, int seq, int kvh, int nt, int part_size,
                                                     int lane) {
   const int np_grp = (a.ctx_lens[seq + nt - 1] + part_size - 1) / part_size;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partials have landed
   int ticket = 0;
   if (lane == 0)
     ticket = __hip_atomic_fetch_add(a.merge_cnt + seq * a.nkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -446,26 +463,21 @@ __device__ __forceinline__ void decode_merge_rows(const AttnArgs& a, int seq, in
     const size_t base = ((size_t)row * a.nq + qh) * a.n_parts;
     // exact max over the partitions: lane sub covers p = sub, sub + 16, ...
     float M = -INFINITY;
-    for (int p = sub; p < np; p += 16) M = fmaxf(M, a.part_ml[(base + p) * 2]);
+    for (int p = sub; p < np; p += 16) M = fmaxf(M, ld_sc1(a.part_ml + (base + p) * 2));
 #pragma unroll
     for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
     float L = 0.f, acc[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) acc[i] = 0.f;
     for (int p = 0; p < np; ++p) {
-      const float m = a.part_ml[(base + p) * 2];
+      const float m = ld_sc1(a.part_ml + (base + p) * 2);
       const float f = (m == -INFINITY) ? 0.f : exp2f(m - M);
       // l * f rounded on its own, then added: attn_reduce_kernel stages l * f
       // through LDS before summing (a contracted fma here would round once less)
-      L += __fmul_rn(a.part_ml[(base + p) * 2 + 1], f);
+      L += __fmul_rn(ld_sc1(a.part_ml + (base + p) * 2 + 1), f);
       const float* po = a.part_o + (base + p) * D + d0;
-      const f32x4 v0 = *reinterpret_cast<const f32x4*>(po);
-      const f32x4 v1 = *reinterpret_cast<const f32x4*>(po + 4);
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        acc[i] += v0[i] * f;
-        acc[4 + i] += v1[i] * f;
-      }
+      for (int i = 0; i < 8; ++i) acc[i] += ld_sc1(po + i) * f;
     }
     if (live) {
       u16x8 ov;
@@ -513,7 +525,7 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
     RowState st;
     init_state(st, a, qrow + (valid ? qi : 0), kvh * a.G + (valid ? r - qi * a.G : 0), valid, lane);
     decode_stream64(st, a, blkv, kvh, k0, k1, kmin, lim, lane);
-    decode_epilogue(st, a, seq, part, qrow, kvh, whole, nt, lane);
+    decode_epilogue<MERGE>(st, a, seq, part, qrow, kvh, whole, nt, lane);
     if (MERGE && !whole && decode_merge_ticket(a, seq, kvh, nt, part_size, lane)) {
       if (n_owed < 64) {
         if (lane == 0) {
@@ -523,15 +535,16 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
         }
         ++n_owed;
       } else {  // (never at decode batch sizes) merge at once
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         decode_merge_rows(a, seq, kvh, qrow, nt, part_size, lane);
       }
     }
   }
   if (!MERGE || n_owed == 0) return;
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  // every load of a handed-off partial is an agent-scope (sc1) load: no acquire
+  // fence, only a compiler barrier (Guideline 16, "Valid forms")
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   for (int i = 0; i < n_owed; ++i) {
     const int e1 = owed[3 * i + 1];
     decode_merge_rows(a, owed[3 * i], e1 & 0xFF, owed[3 * i + 2], e1 >> 8, part_size, lane);

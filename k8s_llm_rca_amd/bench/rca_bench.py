@@ -46,9 +46,16 @@ def _thread_cpu() -> Dict[str, float]:
     names = {t.native_id: t.name for t in threading.enumerate()}
     out: Dict[str, float] = {}
     for tid, cpu in per.items():
-        n = names.get(tid, "other")
+        n = names.get(tid)
+        if n is None:  # a native thread (HIP runtime, torch / OpenMP pools): its kernel-side name
+            try:
+                with open(f"/proc/self/task/{tid}/comm") as f:
+                    n = "native:" + "".join(c for c in f.read().strip() if not c.isdigit()).rstrip("-_:")
+            except OSError:
+                n = "native:?"
         g = "engine" if n == "llm-engine" else "graph_batcher" if n == "graph-batcher" else \
-            "pipelines" if n == "rca-stream" else "main" if n == "MainThread" else "other"
+            "pipelines" if n == "rca-stream" else "main" if n == "MainThread" else \
+            n if n.startswith("native:") else "other"
         out[g] = out.get(g, 0.0) + cpu
     return out
 
@@ -117,20 +124,6 @@ def run(args) -> Optional[Dict[str, Any]]:
     deadline = t_start + args.time_budget if args.time_budget else None
     n_steps, n_warm, quantum, conc = args.steps, args.warmup, args.quantum, args.incidents
     nh_steps = 0 if args.no_hints else args.no_hints_steps
-    # distinct incidents: enough that no two concurrent pipelines share one, capped
-    # so the injected faults stay within the graph-size target (the stream cycles them)
-    need = (n_warm + n_steps + nh_steps) * quantum + 2 * conc
-    n_inc = max(1, min(need, int(0.3 * args.graph_nodes / NODES_PER_INCIDENT)))
-    cluster = generate_cluster(args.graph_nodes, n_inc, seed=args.seed + 7919 * rank)
-    batchers = []
-    if cuda and not args.no_graph_device:
-        # both graphs resident in HBM; every pipeline's CONTAINS / STATE / var-length
-        # operator calls coalesced into one HIP launch per op (graph/batcher.py)
-        from ..graph.batcher import enable_batching
-        from ..graph.device import to_device
-        for g in (cluster.stategraph, cluster.metagraph):
-            to_device(g, device)
-            batchers.append(enable_batching(g))
     pc = None
     tp_mode = args.tp > 1
     if tp_mode:
@@ -147,17 +140,47 @@ def run(args) -> Optional[Dict[str, Any]]:
                                  seed=args.seed + (0 if tp_mode else rank),
                                  num_blocks=None if cuda else 512), pc)
     if tp_mode and rank > 0:
-        eng.serve_worker()  # replays every step rank 0 schedules
+        eng.serve_worker()  # replays every step rank 0 schedules (no graph, no pipelines on this rank)
         return None
+    # distinct incidents: enough that no two concurrent pipelines share one, capped
+    # so the injected faults stay within the graph-size target (the stream cycles them)
+    need = (n_warm + n_steps + nh_steps) * quantum + 2 * conc  # pre-aging cycles them too
+    n_inc = max(1, min(need, int(0.3 * args.graph_nodes / NODES_PER_INCIDENT)))
+    cluster = generate_cluster(args.graph_nodes, n_inc, seed=args.seed + 7919 * rank)
+    batchers = []
+    if cuda and not args.no_graph_device:
+        # both graphs resident in HBM; every pipeline's CONTAINS / STATE / var-length
+        # operator calls coalesced into one HIP launch per op (graph/batcher.py)
+        from ..graph.batcher import enable_batching
+        from ..graph.device import to_device
+        for g in (cluster.stategraph, cluster.metagraph):
+            to_device(g, device)
+            batchers.append(enable_batching(g))
     eng.start()
-    svc = AssistantService(EngineBackend(eng, temperature=args.temperature))
+    backend = EngineBackend(eng, temperature=args.temperature)
+    svc = AssistantService(backend)
     budget = GenerationBudget(semantic_tokens=args.semantic_tokens, explanation_tokens=args.explanation_tokens,
                               conclusion_tokens=args.conclusion_tokens, resolution_tokens=args.resolution_tokens)
     cfg = RCAConfig(model=args.model, hints=not args.no_hints, budget=budget)
     meta_qe = GraphQueryExecutor(cluster.metagraph)
     state_qe = GraphQueryExecutor(cluster.stategraph)
     pipelines = [RCAPipeline(svc, meta_qe, state_qe, cfg) for _ in range(conc)]
+    stream = IncidentStream(pipelines, cluster.incidents, hints=not args.no_hints)
     setup_s = time.perf_counter() - t_start
+    # ---- thread regime: the reference keeps ONE set of three threads per driver and
+    # pushes every incident of its CSV through them (test_with_file.py:28-38,64), so
+    # a steady-state analysis runs against a long history cut at the model window.
+    # Each pipeline's threads are pre-aged with --thread-age prior incidents of the
+    # stream (the pipeline's own prompts and graph queries; replies drawn on the host
+    # through the same grammars: EngineBackend.set_replay) -- their KV is built by
+    # the engine's real prefill on each thread's first run, inside the warm-up.
+    t_age = time.perf_counter()
+    if args.thread_age > 0:
+        backend.set_replay(True, seed=args.seed + 104729 * rank)
+        stream.pre_age(args.thread_age)
+        backend.set_replay(False)
+    age_s = time.perf_counter() - t_age
+    ctx_aged = backend.thread_stats()
 
     last = [time.perf_counter()]
 
@@ -170,10 +193,12 @@ def run(args) -> Optional[Dict[str, Any]]:
             print(f"[bench] t={now - t_start:.0f}s completed={stream.n_ok} errors={stream.n_err} "
                   f"engine_steps={eng.stats['steps']}", file=sys.stderr, flush=True)
 
-    # ---- warm-up: W quanta of completed analyses from the running stream
-    stream = IncidentStream(pipelines, cluster.incidents, hints=not args.no_hints)
+    # ---- warm-up: every pipeline completes an engine analysis on its aged threads
+    # (their history prefill is done and they run at steady-state context), and at
+    # least W quanta complete in all
     stream.start()
-    truncated = not stream.wait_ok(n_warm * quantum, deadline, _poll)
+    truncated = not (stream.wait_each(1, deadline, _poll) and stream.wait_ok(n_warm * quantum, deadline, _poll))
+    warm_s = time.perf_counter() - t_age - age_s
     tracing.reset()
     if not args.no_gc_freeze:
         # the graph store, model config, grammar tables and warm-up results are
@@ -188,6 +213,8 @@ def run(args) -> Optional[Dict[str, Any]]:
     _barrier(sync_world, device)
     stats0 = dict(eng.stats)
     eng.kv.reset_peak()
+    age0 = [p.n_analyses for p in pipelines]
+    ctx0 = backend.thread_stats()
     t_wall0 = time.time()
     cpu0 = _thread_cpu()
     t0 = time.perf_counter()
@@ -195,6 +222,7 @@ def run(args) -> Optional[Dict[str, Any]]:
     done_all = stream.wait_ok(base + n_steps * quantum, deadline, _poll)
     t_end = time.perf_counter()
     cpu1 = _thread_cpu()
+    ctx1 = backend.thread_stats()
     n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
@@ -268,6 +296,16 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "recomputed_after_truncation": d["recompute_tokens"],
                    "decode_rows": d["decode_tokens"]},
         "no_hints": nh,
+        # which regime the window measures: thread age (incidents each pipeline's
+        # three threads carry, replayed + engine-run) and the threads' live context
+        "thread_regime": {
+            "replayed_incidents_per_pipeline": args.thread_age,
+            "incidents_at_t0": {"min": min(age0) if age0 else 0,
+                                "mean": round(sum(age0) / max(1, len(age0)), 2)},
+            "context_tokens_at_t0": ctx0, "context_tokens_at_end": ctx1,
+            "truncations_in_window": ctx1.get("truncations", 0) - ctx0.get("truncations", 0),
+            "mean_decode_context": round(d["decode_ctx_tokens"] / max(1, d["decode_tokens"]), 1),
+            "replay_s": round(age_s, 1), "warmup_s": round(warm_s, 1)},
         "engine": {"steps": d["steps"], "graph_steps": d["graph_steps"],
                    "forward_s": round(d["forward_s"], 3), "sample_s": round(d["sample_s"], 3),
                    "host_s": round(d["host_s"], 3), "evictions": d["evictions"],
@@ -325,6 +363,10 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--steps", type=int, default=10, help="timed steps; one step = --quantum completed analyses per GPU")
     p.add_argument("--warmup", type=int, default=3, help="untimed steps streamed before the timer starts")
     p.add_argument("--quantum", type=int, default=16, help="completed analyses per GPU per step")
+    p.add_argument("--thread-age", type=int, default=12,
+                   help="prior incidents replayed into every pipeline's threads before the stream starts "
+                        "(the reference reuses one set of threads for a whole batch); 12 puts every "
+                        "locator / generator / analyzer thread past its first cut at the model window")
     p.add_argument("--time-budget", type=float, default=360.0,
                    help="seconds after start at which the stream stops waiting and the JSON is printed anyway "
                         "(flagged truncated_by_time_budget); 0 = none")
@@ -356,7 +398,7 @@ def parser() -> argparse.ArgumentParser:
 PRESETS: Dict[str, Dict[str, Any]] = {
     # "OPT-125m CPU backend, 10-node toy k8s dependency graph, single pod-crash RCA (plumbing, no GPU)"
     "opt125m-cpu-toy": dict(model="opt-125m", device="cpu", graph_nodes=10, incidents=1, quantum=1, steps=1,
-                            warmup=0, no_hints_steps=0, time_budget=0),
+                            warmup=0, no_hints_steps=0, time_budget=0, thread_age=0),
     # the headline: "RCA analyses/sec + p50 latency, Llama-3-8B backend, 10k-node graph"
     "llama3-8b-10k": dict(model="llama3-8b", graph_nodes=10_000),
     # "Llama-3-8B TP=1 bf16 on one MI355X, 1k-node synthetic k8s graph"

@@ -84,6 +84,7 @@ class RCAPipeline:
         self.generator = GQ.setup_cypher_generator(service, m)
         self.analyzer = CS.setup_state_semantic_analyzer(service, m)
         self.last_failed_runs = 0  # LLM runs of the last analyze() that failed / expired / were cancelled
+        self.n_analyses = 0  # incidents this pipeline's three threads have carried (thread age)
 
     # ------------------------------------------------------------ formats
     def _locator_fmt(self, src: str, truth) -> Any:
@@ -175,6 +176,7 @@ class RCAPipeline:
                     analysis["statepath"].append(sp)
             result["analysis"].append(analysis)
         t1 = time.time()
+        self.n_analyses += 1
         self.last_failed_runs = sum(
             1 for a in (self.locator, self.generator, self.analyzer)
             for run in self.service.list_runs(a.thread.id, limit=64)
@@ -312,10 +314,48 @@ class IncidentStream:
         self.n_abandoned = 0
         self.errors: List[str] = []
         self._threads: List[threading.Thread] = []
+        self.ok_by_pipeline: List[int] = [0] * len(pipelines)  # successful stream analyses per pipeline
+
+    def pre_age(self, n: int, workers: int = 8) -> None:
+        """Drive every pipeline through ``n`` incidents of the stream's source
+        before :meth:`start` (the stream then continues with the incidents
+        after them), so its threads carry ``n`` incidents of history -- the
+        reference's regime, where one driver pushes every incident of its CSV
+        through the same three threads (``test_with_file.py:28-38,64``).  The
+        caller puts the backend in replay mode first (``EngineBackend.set_replay``)."""
+        jobs: "queue.Queue" = queue.Queue()
+        for p in self.pipelines:
+            jobs.put(p)
+        errs: List[BaseException] = []
+
+        def work():
+            while True:
+                try:
+                    p = jobs.get_nowait()
+                except queue.Empty:
+                    return
+                for _ in range(n):
+                    with self._cv:
+                        i = self._next
+                        self._next += 1
+                    inc = self.incidents[i % len(self.incidents)]
+                    try:
+                        p.analyze(inc.message, inc if self.hints else None)
+                    except BaseException as e:  # noqa: BLE001 - re-raised below
+                        errs.append(e)
+                        return
+
+        ths = [threading.Thread(target=work, daemon=True, name="rca-preage") for _ in range(max(1, workers))]
+        for t in ths:
+            t.start()
+        for t in ths:
+            t.join()
+        if errs:
+            raise errs[0]
 
     def start(self) -> None:
-        for p in self.pipelines:
-            t = threading.Thread(target=self._worker, args=(p,), daemon=True, name="rca-stream")
+        for j, p in enumerate(self.pipelines):
+            t = threading.Thread(target=self._worker, args=(p, j), daemon=True, name="rca-stream")
             t.start()
             self._threads.append(t)
 
@@ -332,7 +372,7 @@ class IncidentStream:
             t.join(max(0.0, end - time.perf_counter()))
         return not any(t.is_alive() for t in self._threads)
 
-    def _worker(self, p: RCAPipeline) -> None:
+    def _worker(self, p: RCAPipeline, j: int) -> None:
         while True:
             with self._cv:
                 if self._stop:
@@ -358,6 +398,7 @@ class IncidentStream:
                 self.done.append((t1, t1 - t, ok))
                 if ok:
                     self.n_ok += 1
+                    self.ok_by_pipeline[j] += 1
                 else:
                     self.n_err += 1
                     self.errors.append(err)
@@ -369,6 +410,19 @@ class IncidentStream:
         re-raise an engine fault)."""
         with self._cv:
             while self.n_ok < n:
+                if deadline is not None and time.perf_counter() >= deadline:
+                    return False
+                self._cv.wait(0.5)
+                if poll is not None:
+                    poll()
+            return True
+
+    def wait_each(self, n_each: int, deadline: Optional[float] = None,
+                  poll: Optional[Callable[[], None]] = None) -> bool:
+        """Block until every pipeline has completed ``n_each`` analyses of the
+        stream (False at ``deadline``)."""
+        with self._cv:
+            while min(self.ok_by_pipeline, default=n_each) < n_each:
                 if deadline is not None and time.perf_counter() >= deadline:
                     return False
                 self._cv.wait(0.5)

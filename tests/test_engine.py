@@ -456,3 +456,54 @@ def test_tiny_chunks_as_decode_rows_match_prefill_path():
         tiny.append(eng.stats["tiny_chunk_tokens"])
     assert tiny[0] == 0 and tiny[1] > 0
     assert outs[0] == outs[1]
+
+
+def test_replay_pre_aging_builds_thread_history():
+    """Pre-aging (bench --thread-age): replayed runs complete on the host with
+    grammar-valid replies of budget length, grow and cut the thread at the
+    window like engine runs, and the thread's first engine run afterwards
+    prefills the whole replayed history (KV built by the real forward)."""
+    from k8s_llm_rca_amd.api.assistant import GenericAssistant
+    from k8s_llm_rca_amd.api.service import AssistantService
+    from k8s_llm_rca_amd.engine.backend import EngineBackend
+    eng = _engine(max_context=600, num_blocks=128)
+    be = EngineBackend(eng, default_max_tokens=16, keep_seed=1)
+    svc = AssistantService(be)
+    a = GenericAssistant(svc)
+    a.create_assistant("You are terse.", "t", "tiny-llama")
+    a.create_thread()
+    a.add_message("seed message that must survive")
+    b = F.GenerationBudget(explanation_tokens=5, conclusion_tokens=7, resolution_tokens=9)
+    be.set_replay(True, seed=3)
+    for i in range(10):
+        a.add_message(f"incident {i} " + "detail " * 30)
+        a.run_assistant(max_tokens=64, response_format=F.summary_grammar(["Pod", "Secret"], b, "Secret"))
+        m = a.wait_get_last_k_message(1, timeout=5)
+        j = json.loads(m.data[0].content[0].text.value)  # grammar-valid JSON, hints followed
+        assert {e["kind"] for e in j["summary"]} == {"Pod", "Secret"}
+        assert [e["relevance_score"] for e in j["summary"] if e["kind"] == "Secret"] == ["10"]
+    assert eng.stats["requests"] == 0  # nothing ran on the engine
+    st = svc.threads[a.thread.id].backend_state
+    assert st.truncations > 0 and st.dropped > 0 and 300 < st.prompt_len <= 600
+    gen = be._gen_tokens  # reply ids kept for the thread's assistant segments
+    assert len(gen) == 1  # earlier ones were consumed when the next prompt was built
+    be.set_replay(False)
+    a.add_message("incident after replay")
+    eng.start()
+    try:
+        a.run_assistant(max_tokens=8)
+        assert a.wait_get_last_k_message(1, timeout=120) is not None
+    finally:
+        eng.stop()
+    assert eng.stats["prefill_tokens"] >= st.prompt_len - 8  # the replayed history was prefilled
+    ts = be.thread_stats()
+    assert ts["threads"] == 1 and ts["truncated_threads"] == 1
+
+
+def test_replay_free_text_runs_to_budget():
+    from k8s_llm_rca_amd.engine.backend import _Replay
+    tok = get_tokenizer()
+    rt = GrammarRuntime(tok, 128256)
+    rep = _Replay(rt, [tok.eot_id, tok.eos_id], True, seed=0)
+    out = rep.generate(F.semantic_grammar(F.GenerationBudget(semantic_tokens=40)), 64)
+    assert len(out) == 40 and tok.eot_id not in out

@@ -112,6 +112,11 @@ def test_bench_self_spawns_ranks_cpu(tmp_path):
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["steps"] == 2
     assert d["analyses_timed"] == 4 and d["errors"] == 0 and not d["truncated_by_time_budget"]
     assert abs(d["config"]["graph_nodes"] - 300) <= 0.2 * 300
+    # the reference's thread regime: every pipeline's threads carry the replayed
+    # incidents plus at least one engine-run incident when the timer starts
+    reg = d["thread_regime"]
+    assert reg["replayed_incidents_per_pipeline"] == 12 and reg["incidents_at_t0"]["min"] >= 13
+    assert reg["context_tokens_at_t0"]["threads"] == 6 and reg["mean_decode_context"] > 0
 
 
 def test_synth_graph_size_tracks_target():

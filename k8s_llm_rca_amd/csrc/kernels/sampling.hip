@@ -26,8 +26,8 @@
 //   * out_cand (top-k / top-p rows): the rank's highest-v allowed candidates
 //     (v, id, v + G), cand_k per row sorted by (v desc, id asc), padded with
 //     (-inf, -1, -inf); the ranks' lists are all-gathered and combined (ops/sampling.py):
-//     exact for top-k <= cand_k, and for a nucleus that holds <= cand_k
-//     tokens of each shard.
+//     exact for rows with top-k <= cand_k (any top-p: the nucleus lies inside
+//     the top-k set); the engine all-gathers the logits of other filtered rows.
 #include "common.h"
 
 namespace k8s {

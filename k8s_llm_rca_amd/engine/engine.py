@@ -1020,17 +1020,30 @@ class LLMEngine:
     def _sample_rows(self, logits, hdr, flat, rows_a) -> torch.Tensor:
         """Every TP rank: the rows of this step's logits that sample (all when
         ``rows_a`` is empty), then the vocab-parallel sampling."""
+        B, L = int(hdr[0]), int(hdr[1])
+        o = 3 * B + L + 3 * B  # the payload's top_k / top_p columns (host copy: no device read)
+        topk_h = flat[o:o + B]
+        topp_h = flat[o + B:o + 2 * B].view(np.float32)
         if rows_a.size:
             dev, rows_d = self._to_dev([flat, rows_a])
             logits = logits.index_select(0, rows_d.long())
         else:
             dev = self._to_dev([flat])[0]
-        return self._sample_shard(logits, hdr, dev)
+        return self._sample_shard(logits, hdr, dev, topk_h, topp_h)
 
-    def _sample_shard(self, logits, hdr, dev) -> torch.Tensor:
+    def _sample_shard(self, logits, hdr, dev, topk_h: np.ndarray, topp_h: np.ndarray) -> torch.Tensor:
         """Every TP rank: masked Gumbel-max over its vocab shard, then an
         all-gather of the [B, 2] winners (a few bytes per row instead of the
-        [B, vocab] logits)."""
+        [B, vocab] logits).  Which rows filter is read from the host copy of
+        the step's payload, so no rank waits for its GPU here.
+
+        Filtered rows: a top-k row with ``k <= CAND_K`` (any top-p) is exact
+        from the ranks' candidate lists -- its whole top-k set, and so its
+        nucleus and the nucleus mass, is inside them.  Any other filtered row
+        (top-p without such a k, or k > CAND_K) all-gathers its logits row and
+        samples it with the single-device kernel over the full vocabulary
+        (same global-id noise): a nucleus of flat logits can hold thousands of
+        tokens per shard, more than any candidate list."""
         import torch.distributed as dist
         B, L, nr, words = (int(x) for x in hdr)
         o = 0
@@ -1051,21 +1064,51 @@ class LLMEngine:
         table = self._wmask if self._wmask is not None else torch.zeros(1, words, dtype=torch.int32,
                                                                          device=self.device)
         off = self.pc.tp_rank * self.model.vocab_local
-        filt = (topk > 0) | (topp < 1.0)
-        pairs, cand = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
-                                 vocab_off=off, pairs=True, top_k=topk, top_p=topp, candidates=True)
-        # one all-gather of [B, 2 + 3 * CAND_K] per rank: the Gumbel-max winner and,
-        # for top-k / top-p rows, the shard's highest-v candidates (B10 distributed top-k)
-        comm = torch.cat([pairs, cand.view(B, -1)], 1).to(self._comm_device())
+        filt_h = (topk_h > 0) | (topp_h < 1.0)
+        cand_h = filt_h & (topk_h > 0) & (topk_h <= SMP.CAND_K)
+        full_h = np.flatnonzero(filt_h & ~cand_h)
+        cdev = self._comm_device()
+        if cand_h.any():
+            pairs, cand = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists,
+                                     self.vocab, vocab_off=off, pairs=True, top_k=topk, top_p=topp, candidates=True)
+            # one all-gather of [B, 2 + 3 * CAND_K] per rank: the Gumbel-max winner and,
+            # for top-k rows, the shard's highest-v candidates (B10 distributed top-k)
+            comm = torch.cat([pairs, cand.view(B, -1)], 1).to(cdev)
+        else:
+            comm = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
+                              vocab_off=off, pairs=True).to(cdev)
         parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
         dist.all_gather(parts, comm, group=self.pc.tp_group)
         g = torch.stack(parts)
         tok = SMP.combine_pairs(g[:, :, :2].contiguous())
-        if bool(filt.any()):
+        if cand_h.any():
+            sel = torch.from_numpy(cand_h).to(g.device)
             ct = SMP.combine_candidates(g[:, :, 2:].reshape(self.pc.tp_size, B, -1, 3), topk.to(g.device),
                                         topp.to(g.device))
-            tok = torch.where(filt.to(g.device), ct, tok)
-        return tok.to(self.device)
+            tok = torch.where(sel, ct, tok)
+        tok = tok.to(self.device)
+        if full_h.size:
+            tok[torch.from_numpy(full_h).to(self.device)] = self._sample_gathered(
+                logits, full_h, temps, seeds, steps, mask_id, table, list_off, list_len, lists, topk, topp)
+        return tok
+
+    def _sample_gathered(self, logits, rows_h, temps, seeds, steps, mask_id, table, list_off, list_len, lists,
+                         topk, topp) -> torch.Tensor:
+        """Rows ``rows_h``: all-gather their logits shards and sample them over
+        the whole vocabulary with the single-device kernel (every rank computes
+        the same tokens)."""
+        import torch.distributed as dist
+        idx = torch.from_numpy(rows_h.astype(np.int64)).to(self.device)
+        cdev = self._comm_device()
+        shard = logits.index_select(0, idx).float().contiguous().to(cdev)
+        parts = [torch.empty_like(shard) for _ in range(self.pc.tp_size)]
+        dist.all_gather(parts, shard, group=self.pc.tp_group)
+        full = torch.cat(parts, 1).to(self.device)  # rank r holds columns [r * vocab_local, ...)
+
+        def pick(t):
+            return t.index_select(0, idx)
+        return SMP.sample(full, pick(temps), pick(seeds), pick(steps), pick(mask_id), table, pick(list_off),
+                          pick(list_len), lists, self.vocab, top_k=pick(topk), top_p=pick(topp))
 
     def _comm_device(self):
         """Device of the sampling all-gather's tensors: RCCL takes device

@@ -74,7 +74,10 @@ def combine_candidates(cands: torch.Tensor, top_k: torch.Tensor, top_p: torch.Te
     """[tp, B, C, 3] per-rank (v, id, v + G) candidates of top-k / top-p rows ->
     [B] int32 tokens: the same top-k / nucleus rules as the kernel over the
     union of the ranks' candidates, then the max of the kernel's own perturbed
-    scores (identical on every rank)."""
+    scores (identical on every rank).  Exact for rows with ``0 < top_k <=
+    CAND_K``: the whole top-k set, hence the nucleus and its mass, is in the
+    union.  The engine sends every other filtered row through a logits
+    all-gather instead (``LLMEngine._sample_gathered``)."""
     tp, B, C, _ = cands.shape
     allc = cands.permute(1, 0, 2, 3).reshape(B, tp * C, 3)
     v, ids, sc = allc[..., 0], allc[..., 1].round().long(), allc[..., 2]

@@ -146,7 +146,7 @@ def test_tp_engine_generation_matches_tp1(world, name):
     assert a == b and all(len(v) == 12 for v in a.values())
 
 
-@pytest.mark.parametrize("top_k,top_p", [(0, 1.0), (5, 1.0), (20, 0.8), (64, 0.95)])
+@pytest.mark.parametrize("top_k,top_p", [(0, 1.0), (5, 1.0), (20, 0.8), (64, 0.95), (0, 0.9), (100, 1.0), (100, 0.8)])
 def test_tp2_distributed_sampling_with_grammar_matches_tp1(top_k, top_p):
     """Vocab-parallel Gumbel-max sampling (masks keyed by global id; top-k /
     top-p through the per-rank candidate lists, exact for k <= CAND_K) must pick the same tokens as

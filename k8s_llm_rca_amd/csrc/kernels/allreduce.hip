@@ -28,7 +28,11 @@
 // E & 1 -- had completed (stream order).
 // Signals are system-scope release stores into the PEER's flag array, waits
 // are system-scope acquire loads of our own; spins are bounded (wall clock)
-// and record a timeout in STATUS instead of hanging the GPU.
+// and record a timeout in STATUS instead of hanging the GPU.  Once STATUS is
+// set every later wait falls through at once (the communicator is dead: its
+// epochs no longer match the peers'), so a fault costs one timeout, not one
+// per collective; the engine reads STATUS with every sampled step
+// (k8s_ar_status_async, ordered before the token copy) and fails its runs.
 #include <cstring>
 
 #include "common.h"
@@ -71,11 +75,12 @@ __device__ __forceinline__ void ar_wait(unsigned char* own, size_t flags, int wo
   const int t = threadIdx.x;
   if (t < world) {
     uint32_t* f = reinterpret_cast<uint32_t*>(own + flags) + t * AR_MAX_BLOCKS + b;
+    uint32_t* status = reinterpret_cast<uint32_t*>(own + AR_STATUS);
     const uint64_t t0 = wall_clock64();
     while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+      if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
       if (wall_clock64() - t0 > timeout_ticks) {
-        __hip_atomic_store(reinterpret_cast<uint32_t*>(own + AR_STATUS), 1u, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
         break;
       }
       __builtin_amdgcn_s_sleep(2);
@@ -292,6 +297,13 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
     hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
                        (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
   return (int)hipGetLastError();
+}
+
+// STATUS -> *host (pinned), stream-ordered after everything issued before it:
+// read it once an event recorded behind this copy has completed.
+K8S_API int k8s_ar_status_async(int id, int* host, hipStream_t s) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  return (int)hipMemcpyAsync(host, g_ctx[id].peers.base[g_ctx[id].rank] + AR_STATUS, 4, hipMemcpyDeviceToHost, s);
 }
 
 // 0 = healthy, 1 = a wait timed out (a peer never arrived); synchronous read.

@@ -78,14 +78,15 @@ class _LazySample:
 
 class InFlight:
     """A sampled step whose tokens have not been processed on the host yet."""
-    __slots__ = ("seqs", "tok", "tok_host", "event", "t0")
+    __slots__ = ("seqs", "tok", "tok_host", "event", "t0", "status")
 
-    def __init__(self, seqs, tok, tok_host, event, t0):
+    def __init__(self, seqs, tok, tok_host, event, t0, status=None):
         self.seqs = seqs
         self.tok = tok            # [B] int32 on the device (feeds the next forward)
         self.tok_host = tok_host  # [B] int32 host copy (pinned on GPU), valid once `event` completes
         self.event = event
         self.t0 = t0
+        self.status = status      # TP: pinned copy of the xGMI STATUS word, taken before the sampling
 
 
 @dataclass
@@ -285,6 +286,8 @@ class LLMEngine:
                       "tiny_chunk_tokens": 0}
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
+        self._fault: Optional[str] = None  # a dead communicator: every later request fails at admission
+        self._test_stall = False  # tests: a TP worker that receives steps but never executes them
 
     def _workspace_bytes(self) -> int:
         mc = self.mc
@@ -436,6 +439,9 @@ class LLMEngine:
             except BaseException as e:  # surface engine faults as failed runs, never a hang
                 log.exception("engine step failed")
                 self.error = e
+                from ..parallel.xgmi import CommFault
+                if isinstance(e, CommFault):
+                    self._fault = repr(e)
                 self._fail_all(repr(e))
 
     def _fail_all(self, err: str) -> None:
@@ -468,6 +474,10 @@ class LLMEngine:
         for item in inc:
             sid, toks, grammar, max_new, temp, seed, on_done, top_k, top_p = item
             s = seqs[sid]
+            if self._fault is not None:  # the TP communicator is dead: nothing can run any more
+                if on_done:
+                    on_done(None, {"error": self._fault})
+                continue
             if s.req is not None:
                 if s.req.cancelled:  # the cancelled request still drains its in-flight sample: next step
                     deferred.append(item)
@@ -1067,7 +1077,7 @@ class LLMEngine:
         filt_h = (topk_h > 0) | (topp_h < 1.0)
         cand_h = filt_h & (topk_h > 0) & (topk_h <= SMP.CAND_K)
         full_h = np.flatnonzero(filt_h & ~cand_h)
-        cdev = self._comm_device()
+        cdev = self._gather_device()
         if cand_h.any():
             pairs, cand = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists,
                                      self.vocab, vocab_off=off, pairs=True, top_k=topk, top_p=topp, candidates=True)
@@ -1077,18 +1087,16 @@ class LLMEngine:
         else:
             comm = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
                               vocab_off=off, pairs=True).to(cdev)
-        parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
-        dist.all_gather(parts, comm, group=self.pc.tp_group)
-        g = torch.stack(parts)
+        g = self._all_gather(comm)
         tok = SMP.combine_pairs(g[:, :, :2].contiguous())
         if cand_h.any():
-            sel = torch.from_numpy(cand_h).to(g.device)
+            sel = self._h2d(cand_h, g.device)
             ct = SMP.combine_candidates(g[:, :, 2:].reshape(self.pc.tp_size, B, -1, 3), topk.to(g.device),
                                         topp.to(g.device))
             tok = torch.where(sel, ct, tok)
         tok = tok.to(self.device)
         if full_h.size:
-            tok[torch.from_numpy(full_h).to(self.device)] = self._sample_gathered(
+            tok[self._h2d(full_h.astype(np.int64), self.device)] = self._sample_gathered(
                 logits, full_h, temps, seeds, steps, mask_id, table, list_off, list_len, lists, topk, topp)
         return tok
 
@@ -1098,7 +1106,7 @@ class LLMEngine:
         the whole vocabulary with the single-device kernel (every rank computes
         the same tokens)."""
         import torch.distributed as dist
-        idx = torch.from_numpy(rows_h.astype(np.int64)).to(self.device)
+        idx = self._h2d(rows_h.astype(np.int64), self.device)
         cdev = self._comm_device()
         shard = logits.index_select(0, idx).float().contiguous().to(cdev)
         parts = [torch.empty_like(shard) for _ in range(self.pc.tp_size)]
@@ -1109,6 +1117,33 @@ class LLMEngine:
             return t.index_select(0, idx)
         return SMP.sample(full, pick(temps), pick(seeds), pick(steps), pick(mask_id), table, pick(list_off),
                           pick(list_len), lists, self.vocab, top_k=pick(topk), top_p=pick(topp))
+
+    def _h2d(self, a: np.ndarray, device) -> torch.Tensor:
+        """Host array -> ``device`` without a host sync (pinned, non-blocking)."""
+        t = torch.from_numpy(np.ascontiguousarray(a))
+        if device.type == "cuda":
+            return t.pin_memory().to(device, non_blocking=True)
+        return t
+
+    def _gather_device(self):
+        """Where the sampler's per-rank winners are gathered: on the device
+        through the xGMI all-to-all when the TP group has one (no host sync,
+        HIP-graph capturable), else on the group's backend device."""
+        car = self.pc.custom_ar
+        if car is not None and self.device.type == "cuda":
+            return self.device
+        return self._comm_device()
+
+    def _all_gather(self, comm: torch.Tensor) -> torch.Tensor:
+        """[tp, *comm.shape]: every TP rank's ``comm``."""
+        import torch.distributed as dist
+        car = self.pc.custom_ar
+        if car is not None and comm.is_cuda and car.a2a_fits(self.pc.tp_size * (-(-comm.numel() * comm.element_size()
+                                                                                   // 16) * 16)):
+            return car.all_gather(comm)
+        parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
+        dist.all_gather(parts, comm, group=self.pc.tp_group)
+        return torch.stack(parts)
 
     def _comm_device(self):
         """Device of the sampling all-gather's tensors: RCCL takes device
@@ -1157,6 +1192,8 @@ class LLMEngine:
             kind, arrs = self._chan.recv()
             if kind == STOP:
                 return
+            if self._test_stall:  # fault injection: this peer stops arriving at the collectives
+                continue
             if kind == SAMPLE:
                 hdr, flat, rows_a = arrs
                 self._last_tok = self._sample_rows(logits, hdr, flat, rows_a)
@@ -1392,6 +1429,13 @@ class LLMEngine:
         if not lists:
             lists = [0]
         filt = bool((topk > 0).any() or (topp < 1.0).any())
+        status = None
+        car = self.pc.custom_ar if self.pc.tp_size > 1 else None
+        if car is not None and self.device.type == "cuda":
+            # the communicator's STATUS, stream-ordered before this sampling: valid
+            # once the sampled tokens are (_process_tokens checks it first)
+            status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            car.status_async(status)
         if self._dist_sample:
             tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
                                   seeds, steps, temps, topk, topp, rows)
@@ -1417,7 +1461,7 @@ class LLMEngine:
         else:
             host, ev = tok, None
         self.stats["sample_s"] += time.perf_counter() - t0
-        return InFlight(seqs, tok, host, ev, t0)
+        return InFlight(seqs, tok, host, ev, t0, status)
 
     def _process_tokens(self, fl: InFlight, placeholders: bool = False) -> List[int]:
         """Host side of a sampled step: wait for its tokens (not for later GPU
@@ -1427,6 +1471,9 @@ class LLMEngine:
         t1 = time.perf_counter()
         if fl.event is not None:
             fl.event.synchronize()
+        if fl.status is not None and int(fl.status[0]) != 0:
+            from ..parallel.xgmi import CommFault
+            raise CommFault("xGMI collective timed out: a TP peer never arrived (allreduce STATUS set)")
         toks = fl.tok_host.tolist()
         now = time.perf_counter()
         if self._pending_ev:

@@ -27,6 +27,11 @@ log = logging.getLogger(__name__)
 ONE_SHOT_MAX = 512 << 10
 
 
+class CommFault(RuntimeError):
+    """A TP / EP collective timed out on this rank (a peer never arrived):
+    every run in flight on the engine fails, and so does every later one."""
+
+
 def _bind(L) -> None:
     if getattr(L, "_ar_bound", False):
         return
@@ -44,6 +49,7 @@ def _bind(L) -> None:
         "k8s_ar_allreduce_bf16": ([c_int, P, P, c_long, c_int, P], c_int),
         "k8s_ar_alltoall_bf16": ([c_int, P, P, c_long, P], c_int),
         "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
+        "k8s_ar_status_async": ([c_int, P, P], c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -119,6 +125,28 @@ class XgmiAllReduce:
         _check(self.L.k8s_ar_alltoall_bf16(self.id, send.data_ptr(), recv.data_ptr(), chunk, stream_ptr(send)),
                "k8s_ar_alltoall_bf16")
         return recv
+
+    def all_gather(self, x: torch.Tensor) -> torch.Tensor:
+        """[world, *x.shape] = every rank's ``x`` (any dtype: the bytes are
+        moved as bf16 pairs through :meth:`all_to_all` with the row replicated
+        for every destination).  Device-side, no host sync: the TP sampler's
+        winners / candidates travel this way (``LLMEngine._sample_shard``)."""
+        flat = x.contiguous().view(-1).view(torch.uint8)
+        nb = flat.numel()
+        pad = (-nb) % 16
+        if pad:
+            flat = torch.cat([flat, flat.new_zeros(pad)])
+        row = flat.view(torch.bfloat16)
+        send = row.unsqueeze(0).expand(self.world, -1).contiguous()
+        recv = torch.empty_like(send)
+        self.all_to_all(send, recv)
+        out = recv.view(torch.uint8)[:, :nb].contiguous()
+        return out.view(x.dtype).view(self.world, *x.shape)
+
+    def status_async(self, host: torch.Tensor) -> None:
+        """Copy this rank's STATUS word into ``host`` (pinned int32[1]) on the
+        current stream, ordered after the collectives issued before it."""
+        _check(self.L.k8s_ar_status_async(self.id, host.data_ptr(), stream_ptr()), "k8s_ar_status_async")
 
     def a2a_fits(self, nbytes: int) -> bool:
         return nbytes <= 2 * self.max_bytes and (nbytes // 2) % (8 * self.world) == 0

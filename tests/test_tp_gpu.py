@@ -44,19 +44,28 @@ def _worker(rank, world, port, out_dir):
                            temperature=0.0, use_graphs=graphs)
         model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")
         eng = LLMEngine(cfg, pc, model=model)
-        if rank > 0:
-            eng.serve_worker()
-        else:
-            outs = {}
-            for i in range(5):
-                sid = eng.new_sequence()
-                toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "message %d " % i * (3 + 4 * i)) + \
-                    eng.tok.header("assistant")
-                eng.submit(sid, toks, None, 24, temperature=0.0 if i % 2 == 0 else 0.8, seed=3,
-                           on_done=lambda g, st, i=i: outs.__setitem__(i, g))
-            eng.run_until_idle()
-            eng.stop_workers()
-            res[graphs] = {"outs": outs, "graph_steps": eng.stats["graph_steps"], "exec": model._exec is not None}
+        # pass 0 captures every decode bucket; pass 1 replays the same work and, on
+        # the worker, runs under torch's sync checker: a worker step never waits
+        # for its own GPU (its sampling winners travel over the xGMI all-to-all)
+        for p in range(2 if graphs else 1):
+            if rank > 0:
+                if p == 1:
+                    torch.cuda.set_sync_debug_mode("error")
+                eng.serve_worker()
+                torch.cuda.set_sync_debug_mode(0)
+            else:
+                outs = {}
+                for i in range(5):
+                    sid = eng.new_sequence()
+                    toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "message %d " % i * (3 + 4 * i)) \
+                        + eng.tok.header("assistant")
+                    eng.submit(sid, toks, None, 24, temperature=0.0 if i % 2 == 0 else 0.8, seed=3,
+                               on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+                eng.run_until_idle()
+                eng.stop_workers()
+                res[(graphs, p)] = {"outs": outs, "graph_steps": eng.stats["graph_steps"],
+                                    "exec": model._exec is not None}
+            dist.barrier()
         torch.cuda.synchronize()
         dist.barrier()
         del eng, model
@@ -76,7 +85,80 @@ def test_tp2_graph_replay_matches_eager_processes_sharing_one_gpu():
         mp.spawn(_worker, args=(2, _free_port(), d), nprocs=2, join=True)
         res = torch.load(os.path.join(d, "r.pt"), weights_only=True)
     assert res["status"] == 0
-    eager, graph = res[False], res[True]
+    eager, graph, again = res[(False, 0)], res[(True, 0)], res[(True, 1)]
     assert eager["graph_steps"] == 0 and graph["graph_steps"] > 0
     assert graph["exec"] and eager["exec"]
     assert eager["outs"] == graph["outs"] and all(v is not None and len(v) == 24 for v in graph["outs"].values())
+    # the sync-checked pass: same greedy tokens (sampled rows differ: the noise is
+    # keyed by the new sequences' ids), every run complete
+    assert all(again["outs"][i] == graph["outs"][i] for i in (0, 2, 4))
+    assert all(v is not None and len(v) == 24 for v in again["outs"].values())
+
+
+def _stall_worker(rank, world, port, out_dir):
+    """Rank 1 stops arriving at the collectives after the first request: rank
+    0's all-reduce waits time out, STATUS is set, and the engine fails the
+    runs in flight (and every later one) instead of returning wrong tokens."""
+    import time
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    from k8s_llm_rca_amd.parallel.xgmi import CommFault, XgmiAllReduce
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0)
+    cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
+                       temperature=0.0, use_graphs=True)
+    model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")
+    eng = LLMEngine(cfg, pc, model=model)
+    res = {}
+    if rank > 0:
+        eng.serve_worker()       # the healthy request
+        eng._test_stall = True
+        eng.serve_worker()       # receives every later step, executes none
+    else:
+        def run(n, tag):
+            done = {}
+            for i in range(n):
+                sid = eng.new_sequence()
+                toks = eng.tok.system_prefix("sys") + eng.tok.message("user", f"{tag} {i} " * 6) + \
+                    eng.tok.header("assistant")
+                eng.submit(sid, toks, None, 16, seed=3, on_done=lambda g, st, i=i: done.__setitem__(i, (g, st)))
+            t0 = time.time()
+            while len(done) < n and time.time() - t0 < 120:
+                time.sleep(0.05)
+            return done
+        eng.start()
+        ok = run(1, "healthy")
+        eng.stop()
+        eng.stop_workers()       # the worker now stalls
+        eng.start()
+        bad = run(3, "stalled")
+        late = run(1, "late")
+        eng.stop()
+        eng.stop_workers()
+        res = {"ok": [g is not None and len(g) == 16 for g, _ in ok.values()],
+               "bad": [(g is None, st.get("error", "")) for g, st in bad.values()] if len(bad) == 3 else None,
+               "late": [(g is None, st.get("error", "")) for g, st in late.values()],
+               "fault": isinstance(eng.error, CommFault), "status": pc.custom_ar.status()}
+        torch.save(res, os.path.join(out_dir, "stall.pt"))
+    torch.cuda.synchronize()
+    dist.barrier()
+    pc.custom_ar.close()
+    dist.destroy_process_group()
+
+
+def test_tp2_stalled_peer_fails_runs():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_stall_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        res = torch.load(os.path.join(d, "stall.pt"), weights_only=True)
+    assert res["ok"] == [True]
+    assert res["fault"] and res["status"] == 1
+    assert res["bad"] is not None and all(failed for failed, _ in res["bad"]), res["bad"]
+    assert all(failed and "timed out" in err for failed, err in res["late"]), res["late"]

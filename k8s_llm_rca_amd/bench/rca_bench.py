@@ -126,6 +126,12 @@ def run(args) -> Optional[Dict[str, Any]]:
     nh_steps = 0 if args.no_hints else args.no_hints_steps
     pc = None
     tp_mode = args.tp > 1
+    if args.tp_sim > 1:
+        # one rank of a TP=N deployment at real shapes, collectives stood in (parallel/tpsim.py)
+        if not cuda or world > 1 or tp_mode:
+            raise SystemExit("--tp-sim runs ONE process on one GPU")
+        from ..parallel.tpsim import sim_context
+        pc = sim_context(args.tp_sim)
     if tp_mode:
         import torch.distributed as dist
         from ..parallel.groups import ParallelContext, attach_custom_allreduce
@@ -212,6 +218,7 @@ def run(args) -> Optional[Dict[str, Any]]:
     # ---- timed: exactly K quanta of completed analyses, barrier + sync on both sides
     _barrier(sync_world, device)
     stats0 = dict(eng.stats)
+    sim0 = dict(eng.sim_rows)
     eng.kv.reset_peak()
     age0 = [p.n_analyses for p in pipelines]
     ctx0 = backend.thread_stats()
@@ -228,6 +235,23 @@ def run(args) -> Optional[Dict[str, Any]]:
     elapsed = time.perf_counter() - t0
     truncated = truncated or not done_all
     d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
+    sim = None
+    if args.tp_sim > 1:
+        from ..parallel.tpsim import project
+        hist = {T: n - sim0.get(T, 0) for T, n in eng.sim_rows.items() if n - sim0.get(T, 0) > 0}
+        pr = project(hist, pc, eng.mc.hidden, eng.mc.n_layers, device)
+        wall_p = elapsed - pr["standin_s"] + pr["modelled_s"]
+        sim = {"tp": args.tp_sim, "rank": 0,
+               "what": "ONE rank of a TP=%d engine at real shapes on one GPU; every collective is a local "
+                       "stand-in moving the same bytes (parallel/tpsim.py); a projection, not a scaling "
+                       "measurement" % args.tp_sim,
+               "measured_value": round(n_done / elapsed, 4) if elapsed > 0 else 0.0,
+               "standin_collectives_s": round(pr["standin_s"], 3),
+               "modelled_xgmi_collectives_s": round(pr["modelled_s"], 3),
+               "projected_value": round(n_done / wall_p, 4) if wall_p > 0 else 0.0,
+               "projected_ms_per_step": round(1000.0 * wall_p / n_steps, 2),
+               "collective_share_modelled": round(pr["modelled_s"] / wall_p, 4) if wall_p > 0 else 0.0,
+               "per_T": pr["per_T"]}
     gq = {k: 1e3 * v["total_s"] for k, v in tracing.snapshot().items()}
     bstats = [dict(b.stats) for b in batchers]
     lat = stream.window(t0, t_end + 1e-9)
@@ -265,6 +289,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                   "mixtral-8x7b": "Mixtral-8x7B"}.get(args.model, args.model)
     metric = METRIC if (args.model == "llama3-8b" and args.graph_nodes == 10_000) else (
         f"RCA analyses/sec + p50 end-to-end latency, {model_name} backend, {args.graph_nodes}-node graph")
+    if args.tp_sim > 1:
+        metric = f"PROJECTION (rank 0 of TP={args.tp_sim} simulated on one GPU): " + metric
     res = {
         "metric": metric,
         "value": round(value, 4),
@@ -280,7 +306,8 @@ def run(args) -> Optional[Dict[str, Any]]:
         "data": "synthetic k8s stategraph (seeded generator, fault injection) + random-init weights",
         "config": {"model": model_name,
                    "global_batch": conc * sync_world, "seq_len": eng.max_context,
-                   "parallelism": f"tp{world}" if tp_mode else f"dp{world}",
+                   "parallelism": (f"tp{args.tp_sim}-sim-rank0" if args.tp_sim > 1 else
+                                   f"tp{world}" if tp_mode else f"dp{world}"),
                    "graph_nodes": cluster.stategraph.num_nodes, "graph_nodes_target": args.graph_nodes,
                    "distinct_incidents": len(cluster.incidents),
                    "concurrent_analyses_per_gpu": conc, "analyses_per_step": quantum * sync_world,
@@ -296,6 +323,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "recomputed_after_truncation": d["recompute_tokens"],
                    "decode_rows": d["decode_tokens"]},
         "no_hints": nh,
+        "tp_sim": sim,
         # which regime the window measures: thread age (incidents each pipeline's
         # three threads carry, replayed + engine-run) and the threads' live context
         "thread_regime": {
@@ -374,6 +402,9 @@ def parser() -> argparse.ArgumentParser:
                    help="after the timed window, steps measured with the oracle hints off (0 = skip)")
     p.add_argument("--model", default="llama3-8b")
     p.add_argument("--tp", type=int, default=1, help="tensor-parallel degree (one engine over all ranks)")
+    p.add_argument("--tp-sim", type=int, default=0,
+                   help="project a TP=N engine from ONE GPU: rank 0's shard at real shapes, collectives stood "
+                        "in by local kernels moving the same bytes (result line: tp_sim)")
     p.add_argument("--device", default="cuda")
     p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses (pipelines) per GPU")
     p.add_argument("--graph-nodes", type=int, default=10_000)

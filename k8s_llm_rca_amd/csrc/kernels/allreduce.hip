@@ -58,6 +58,8 @@ struct ARCtx {
   long max_bytes;
   uint64_t timeout_ticks;
   bool used;
+  int sim;          // loopback stand-in (tp-sim): every "peer" buffer is local, waits are skipped
+  void* own_alloc;  // loopback: the one allocation holding all `world` buffers
 };
 
 static ARCtx g_ctx[16];
@@ -71,9 +73,9 @@ __device__ __forceinline__ void ar_signal(const ARPeers& P, size_t flags, int wo
 }
 
 __device__ __forceinline__ void ar_wait(unsigned char* own, size_t flags, int world, int b, uint32_t e,
-                                        uint64_t timeout_ticks) {
+                                        uint64_t timeout_ticks, int sim) {
   const int t = threadIdx.x;
-  if (t < world) {
+  if (t < world && !sim) {
     uint32_t* f = reinterpret_cast<uint32_t*>(own + flags) + t * AR_MAX_BLOCKS + b;
     uint32_t* status = reinterpret_cast<uint32_t*>(own + AR_STATUS);
     const uint64_t t0 = wall_clock64();
@@ -109,7 +111,7 @@ __device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off
 template <bool TWO_SHOT>
 __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                                          long n, long slice, int world, int rank, ARPeers P,
-                                                         long max_bytes, uint64_t timeout_ticks) {
+                                                         long max_bytes, uint64_t timeout_ticks, int sim) {
   const int b = blockIdx.x, t = threadIdx.x;
   unsigned char* own = P.base[rank];
   uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
@@ -128,7 +130,7 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
   __threadfence_system();
   __syncthreads();
   ar_signal(P, AR_FLAGS_A, world, rank, b, e);
-  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks);
+  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
 
   if (!TWO_SHOT) {
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
@@ -141,7 +143,7 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
     __threadfence_system();
     __syncthreads();
     ar_signal(P, AR_FLAGS_B, world, rank, b, e);
-    ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks);
+    ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks, sim);
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS) {
       const int owner = (int)((i - i0) / part);
       *reinterpret_cast<u16x8*>(out + i) = *reinterpret_cast<const u16x8*>(P.base[owner] + res + 2 * i);
@@ -169,7 +171,7 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
 // its call e - 2 -- the region's last reader -- completed.
 __global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restrict__ send, uint16_t* __restrict__ recv,
                                                         long chunk, long slice, int world, int rank, ARPeers P,
-                                                        long max_bytes, uint64_t timeout_ticks) {
+                                                        long max_bytes, uint64_t timeout_ticks, int sim) {
   const int b = blockIdx.x, t = threadIdx.x;
   unsigned char* own = P.base[rank];
   uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
@@ -190,7 +192,7 @@ __global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restr
   __threadfence_system();
   __syncthreads();
   ar_signal(P, AR_FLAGS_A, world, rank, b, e);
-  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks);
+  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
   for (int r = 0; r < world; ++r) {
     const unsigned char* srcb = own + half + 2 * ((size_t)r * chunk);
     uint16_t* dst = recv + (size_t)r * chunk;
@@ -224,7 +226,7 @@ K8S_API int k8s_ar_alltoall_bf16(int id, const void* send, void* recv, long chun
   slice = (slice + 7) / 8 * 8;
   nb = (chunk + slice - 1) / slice;
   hipLaunchKernelGGL(a2a_kernel, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)send, (uint16_t*)recv,
-                     chunk, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+                     chunk, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
   return (int)hipGetLastError();
 }
 
@@ -266,14 +268,42 @@ K8S_API int k8s_ar_register(int world, int rank, void** bases, long max_bytes, d
     c.rank = rank;
     c.max_bytes = max_bytes;
     c.timeout_ticks = (uint64_t)(timeout_s * khz * 1000.0);
+    c.sim = 0;
+    c.own_alloc = nullptr;
     c.used = true;
     return id;
   }
   return -1;
 }
 
+// tp-sim: a `world`-rank communicator whose every buffer lives on THIS GPU
+// (one allocation, `world` slots), registered as rank 0 with the waits
+// skipped.  The kernels then move exactly the bytes of the real collective
+// -- stage, signal every "peer", read every "peer" slot -- but over local HBM
+// instead of xGMI: a labelled stand-in for per-rank projections
+// (bench --tp-sim), never a collective.
+K8S_API int k8s_ar_register_loopback(int world, long max_bytes) {
+  if (world < 1 || world > AR_MAX_WORLD || max_bytes % 16) return -1;
+  const size_t per = (size_t)AR_DATA + 8 * (size_t)max_bytes;
+  void* base = nullptr;
+  if (hipMalloc(&base, per * world) != hipSuccess) return -1;
+  if (hipMemset(base, 0, per * world) != hipSuccess) return -1;
+  void* bases[AR_MAX_WORLD];
+  for (int p = 0; p < world; ++p) bases[p] = (unsigned char*)base + per * p;
+  const int id = k8s_ar_register(world, 0, bases, max_bytes, 1.0);
+  if (id < 0) {
+    (void)hipFree(base);
+    return -1;
+  }
+  g_ctx[id].sim = 1;
+  g_ctx[id].own_alloc = base;
+  return id;
+}
+
 K8S_API int k8s_ar_unregister(int id) {
   if (id < 0 || id >= 16) return (int)hipErrorInvalidValue;
+  if (g_ctx[id].own_alloc) (void)hipFree(g_ctx[id].own_alloc);
+  g_ctx[id].own_alloc = nullptr;
   g_ctx[id].used = false;
   return 0;
 }
@@ -292,10 +322,10 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
   nb = (n + slice - 1) / slice;
   if (mode == 2)
     hipLaunchKernelGGL(ar_kernel<true>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
   else
     hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks);
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
   return (int)hipGetLastError();
 }
 

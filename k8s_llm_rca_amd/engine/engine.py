@@ -259,15 +259,17 @@ class LLMEngine:
         # TP: the leader's host work of step n overlaps step n+1 on every rank too
         # (the workers take the sampled tokens from their own device copy)
         self._chan = None
-        if self.pc.tp_size > 1:
+        self._sim = bool(getattr(self.pc, "sim", False))  # tp-sim: rank 0 alone, collectives stood in
+        self.sim_rows: Dict[int, int] = {}  # tp-sim: forwards per row count (collective projection)
+        if self.pc.tp_size > 1 and not self._sim:
             from ..parallel.channel import make_channel
             self._chan = make_channel(self.pc)  # host-side step metadata (parallel/channel.py)
         self._last_tok = None  # TP workers: device tokens of the last sampling (decode inputs of the next step)
         # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
-        self._dist_sample = (self.pc.tp_size > 1 and hasattr(self.model, "vocab_local")
+        self._dist_sample = (self.pc.tp_size > 1 and not self._sim and hasattr(self.model, "vocab_local")
                              and self.model.vocab_local % 8 == 0)
         # TP: every rank needs the sampled tokens on its device to overlap steps
-        self._async = cfg.async_steps and (self.pc.tp_size == 1 or self._dist_sample)
+        self._async = cfg.async_steps and (self.pc.tp_size == 1 or self._dist_sample or self._sim)
         self._mask_sent = 0      # rank 0: mask-table rows already broadcast to the workers
         self._wmask = None       # TP ranks: device copy of the mask table (rows received so far)
         # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
@@ -948,6 +950,8 @@ class LLMEngine:
 
         (_, _, T, nd, n_dec, maxb_d, n_pre, maxb_p, n_tiles, ns, n_parts, n_merge, part,
          n_items) = [int(v) for v in header]
+        if self._sim:
+            self.sim_rows[T] = self.sim_rows.get(T, 0) + 1
         o = 0
 
         def take(n, shape=None):
@@ -1350,6 +1354,8 @@ class LLMEngine:
         row i's input id is ``tok[src[i]]`` where ``src[i] >= 0``."""
         st = self._ensure_static()
         assert mb == self.max_blocks_per_seq
+        if self._sim:
+            self.sim_rows[Bb] = self.sim_rows.get(Bb, 0) + 1
         hi = st["host_i"] = st["host_i"] ^ 1
         if st["host_ev"][hi] is not None:
             st["host_ev"][hi].synchronize()  # its previous upload has long completed in practice

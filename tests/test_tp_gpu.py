@@ -162,3 +162,30 @@ def test_tp2_stalled_peer_fails_runs():
     assert res["fault"] and res["status"] == 1
     assert res["bad"] is not None and all(failed for failed, _ in res["bad"]), res["bad"]
     assert all(failed and "timed out" in err for failed, err in res["late"]), res["late"]
+
+
+def test_tp_sim_rank0_runs_real_kernels_with_standin_collectives():
+    """bench --tp-sim: rank 0 of a TP=4 engine on one GPU (shard shapes, the
+    native executor, HIP graphs, the xGMI kernels on a loopback communicator)
+    generates complete runs, and the projection prices every forward's
+    collectives both as stood in and as modelled."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.parallel.tpsim import project, sim_context
+    pc = sim_context(4)
+    eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64,
+                                 max_batch_tokens=256, temperature=0.8), pc)
+    assert eng.model.nq == 2 and eng.model.inter == 256 and eng._chan is None and not eng._dist_sample
+    outs = {}
+    for i in range(4):
+        sid = eng.new_sequence()
+        toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "sim %d " % i * 9) + eng.tok.header("assistant")
+        eng.submit(sid, toks, None, 20, seed=1, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+    eng.run_until_idle()
+    assert len(outs) == 4 and all(g is not None and len(g) == 20 for g in outs.values())
+    assert eng.model._exec is not None and eng.stats["graph_steps"] > 0 and sum(eng.sim_rows.values()) > 0
+    pr = project(eng.sim_rows, pc, eng.mc.hidden, eng.mc.n_layers, "cuda:0")
+    assert pr["standin_s"] > 0 and pr["modelled_s"] > 0
+    assert pc.custom_ar.status() == 0
+    pc.custom_ar.close()

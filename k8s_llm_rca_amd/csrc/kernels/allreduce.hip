@@ -33,6 +33,7 @@
 // epochs no longer match the peers'), so a fault costs one timeout, not one
 // per collective; the engine reads STATUS with every sampled step
 // (k8s_ar_status_async, ordered before the token copy) and fails its runs.
+#include <cstdlib>
 #include <cstring>
 
 #include "common.h"
@@ -64,11 +65,31 @@ struct ARCtx {
 
 static ARCtx g_ctx[16];
 
-__device__ __forceinline__ void ar_signal(const ARPeers& P, size_t flags, int world, int rank, int b, uint32_t e) {
+// K8SRCA_AR_FENCE_ALL=1: the old publish (a system fence in every wave), for A/B
+static int fence_all() {
+  const char* e = std::getenv("K8SRCA_AR_FENCE_ALL");  // per launch: A/B-able in one process
+  return (e && e[0] == '1') ? 1 : 0;
+}
+
+// Publish this block's stores, then raise its flag in every rank's buffer.
+// Every storing wave drains its own stores (vmcnt(0)) before the barrier; ONE
+// wave then issues ONE system-scope release (the L2 write-back) and the flag
+// stores behind an explicit vmcnt(0) (hipcc can drop the fence's own wait:
+// MI355X_MICROARCH.md "Compiler hazard").  fence_all = the previous form, a
+// system fence in every wave (8 L2 write-backs per block; A/B only).
+__device__ __forceinline__ void ar_publish(const ARPeers& P, size_t flags, int world, int rank, int b, uint32_t e,
+                                           int fence_all) {
   const int t = threadIdx.x;
-  if (t < world) {
-    uint32_t* f = reinterpret_cast<uint32_t*>(P.base[t] + flags) + rank * AR_MAX_BLOCKS + b;
-    __hip_atomic_store(f, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+  if (fence_all) __threadfence_system();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (t < world) {
+      uint32_t* f = reinterpret_cast<uint32_t*>(P.base[t] + flags) + rank * AR_MAX_BLOCKS + b;
+      __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
   }
 }
 
@@ -111,7 +132,8 @@ __device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off
 template <bool TWO_SHOT>
 __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                                          long n, long slice, int world, int rank, ARPeers P,
-                                                         long max_bytes, uint64_t timeout_ticks, int sim) {
+                                                         long max_bytes, uint64_t timeout_ticks, int sim,
+                                                         int fence_all) {
   const int b = blockIdx.x, t = threadIdx.x;
   unsigned char* own = P.base[rank];
   uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
@@ -127,9 +149,7 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
   // 1) stage this rank's slice
   for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
     *reinterpret_cast<u16x8*>(own + data + 2 * i) = *reinterpret_cast<const u16x8*>(in + i);
-  __threadfence_system();
-  __syncthreads();
-  ar_signal(P, AR_FLAGS_A, world, rank, b, e);
+  ar_publish(P, AR_FLAGS_A, world, rank, b, e, fence_all);
   ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
 
   if (!TWO_SHOT) {
@@ -140,9 +160,7 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
     const long p0 = i0 + (long)rank * part, p1 = min(i1, p0 + part);
     for (long i = p0 + 8L * t; i < p1; i += 8L * AR_THREADS)
       *reinterpret_cast<u16x8*>(own + res + 2 * i) = ar_sum8(P, world, data + 2 * i);
-    __threadfence_system();
-    __syncthreads();
-    ar_signal(P, AR_FLAGS_B, world, rank, b, e);
+    ar_publish(P, AR_FLAGS_B, world, rank, b, e, fence_all);
     ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks, sim);
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS) {
       const int owner = (int)((i - i0) / part);
@@ -171,7 +189,8 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
 // its call e - 2 -- the region's last reader -- completed.
 __global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restrict__ send, uint16_t* __restrict__ recv,
                                                         long chunk, long slice, int world, int rank, ARPeers P,
-                                                        long max_bytes, uint64_t timeout_ticks, int sim) {
+                                                        long max_bytes, uint64_t timeout_ticks, int sim,
+                                                        int fence_all) {
   const int b = blockIdx.x, t = threadIdx.x;
   unsigned char* own = P.base[rank];
   uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
@@ -189,9 +208,7 @@ __global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restr
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
       *reinterpret_cast<u16x8*>(dst + 2 * i) = *reinterpret_cast<const u16x8*>(src + i);
   }
-  __threadfence_system();
-  __syncthreads();
-  ar_signal(P, AR_FLAGS_A, world, rank, b, e);
+  ar_publish(P, AR_FLAGS_A, world, rank, b, e, fence_all);
   ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
   for (int r = 0; r < world; ++r) {
     const unsigned char* srcb = own + half + 2 * ((size_t)r * chunk);
@@ -226,7 +243,7 @@ K8S_API int k8s_ar_alltoall_bf16(int id, const void* send, void* recv, long chun
   slice = (slice + 7) / 8 * 8;
   nb = (chunk + slice - 1) / slice;
   hipLaunchKernelGGL(a2a_kernel, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)send, (uint16_t*)recv,
-                     chunk, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
+                     chunk, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
   return (int)hipGetLastError();
 }
 
@@ -285,8 +302,8 @@ K8S_API int k8s_ar_register(int world, int rank, void** bases, long max_bytes, d
 K8S_API int k8s_ar_register_loopback(int world, long max_bytes) {
   if (world < 1 || world > AR_MAX_WORLD || max_bytes % 16) return -1;
   const size_t per = (size_t)AR_DATA + 8 * (size_t)max_bytes;
-  void* base = nullptr;
-  if (hipMalloc(&base, per * world) != hipSuccess) return -1;
+  void* base = nullptr;  // uncached, like the IPC buffers of a real communicator (k8s_ar_alloc)
+  if (hipExtMallocWithFlags(&base, per * world, hipDeviceMallocUncached) != hipSuccess) return -1;
   if (hipMemset(base, 0, per * world) != hipSuccess) return -1;
   void* bases[AR_MAX_WORLD];
   for (int p = 0; p < world; ++p) bases[p] = (unsigned char*)base + per * p;
@@ -322,10 +339,10 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
   nb = (n + slice - 1) / slice;
   if (mode == 2)
     hipLaunchKernelGGL(ar_kernel<true>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
   else
     hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim);
+                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
   return (int)hipGetLastError();
 }
 

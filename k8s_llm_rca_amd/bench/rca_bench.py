@@ -130,8 +130,9 @@ def run(args) -> Optional[Dict[str, Any]]:
         # one rank of a TP=N deployment at real shapes, collectives stood in (parallel/tpsim.py)
         if not cuda or world > 1 or tp_mode:
             raise SystemExit("--tp-sim runs ONE process on one GPU")
+        from ..models.config import get_config
         from ..parallel.tpsim import sim_context
-        pc = sim_context(args.tp_sim)
+        pc = sim_context(args.tp_sim, ep=args.tp_sim if get_config(args.model).n_experts else 1)
     if tp_mode:
         import torch.distributed as dist
         from ..parallel.groups import ParallelContext, attach_custom_allreduce
@@ -239,12 +240,14 @@ def run(args) -> Optional[Dict[str, Any]]:
     if args.tp_sim > 1:
         from ..parallel.tpsim import project
         hist = {T: n - sim0.get(T, 0) for T, n in eng.sim_rows.items() if n - sim0.get(T, 0) > 0}
-        pr = project(hist, pc, eng.mc.hidden, eng.mc.n_layers, device)
+        pr = project(hist, pc, eng.mc.hidden, eng.mc.n_layers, device,
+                     moe_k=eng.mc.top_k if eng.mc.n_experts else 0)
         wall_p = elapsed - pr["standin_s"] + pr["modelled_s"]
         sim = {"tp": args.tp_sim, "rank": 0,
-               "what": "ONE rank of a TP=%d engine at real shapes on one GPU; every collective is a local "
+               "ep": pc.ep_size,
+               "what": "ONE rank of a TP=%d%s engine at real shapes on one GPU; every collective is a local "
                        "stand-in moving the same bytes (parallel/tpsim.py); a projection, not a scaling "
-                       "measurement" % args.tp_sim,
+                       "measurement" % (args.tp_sim, f" / EP={pc.ep_size}" if pc.ep_size > 1 else ""),
                "measured_value": round(n_done / elapsed, 4) if elapsed > 0 else 0.0,
                "standin_collectives_s": round(pr["standin_s"], 3),
                "modelled_xgmi_collectives_s": round(pr["modelled_s"], 3),

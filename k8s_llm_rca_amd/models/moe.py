@@ -84,13 +84,17 @@ class MoELayerSet:
     GLDS_MAX_ROWS = int(os.environ.get("K8S_MOE_GLDS_MAX_ROWS", "384"))  # 0 disables (A/B)
     GLDS_UP = (13, 1)
 
-    def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor) -> torch.Tensor:
+    def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor,
+                device_offsets: bool = False) -> torch.Tensor:
         """Grouped SwiGLU over contiguous expert slices offsets[e]..offsets[e+1]
         (``offsets`` int32 [E_local+1], on the rows' device).  Decode-sized
         batches use the grouped kernel (weight streaming, no host sync);
         prefill-sized ones the per-expert library GEMMs, which pay one sync
-        for the offsets but run near the MFMA roof."""
-        if x_perm.is_cuda and x_perm.shape[0] > self.GROUPED_MAX_ROWS:
+        for the offsets but run near the MFMA roof.  ``device_offsets``: the
+        grouped kernels whatever the row count (the EP dispatch buffer holds
+        ``ep``-fold capacity rows, most of them the never-computed null
+        expert: a host read of the offsets would stall every prefill layer)."""
+        if x_perm.is_cuda and x_perm.shape[0] > self.GROUPED_MAX_ROWS and not device_offsets:
             offs = offsets.tolist()
             out = torch.empty_like(x_perm)
             for e in range(self.E_local):
@@ -108,5 +112,5 @@ class MoELayerSet:
         # un-fused down GEMM beats the SwiGLU-fused operand load (244 vs 287-305
         # us per layer at decode sizes), and splitting K (only 32 column tiles
         # per expert) fills the chip: 168-192 us
-        splits = self.DOWN_SPLITS if rows <= self.SPLIT_MAX_ROWS else 1
+        splits = self.DOWN_SPLITS if rows <= self.SPLIT_MAX_ROWS and not device_offsets else 1
         return M.grouped_gemm(N.silu_mul(gu), self.w2[li], offsets, splits=splits)

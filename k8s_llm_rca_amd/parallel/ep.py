@@ -17,7 +17,8 @@ rows, and for those:
 Over xGMI each all-to-all moves ``T/ep * k * H * 2`` bytes split across the 7
 peer links (RCCL), twice per layer.
 
-Decode-sized batches (``T <= FIXED_MAX_T``) take :func:`ep_moe_forward_fixed`
+Decode-sized batches (``T <= FIXED_MAX_T``), and any batch whose padded
+dispatch fits the xGMI communicator's buffer, take :func:`ep_moe_forward_fixed`
 instead: fixed-capacity dispatch buffers (every destination gets room for all
 of the rank's ``per * k`` slots), so every collective has a static size known
 on the host -- no counts exchange, no ``.tolist()`` host sync -- and, on the
@@ -40,12 +41,23 @@ from ..ops import moe as M
 FIXED_MAX_T = 256
 
 
-def _a2a(pc, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
-    """Equal-split all-to-all over the EP group: ``send`` / ``recv`` [ep, ...]."""
+def _on_xgmi(pc, nbytes: int) -> bool:
     car = pc.custom_ar
-    if (car is not None and send.is_cuda and send.dtype == torch.bfloat16 and pc.ep_group is pc.tp_group
-            and car.a2a_fits(send.numel() * 2)):
-        return car.all_to_all(send, recv)
+    return car is not None and pc.ep_group is pc.tp_group and car.a2a_fits(nbytes)
+
+
+def _a2a(pc, send: torch.Tensor, recv: torch.Tensor, sim_replicate: bool = True) -> torch.Tensor:
+    """Equal-split all-to-all over the EP group: ``send`` / ``recv`` [ep, ...].
+    Under tp-sim (rank 0 alone, parallel/tpsim.py) the loopback kernel moves
+    the bytes and every "peer" region then carries this rank's own region --
+    the same routing statistics from every rank, so the local expert sees the
+    row count it would on a real EP group."""
+    car = pc.custom_ar
+    if send.is_cuda and send.dtype == torch.bfloat16 and _on_xgmi(pc, send.numel() * 2):
+        car.all_to_all(send, recv)
+        if getattr(pc, "sim", False) and sim_replicate:
+            recv[1:] = recv[0:1]
+        return recv
     dist.all_to_all_single(recv, send, group=pc.ep_group)
     return recv
 
@@ -77,7 +89,8 @@ def ep_moe_forward_fixed(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, to
     recv_e = recv[:, H].float().round().to(torch.int32).contiguous()
     o2, inv2, offs2 = M.align(recv_e.view(-1, 1), El + 1)            # null bucket sorts last
     xs = recv[:, :H].index_select(0, o2.long())
-    ys = moe.experts(li, xs, offs2[: El + 1].contiguous())            # rows past offs2[El] are never computed
+    # rows past offs2[El] are never computed; the grouped kernels read the offsets on the device
+    ys = moe.experts(li, xs, offs2[: El + 1].contiguous(), device_offsets=True)
     out_recv = ys.index_select(0, inv2.long()).contiguous()
     back = _a2a(pc, out_recv.view(ep, C * H), torch.empty(ep, C * H, dtype=y.dtype, device=dev)).view(ep * C, H)
     own = y.new_zeros((per, H))
@@ -86,12 +99,20 @@ def ep_moe_forward_fixed(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, to
         own[:n_own] = M.combine(y_slots.contiguous(), slots.to(torch.int32), topk_w[lo:hi].contiguous(), n_own, k)
     # all-gather of the owned rows as an all-to-all of `ep` copies (one static-size collective)
     gathered = _a2a(pc, own.unsqueeze(0).expand(ep, per, H).contiguous().view(ep, per * H),
-                    torch.empty(ep, per * H, dtype=y.dtype, device=dev))
+                    torch.empty(ep, per * H, dtype=y.dtype, device=dev), sim_replicate=False)
     return gathered.view(ep * per, H)[:T]
 
 
 def ep_moe_forward(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids: torch.Tensor) -> torch.Tensor:
-    if y.shape[0] <= FIXED_MAX_T:
+    """Decode-sized batches, and every batch whose fixed-capacity dispatch fits
+    the xGMI communicator (prefill included: no counts exchange, no host sync;
+    the price is ``ep``-fold padded all-to-alls), take the static-size path;
+    larger ones the exact variable-size RCCL path."""
+    T, H = y.shape
+    pc = moe.pc
+    per = (T + pc.ep_size - 1) // pc.ep_size
+    fixed_bytes = pc.ep_size * per * moe.k * (H + 8) * 2
+    if T <= FIXED_MAX_T or (y.is_cuda and _on_xgmi(pc, fixed_bytes)):
         return ep_moe_forward_fixed(moe, li, y, topk_w, topk_ids)
     return ep_moe_forward_var(moe, li, y, topk_w, topk_ids)
 

@@ -135,7 +135,10 @@ def attach_custom_allreduce(pc: ParallelContext) -> ParallelContext:
             and dist.get_backend(pc.tp_group) == "nccl"):
         try:
             from .xgmi import XgmiAllReduce
-            pc.custom_ar = XgmiAllReduce(pc.tp_group)
+            # 64 MiB: every TP all-reduce up to 4,096 tokens of 70B (8,192 x bf16) stays on the
+            # xGMI two-shot, which reads the N-1 peers over N-1 links at once (512 MiB of HBM a rank)
+            mb = int(os.environ.get("K8S_RCA_AR_MAX_MB", "64"))
+            pc.custom_ar = XgmiAllReduce(pc.tp_group, max_bytes=mb << 20)
         except Exception as e:  # noqa: BLE001 - RCCL remains correct, only slower for small messages
             import logging
             logging.getLogger(__name__).warning("xGMI all-reduce unavailable (%s); using RCCL", e)

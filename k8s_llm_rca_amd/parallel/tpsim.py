@@ -37,20 +37,21 @@ from .xgmi import ONE_SHOT_MAX, _bind, _check
 
 XGMI_LINK_GBPS = 153.0   # one xGMI link, per direction (7 links per GPU)
 XGMI_HOP_US = 2.5        # one flag hand-off across the fabric (signal -> visible on the peer)
+RCCL_BUS_GBPS = 300.0    # assumed RCCL all-reduce bus bandwidth on an 8-GPU xGMI node (not measured here)
 
 
 def xgmi_model_us(nbytes: int, world: int, mode: int) -> float:
     """Modelled time of one bf16 all-reduce of ``nbytes`` over a full xGMI
     mesh: one-shot reads (N-1) peer slices in parallel over N-1 links (one
-    hop), two-shot moves 2 (N-1)/N of the message in two hops, and the RCCL
-    ring (mode 0) 2 (N-1)/N of it over one link per direction with N-1 hops
-    per half."""
+    hop), two-shot moves 2 (N-1)/N of the message in two hops, and RCCL
+    (mode 0, messages past the xGMI buffer) 2 (N-1)/N of it at
+    ``RCCL_BUS_GBPS`` with 2 (N-1) ring hops."""
     bw = XGMI_LINK_GBPS * 1e3  # bytes per us
     if mode == 1:
         return XGMI_HOP_US + nbytes / bw
     if mode == 2:
         return 2 * XGMI_HOP_US + 2 * nbytes / (world * bw)
-    return 2 * (world - 1) * XGMI_HOP_US + 2 * (world - 1) / world * nbytes / bw
+    return 2 * (world - 1) * XGMI_HOP_US + 2 * (world - 1) / world * nbytes / (RCCL_BUS_GBPS * 1e3)
 
 
 class LoopbackAR:
@@ -168,37 +169,64 @@ def _scratch(device, n: int, dtype) -> torch.Tensor:
     return b
 
 
-def sim_context(tp: int, max_bytes: int = 8 << 20) -> SimParallelContext:
-    pc = SimParallelContext(tp_size=tp, tp_rank=0, ep_size=1, ep_rank=0)
+def sim_context(tp: int, max_bytes: int = 64 << 20, ep: int = 1) -> SimParallelContext:
+    """``ep`` = tp for a MoE model: experts sharded over the same ranks (EP=8:
+    one Mixtral expert per rank), attention tensor-parallel."""
+    pc = SimParallelContext(tp_size=tp, tp_rank=0, ep_size=ep, ep_rank=0)
     pc.custom_ar = LoopbackAR(tp, max_bytes)
     return pc
 
 
-def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int, device) -> dict:
+def a2a_model_us(nbytes: int, world: int) -> float:
+    """Modelled equal-split all-to-all of ``nbytes`` per rank over a full
+    xGMI mesh: (N-1)/N of them leave over N-1 links at once, one hop."""
+    return XGMI_HOP_US + nbytes / (world * XGMI_LINK_GBPS * 1e3)
+
+
+def _time_us(fn, reps: int = 20) -> float:
+    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    for _ in range(3):
+        fn()
+    ev0.record()
+    for _ in range(reps):
+        fn()
+    ev1.record()
+    ev1.synchronize()
+    return ev0.elapsed_time(ev1) * 1e3 / reps
+
+
+def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int, device, moe_k: int = 0) -> dict:
     """Collective time of a simulated run: for every forward size T seen
-    (``rows_hist`` = {T: forwards}) the two [T, hidden] bf16 all-reduces per
-    layer, timed as stood in on this GPU and as modelled over xGMI
-    (:func:`xgmi_model_us`).  ``projected`` wall = measured wall - stand-in +
-    modelled (the collectives are serial in the step's stream)."""
+    (``rows_hist`` = {T: forwards}) the layer's collectives, timed as stood in
+    on this GPU and as modelled over xGMI (:func:`xgmi_model_us`,
+    :func:`a2a_model_us`).  Dense: two [T, hidden] bf16 all-reduces per layer.
+    MoE (``moe_k`` = top-k, EP = TP): one all-reduce (o_proj) and the three
+    fixed-capacity all-to-alls of ``parallel/ep.py`` (dispatch, combine, row
+    all-gather).  ``projected`` wall = measured wall - stand-in + modelled (the
+    collectives are serial in the step's stream)."""
     standin_us = model_us = 0.0
     per_t = {}
-    ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    N = pc.tp_size
     for T, n in sorted(rows_hist.items()):
         t = torch.zeros(T * hidden, dtype=torch.bfloat16, device=device)
         car = pc.custom_ar
         mode = car.mode_for(t) if car is not None else 0
-        for _ in range(3):
-            pc.all_reduce(t)
-        reps = 20
-        ev0.record()
-        for _ in range(reps):
-            pc.all_reduce(t)
-        ev1.record()
-        ev1.synchronize()
-        s_us = ev0.elapsed_time(ev1) * 1e3 / reps
-        m_us = xgmi_model_us(T * hidden * 2, pc.tp_size, mode)
-        k = 2 * n_layers * n
-        standin_us += k * s_us
-        model_us += k * m_us
-        per_t[int(T)] = {"forwards": int(n), "mode": mode, "standin_us": round(s_us, 2), "model_us": round(m_us, 2)}
+        s_us = _time_us(lambda: pc.all_reduce(t))
+        m_us = xgmi_model_us(T * hidden * 2, N, mode)
+        n_ar = 1 if moe_k else 2
+        s_tot, m_tot = n_ar * s_us, n_ar * m_us
+        if moe_k:
+            per = (T + N - 1) // N
+            for row_elems in ((per * moe_k) * (hidden + 8), (per * moe_k) * hidden, per * hidden):
+                nb = N * row_elems * 2
+                if car is not None and car.a2a_fits(nb):
+                    send = torch.zeros(N, row_elems, dtype=torch.bfloat16, device=device)
+                    recv = torch.empty_like(send)
+                    s_tot += _time_us(lambda: car.all_to_all(send, recv))
+                m_tot += a2a_model_us(nb, N)
+        k = n_layers * n
+        standin_us += k * s_tot
+        model_us += k * m_tot
+        per_t[int(T)] = {"forwards": int(n), "mode": mode, "standin_us": round(s_tot, 2),
+                         "model_us": round(m_tot, 2)}
     return {"standin_s": standin_us / 1e6, "modelled_s": model_us / 1e6, "per_T": per_t}

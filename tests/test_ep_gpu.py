@@ -56,6 +56,15 @@ def _worker(rank, world, port, out_dir):
         g.replay()
         torch.cuda.synchronize()
         res[T] = (eager.cpu(), out.clone().cpu())
+    # prefill-sized batches (> FIXED_MAX_T) on the same fixed-capacity dispatch: no
+    # counts exchange, no host read of the expert offsets -- checked by torch
+    for T in (300, 600):
+        y = torch.randn(T, cfg.hidden, generator=torch.Generator().manual_seed(T)).bfloat16().cuda()
+        torch.cuda.synchronize()
+        torch.cuda.set_sync_debug_mode("error")
+        out = moe.forward(1, y)
+        torch.cuda.set_sync_debug_mode(0)
+        res[T] = (out.cpu(), out.cpu())
     status = pc.custom_ar.status()
     pc.custom_ar.close()
     if rank == 0:
@@ -73,7 +82,7 @@ def _reference():
     moe = MoELayerSet(cfg, "cuda", torch.bfloat16, ParallelContext(), torch.Generator(device="cuda").manual_seed(11),
                       0.02, full_slice=True)
     out = {}
-    for T in (1, 16, 48):
+    for T in (1, 16, 48, 300, 600):
         y = torch.randn(T, cfg.hidden, generator=torch.Generator().manual_seed(T)).bfloat16().cuda()
         out[T] = moe.forward(1, y).float().cpu()
     return out

@@ -110,10 +110,20 @@ def ep_moe_forward(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, topk_ids
     larger ones the exact variable-size RCCL path."""
     T, H = y.shape
     pc = moe.pc
-    per = (T + pc.ep_size - 1) // pc.ep_size
-    fixed_bytes = pc.ep_size * per * moe.k * (H + 8) * 2
-    if T <= FIXED_MAX_T or (y.is_cuda and _on_xgmi(pc, fixed_bytes)):
+    ep = pc.ep_size
+
+    def fixed_bytes(t):
+        return ep * ((t + ep - 1) // ep) * moe.k * (H + 8) * 2
+
+    if T <= FIXED_MAX_T or (y.is_cuda and _on_xgmi(pc, fixed_bytes(T))):
         return ep_moe_forward_fixed(moe, li, y, topk_w, topk_ids)
+    if y.is_cuda and _on_xgmi(pc, fixed_bytes(FIXED_MAX_T)):
+        # larger than the buffer: row blocks that fit it (MoE is per token: exact)
+        tc = FIXED_MAX_T
+        while tc * 2 <= T and _on_xgmi(pc, fixed_bytes(tc * 2)):
+            tc *= 2
+        return torch.cat([ep_moe_forward_fixed(moe, li, y[a:a + tc], topk_w[a:a + tc], topk_ids[a:a + tc])
+                          for a in range(0, T, tc)])
     return ep_moe_forward_var(moe, li, y, topk_w, topk_ids)
 
 

@@ -91,6 +91,8 @@ def lib_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torc
         N = w.shape[0]
         if out is None:
             out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+        if M == 0:
+            return out
         ws = _blaslt_ws.get(x.device)
         if ws is None:
             ws = _blaslt_ws[x.device] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=x.device)
@@ -110,6 +112,8 @@ def linear_f32out(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
         M, K = x.shape
         N = w.shape[0]
         out = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        if M == 0:  # a step whose chunks all end mid-prompt samples no row
+            return out
         ws = _blaslt_ws.get(x.device)
         if ws is None:
             ws = _blaslt_ws[x.device] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=x.device)

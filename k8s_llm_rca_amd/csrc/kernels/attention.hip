@@ -74,6 +74,7 @@ struct AttnArgs {
   // in-kernel split-KV merge (K8SRCA_DECODE_MERGE=1): arrival counter per (lead row, kv head),
   // zero between launches (the last arriver resets its own); null: attn_reduce_kernel merges
   int* merge_cnt;
+  int pf_rows;            // rows per prefill partial slot (128: pg64 kernel, 256: w8 kernel)
 };
 
 struct RowState {
@@ -874,6 +875,222 @@ __global__ void __launch_bounds__(256, 2) attn_prefill_pg64_kernel(AttnArgs a) {
     }
 }
 
+// ------------------------------------------------ prefill (paged, BS 64, 8 waves)
+// The 256-row form of the pg64 kernel: workgroup = 8 waves x 32 rows = 256
+// (token, q-head) rows of one sequence (256/G tokens), so every staged K/V page
+// feeds twice the MFMA work of the 4-wave form (half the staging per query
+// token), and pages arrive by LDS-DMA (global_load_lds, no VGPR round trip, no
+// ds_write pass) into a 4-page LDS ring: page i+3 is issued right after the
+// barrier that retires page i, so three pages (96 KB) are in flight while a
+// page is computed.  Synchronisation as the GEMM ring (gemm_stream.hip): one
+// __shared__ array, counted vmcnt + raw s_barrier (never __syncthreads inside
+// the loop: its fence would drain the DMAs), lgkmcnt(0) after the fragment
+// reads.  The LDS images are the pg64 kernel's (XOR-swizzled chunks), written
+// lane-linearly with the swizzle moved to the DMA SOURCE address, so the
+// per-row arithmetic -- and hence each row's result -- is the pg64 kernel's.
+// The tile's page ids are staged in LDS once (no global load in the loop).
+constexpr int PF8_WAVES = 8;
+constexpr int PF8_ROWS = 32 * PF8_WAVES;            // rows per workgroup
+constexpr int PF8_NB = 4;                           // ring pages
+constexpr int PF8_STAGE = PF_KBYTES + PF_VBYTES;    // 32 KB
+constexpr int PF8_MAXP = 1024;                      // page ids staged in LDS
+constexpr int PF8_DMA = 4;                          // DMAs per thread per page (2 K + 2 V)
+
+__device__ __forceinline__ void pf8_glds(const uint16_t* src, unsigned char* lds_dst) {
+  __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
+}
+
+__global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
+  __shared__ __attribute__((aligned(16))) unsigned char lds[PF8_NB * PF8_STAGE + 4 * PF8_MAXP];
+  int* s_blk = reinterpret_cast<int*>(lds + PF8_NB * PF8_STAGE);
+  const int kvh = blockIdx.x % a.nkv, tile = blockIdx.x / a.nkv;  // kv head -> XCD (nkv == 8)
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  const int r = lane & 31, hi = lane >> 5;
+  const int seq = a.tile_seq[tile];
+  const int tok0 = a.tile_tok0[tile];
+  const int tlen = a.tile_len[tile];
+  const int qs = a.q_start[seq];
+  const int qlen = a.q_start[seq + 1] - qs;
+  const int ctx = a.ctx_lens[seq];
+  const int* bt = a.block_tables + (size_t)seq * a.bt_stride;
+  const int base_pos = ctx - qlen + (tok0 - qs);
+
+  const int grow = w * 32 + r;
+  const int tt = grow / a.G, g = grow % a.G;
+  const bool valid = tt < tlen;
+  const int limit = valid ? base_pos + tt + 1 : 0;
+  const int wt0 = (w * 32) / a.G, wt1 = min(tlen - 1, (w * 32 + 31) / a.G);
+  const bool wave_live = wt0 < tlen;
+  const int wave_lo = base_pos + wt0 + 1;
+  const int wave_hi = wave_live ? base_pos + wt1 + 1 : 0;
+  const int kv_end = base_pos + tlen;
+  const int p_begin = a.tile_kv0[tile];
+  const int n_pages = min(a.tile_kv1[tile], (kv_end + PF_PAGE - 1) / PF_PAGE);
+  const int np = n_pages - p_begin;  // host-checked <= PF8_MAXP
+  const int slot = a.tile_slot[tile];
+
+  for (int i = tid; i < np; i += 512) s_blk[i] = bt[p_begin + i];
+  bf16x8 qf[8];
+  {
+    const uint16_t* qp = a.q + (size_t)(tok0 + (valid ? tt : 0)) * a.q_stride + (kvh * a.G + g) * D + 8 * hi;
+#pragma unroll
+    for (int s = 0; s < 8; ++s) qf[s] = valid ? load16(qp + 16 * s) : zero8();
+  }
+#pragma unroll
+  for (int s = 0; s < 8; ++s) asm volatile("" ::"v"(qf[s]));
+  __syncthreads();  // page ids visible; every ordinary load retired before the first DMA
+
+  f32x16 o[4];
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int i = 0; i < 16; ++i) o[dt][i] = 0.f;
+  float m = -INFINITY, l = 0.f;
+
+  // this thread's DMA sources: K pieces 2w, 2w+1 (4 key rows of 256 B each);
+  // V pieces 2w, 2w+1 (8 d-rows of 128 B each); lane-linear LDS, swizzled source
+  int koff[2], voff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int pc = 2 * w + i;
+    const int key = 4 * pc + (lane >> 4), kc = (lane & 15) ^ (key & 15);
+    koff[i] = key * D + 8 * kc;
+    const int d = 8 * pc + (lane >> 3), vc = (lane & 7) ^ ((d >> 1) & 7);
+    voff[i] = d * PF_PAGE + 8 * vc;
+  }
+  auto issue = [&](int stage, int i) {
+    const size_t page = (size_t)s_blk[i] * a.nkv + kvh;
+    const uint16_t* kp = a.kc + page * (size_t)(PF_PAGE * D);
+    const uint16_t* vp = a.vc + page * (size_t)(D * PF_PAGE);
+    unsigned char* kl = lds + stage * PF8_STAGE;
+    unsigned char* vl = kl + PF_KBYTES;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pf8_glds(kp + koff[j], kl + (2 * w + j) * 1024);
+#pragma unroll
+    for (int j = 0; j < 2; ++j) pf8_glds(vp + voff[j], vl + (2 * w + j) * 1024);
+  };
+
+  const int kreg = (r & 3) + 4 * (r >> 3), khi = (r >> 2) & 1;
+  const int krow0 = pf_key(kreg, khi);
+  // the younger half of the workgroup loses VALU arbitration on every segment:
+  // one static priority bump for it (cdna_hip_programming.md T5, static form)
+  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+
+  if (np > 0) {
+#pragma unroll
+    for (int j = 0; j < PF8_NB - 1; ++j) issue(j, min(j, np - 1));
+  }
+  for (int i = 0; i < np; ++i) {
+    // this wave's DMAs of page i are done when only the two later pages' remain
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PF8_NB - 2) * PF8_DMA) : "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done reading page i-1
+    issue((i + PF8_NB - 1) % PF8_NB, min(i + PF8_NB - 1, np - 1));  // refill page i-1's stage (clamped)
+    const int k0 = (p_begin + i) * PF_PAGE;
+    if (wave_live && k0 < wave_hi) {
+      const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
+      const unsigned char* vl = kl + PF_KBYTES;
+      f32x16 sc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = 32 * kt + krow0;
+        const unsigned char* kr = kl + key * 256;
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s + hi) ^ (key & 15)) << 4));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
+        }
+        sc[kt] = acc;
+      }
+      if (k0 + PF_PAGE > wave_lo) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
+      }
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mcand = cmax * a.scale_log2;
+      const bool upd = mcand > m + 8.f;
+      const float mnew = upd ? mcand : m;
+      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
+      const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
+      bf16x8 pf[2][2];
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
+            psum += e;
+            pf[kt][s][j] = (__bf16)e;
+          }
+      l = l * alpha + psum;
+      m = mnew;
+      if (__ballot(upd)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int d = 32 * dt + r;
+        const unsigned char* vr = vl + d * 128;
+        const int sw = (d >> 1) & 7;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
+          }
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+  __builtin_amdgcn_s_setprio(0);
+
+  if (!valid) return;
+  l += __shfl_xor(l, 32, 64);
+  if (slot >= 0) {  // split tile: unnormalised partial, merged by attn_prefill_merge
+    const size_t rbase = ((size_t)slot * a.nkv + kvh) * PF8_ROWS + grow;
+    float* po = a.pf_o + rbase * D;
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4)
+        *reinterpret_cast<f32x4*>(po + 32 * dt + 8 * q4 + 4 * hi) =
+            f32x4{o[dt][4 * q4], o[dt][4 * q4 + 1], o[dt][4 * q4 + 2], o[dt][4 * q4 + 3]};
+    if (hi == 0) {
+      a.pf_ml[rbase * 2] = m;
+      a.pf_ml[rbase * 2 + 1] = l;
+    }
+    return;
+  }
+  const float inv = l > 0.f ? 1.f / l : 0.f;
+  uint16_t* dst = a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D;
+#pragma unroll
+  for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      u16x4 v;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * q4 + e] * inv);
+      *reinterpret_cast<u16x4*>(dst + 32 * dt + 8 * q4 + 4 * hi) = v;
+    }
+}
+
 // grid: (n_merge * nkv, PF_ROWS / 4); block 256: ONE WAVE PER ROW (a wave
 // walking many rows serialises np dependent loads per row).  Two passes:
 // M = max_p m_p, then O = sum_p o_p 2^(m_p - M) / sum_p l_p 2^(m_p - M), 2 dims per lane.
@@ -890,13 +1107,13 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
   float M = -INFINITY;
 #pragma unroll 4
   for (int p = 0; p < np; ++p) {
-    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * PF_ROWS + row;
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * a.pf_rows + row;
     M = fmaxf(M, a.pf_ml[rb * 2]);
   }
   float L = 0.f, o0 = 0.f, o1 = 0.f;
 #pragma unroll 4
   for (int p = 0; p < np; ++p) {
-    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * PF_ROWS + row;
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * a.pf_rows + row;
     const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
     const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
     // a part that saw no key of the row has m = -inf: weight 0
@@ -982,6 +1199,13 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   return (int)hipGetLastError();
 }
 
+// K8SRCA_PF_W8 (default 1): 256-row LDS-DMA prefill workgroups; 0 = the 128-row
+// pg64 kernel.  Read per launch, like the planner reads it per plan.
+static bool prefill_w8() {
+  const char* v = std::getenv("K8SRCA_PF_W8");
+  return !(v && v[0] == '0');
+}
+
 K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                              int bt_stride, const int* ctx_lens, const int* q_start, const int* tile_seq,
                              const int* tile_tok0, const int* tile_len, const int* tile_kv0, const int* tile_kv1,
@@ -1020,8 +1244,15 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
   if (n_tiles <= 0) return (int)hipSuccess;
   if (BS == PF_PAGE && PF_ROWS % a.G == 0) {
     if (n_merge > 0 && (!pf_o || !pf_ml)) return (int)hipErrorInvalidValue;
-    hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
-    if (n_merge > 0) hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(n_merge * nkv, PF_ROWS / 4), dim3(256), 0, stream, a);
+    // the tile size is the planner's (ops/attention.py pf_wg_rows(): the same switch)
+    const bool w8 = prefill_w8() && PF8_ROWS % a.G == 0 && bt_stride <= PF8_MAXP;
+    a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
+    if (w8)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    else
+      hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
+    if (n_merge > 0)
+      hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(n_merge * nkv, a.pf_rows / 4), dim3(256), 0, stream, a);
   } else {
     if (n_merge > 0) return (int)hipErrorInvalidValue;  // the generic kernel does not split
     hipLaunchKernelGGL(attn_prefill_kernel, dim3(n_tiles, nkv), dim3(256), 0, stream, a);

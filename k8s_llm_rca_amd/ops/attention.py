@@ -312,13 +312,25 @@ def build_decode_items(ctx_lens, q_rows, part: int, chain=None, gmax: int = 1):
     return out[order]
 
 
+def pf_wg_rows(G: int) -> int:
+    """(token, q-head) rows per paged-64 prefill workgroup: 256 for the 8-wave
+    LDS-DMA kernel (``K8SRCA_PF_W8``, default on; the C launcher reads the
+    same switch per launch), 128 for the 4-wave pg64 kernel."""
+    if os.environ.get("K8SRCA_PF_W8", "1") != "0" and PF8_ROWS % G == 0:
+        return PF8_ROWS
+    return PF_ROWS
+
+
 def prefill_tile_tokens(G: int, block_size: int) -> int:
-    """Tokens per prefill tile: the paged-64 kernel covers 128 (token, q-head)
-    rows per workgroup, the generic one 64."""
-    return max(1, (128 if block_size == 64 and 128 % G == 0 else 64) // G)
+    """Tokens per prefill tile: the paged-64 kernels cover 256 (8 waves) or
+    128 (4 waves) (token, q-head) rows per workgroup, the generic one 64."""
+    if block_size == 64 and PF_ROWS % G == 0:
+        return max(1, pf_wg_rows(G) // G)
+    return max(1, 64 // G)
 
 
-PF_ROWS = 128               # (token, q-head) rows per paged-64 prefill workgroup
+PF_ROWS = 128               # (token, q-head) rows per pg64 prefill workgroup
+PF8_ROWS = 256              # rows per 8-wave (w8) prefill workgroup
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
 # split long key ranges until a prefill launch has about this many workgroups
 PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
@@ -382,7 +394,7 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
             n = min(per, b - t)
             tiles.append((base + (t - a) + n, s, t, n))
     plan = PrefillPlan(*[[] for _ in range(10)])
-    split = block_size == 64 and ctx_lens_host is not None and 128 % G == 0
+    split = block_size == 64 and ctx_lens_host is not None and PF_ROWS % G == 0
     # sequences with the most work first; inside a sequence, longest tile first
     work = {}
     for end, s, _, n in tiles:
@@ -436,9 +448,10 @@ def attach_plan(meta: "AttnMeta", plan: PrefillPlan, device, workspace: Optional
 
 
 def prefill_workspace(nkv: int, device, slots: int = PF_MAX_SLOTS, D: int = HEAD_DIM) -> tuple:
-    """fp32 partial-O / (max, sum) buffers for ``slots`` split-tile parts."""
-    return (torch.empty(slots * nkv * PF_ROWS * D, dtype=torch.float32, device=device),
-            torch.empty(slots * nkv * PF_ROWS * 2, dtype=torch.float32, device=device))
+    """fp32 partial-O / (max, sum) buffers for ``slots`` split-tile parts
+    (sized for the larger, 256-row workgroup)."""
+    return (torch.empty(slots * nkv * PF8_ROWS * D, dtype=torch.float32, device=device),
+            torch.empty(slots * nkv * PF8_ROWS * 2, dtype=torch.float32, device=device))
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta, nq: int,

@@ -737,3 +737,30 @@ def test_grouped_glds_matches_per_expert(E, N, K, cfg, splits):
     got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), splits=splits, glds=cfg).float().cpu()
     ref = MO.grouped_gemm(a, w, offs).float()
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
+@pytest.mark.parametrize("ctx,qlen", [([7], [7]), ([4100, 700], [900, 700]), ([8000], [1500]), ([130, 64, 3000], [66, 64, 700])])
+def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
+    """The 8-wave LDS-DMA prefill kernel (256-row workgroups, K8SRCA_PF_W8=1)
+    against the 4-wave pg64 kernel and the fp32 reference, with and without
+    split-KV tiles (the planner splits long key ranges when a launch has few
+    workgroups)."""
+    _need_gpu()
+    torch.manual_seed(3)
+    BS = 64
+    NB = sum((c + BS - 1) // BS for c in ctx) + 4
+    kc, vc = _setup_cache(nkv, BS, NB, dev)
+    T = sum(qlen)
+    q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+    scale = 1 / math.sqrt(128)
+    outs = {}
+    for w8 in ("1", "0"):
+        monkeypatch.setenv("K8SRCA_PF_W8", w8)
+        torch.manual_seed(7)  # the same block tables for both kernels
+        meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
+        outs[w8] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
+    monkeypatch.setenv("K8SRCA_PF_W8", "1")
+    ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
+    torch.testing.assert_close(outs["1"].cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    torch.testing.assert_close(outs["1"].float(), outs["0"].float(), atol=1e-2, rtol=1e-2)

@@ -6,6 +6,7 @@ prioritised from measurements (run on the GPU box).
 import argparse
 import json
 import math
+import os
 import sys
 import time
 
@@ -57,6 +58,7 @@ def main():
     ap.add_argument("--trace", default="profiles/r1_shape_trace_128.jsonl")
     ap.add_argument("--samples", type=int, default=80)
     ap.add_argument("--variants", default="", help="replay: comma list of planner variants (default all)")
+    ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with both kernels (PF_W8 1 / 0)")
     args = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -154,22 +156,32 @@ def main():
             for b, (u, by, n) in agg.items():
                 if n:
                     res[f"replay decode {name} B{b[0]}-{b[1]}"] = f"n={n} {u / n:.1f}us/step {by / u / 1e6:.2f} TB/s"
-        tot_us = fl = 0.0
+        # prefill: the 8-wave LDS-DMA kernel (K8SRCA_PF_W8=1) and the 4-wave pg64
+        # kernel interleaved per recorded step (same process, same data)
+        kinds = ("1", "0") if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        tot = {k: 0.0 for k in kinds}
+        fl = 0.0
         idx = torch.randperm(len(pre), generator=rng)[: args.samples].tolist()
         for i in idx:
             ctx = [c for c, q in pre[i]]
             ql = [q for c, q in pre[i]]
-            meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
-            kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
-            vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
             T = sum(ql)
-            q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
-            out = torch.empty(T, nq * 128, device=dev).bfloat16()
-            us = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
-                        iters=10, warm=2)
-            tot_us += us
+            for k in kinds:
+                os.environ["K8SRCA_PF_W8"] = k
+                torch.manual_seed(i)
+                meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
+                if k == kinds[0]:
+                    kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
+                    vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
+                    q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
+                    out = torch.empty(T, nq * 128, device=dev).bfloat16()
+                tot[k] += timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
+                                 iters=10, warm=2)
             fl += sum(sum(c - qq + j + 1 for j in range(qq)) for c, qq in zip(ctx, ql)) * nq * 128 * 4
-        res[f"replay prefill {len(idx)} steps"] = f"{tot_us / len(idx):.1f}us/step {fl / tot_us / 1e6:.1f} TFLOP/s"
+        for k in kinds:
+            res[f"replay prefill {len(idx)} steps PF_W8={k}"] = (f"{tot[k] / len(idx):.1f}us/step "
+                                                               f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
+        os.environ["K8SRCA_PF_W8"] = kinds[0]
     if args.what == "moe":
         from k8s_llm_rca_amd.ops import moe as MO
         E, H, I = 8, 4096, 14336

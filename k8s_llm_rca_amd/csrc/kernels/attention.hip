@@ -976,122 +976,87 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   // one static priority bump for it (cdna_hip_programming.md T5, static form)
   if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
 
-  // Two pages in the pipeline (cdna_hip_programming.md T15): iteration i issues
-  // QK^T of page i, then P.V of page i-1 (P already in registers), and its VALU
-  // work -- page i's mask, max, rescale decision and exp -> P -- overlaps those
-  // P.V MFMAs.  The decision comes after page i-1's P.V in program order, so a
-  // rescale scales everything still at the old max exactly once (T13).
-  // Ring: page i-1's V and page i's K are read in iteration i, so the stage
-  // refilled after iteration i's barrier is page i-2's: two pages in flight.
-  auto qk = [&](const unsigned char* kl, f32x16 (&sc)[2]) {
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt) {
-      const int key = 32 * kt + krow0;
-      const unsigned char* kr = kl + key * 256;
-      f32x16 acc;
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-      for (int s2 = 0; s2 < 8; ++s2) {
-        const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s2 + hi) ^ (key & 15)) << 4));
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s2], acc, 0, 0, 0);
-      }
-      sc[kt] = acc;
-    }
-  };
-  auto pv = [&](const bf16x8 (&pf)[2][2], const unsigned char* vl) {
-#pragma unroll
-    for (int dt = 0; dt < 4; ++dt) {
-      const int d = 32 * dt + r;
-      const unsigned char* vr = vl + d * 128;
-      const int sw = (d >> 1) & 7;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s2 = 0; s2 < 2; ++s2) {
-          const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s2 + hi) ^ sw) << 4));
-          o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s2], o[dt], 0, 0, 0);
-        }
-    }
-  };
-  // causal mask (raw scores; scale > 0 so the max commutes), the deferred-max
-  // decision (rescaling O and l when the reference moves), then exp -> P and l
-  auto softmax = [&](f32x16 (&sc)[2], int k0, bf16x8 (&pf)[2][2]) {
-    if (k0 + PF_PAGE > wave_lo) {
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e)
-          if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
-    }
-    float cmax = -INFINITY;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
-    cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-    const float mcand = cmax * a.scale_log2;
-    const bool upd = mcand > m + 8.f;
-    if (__ballot(upd)) {
-      const float mnew = upd ? mcand : m;
-      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
-      l *= alpha;
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
-      m = mnew;
-    }
-    const float nmsub = (m == -INFINITY) ? 0.f : -m;
-    float psum = 0.f;
-#pragma unroll
-    for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-      for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s2 + j], a.scale_log2, nmsub));
-          psum += e;
-          pf[kt][s2][j] = (__bf16)e;
-        }
-    l += psum;
-  };
-
   if (np > 0) {
 #pragma unroll
-    for (int j = 0; j < PF8_NB - 2; ++j) issue(j, min(j, np - 1));
+    for (int j = 0; j < PF8_NB - 1; ++j) issue(j, min(j, np - 1));
   }
-  // one pipeline step; `cur` / `prev` are the two named P buffers, swapped by
-  // unrolling the loop by two (static indexing: rule 20, no register copies)
-  bool prev_live = false;
-  auto step = [&](int i, bf16x8 (&cur)[2][2], bf16x8 (&prev)[2][2]) {
-    const unsigned char* vprev = lds + ((i + PF8_NB - 1) % PF8_NB) * PF8_STAGE + PF_KBYTES;
-    if (i < np) {
-      // page i landed when only page i+1's DMAs remain
-      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PF8_DMA) : "memory");
-      __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done with page i-2
-      issue((i + 2) % PF8_NB, min(i + 2, np - 1));  // page i-2's stage (clamped at the end)
-      const int k0 = (p_begin + i) * PF_PAGE;
-      const bool cur_live = wave_live && k0 < wave_hi;
-      if (cur_live) {
-        f32x16 sc[2];
-        qk(lds + (i % PF8_NB) * PF8_STAGE, sc);
-        if (prev_live) pv(prev, vprev);
-        softmax(sc, k0, cur);
-      } else if (prev_live) {
-        pv(prev, vprev);
+  for (int i = 0; i < np; ++i) {
+    // this wave's DMAs of page i are done when only the two later pages' remain
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PF8_NB - 2) * PF8_DMA) : "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done reading page i-1
+    issue((i + PF8_NB - 1) % PF8_NB, min(i + PF8_NB - 1, np - 1));  // refill page i-1's stage (clamped)
+    const int k0 = (p_begin + i) * PF_PAGE;
+    if (wave_live && k0 < wave_hi) {
+      const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
+      const unsigned char* vl = kl + PF_KBYTES;
+      f32x16 sc[2];
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt) {
+        const int key = 32 * kt + krow0;
+        const unsigned char* kr = kl + key * 256;
+        f32x16 acc;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s) {
+          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s + hi) ^ (key & 15)) << 4));
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
+        }
+        sc[kt] = acc;
       }
-      prev_live = cur_live;
-    } else if (prev_live) {
-      pv(prev, vprev);
-      prev_live = false;
+      if (k0 + PF_PAGE > wave_lo) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
+      }
+      float cmax = -INFINITY;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
+      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      const float mcand = cmax * a.scale_log2;
+      const bool upd = mcand > m + 8.f;
+      const float mnew = upd ? mcand : m;
+      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
+      const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
+      bf16x8 pf[2][2];
+      float psum = 0.f;
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
+            psum += e;
+            pf[kt][s][j] = (__bf16)e;
+          }
+      l = l * alpha + psum;
+      m = mnew;
+      if (__ballot(upd)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+      }
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int d = 32 * dt + r;
+        const unsigned char* vr = vl + d * 128;
+        const int sw = (d >> 1) & 7;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
+          }
+      }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  };
-  bf16x8 pA[2][2], pB[2][2];
-  for (int i = 0; i <= np; i += 2) {
-    step(i, pA, pB);
-    if (i + 1 <= np) step(i + 1, pB, pA);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
   __builtin_amdgcn_s_setprio(0);

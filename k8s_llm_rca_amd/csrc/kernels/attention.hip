@@ -900,6 +900,12 @@ __device__ __forceinline__ void pf8_glds(const uint16_t* src, unsigned char* lds
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
+// VAR (A/B only, K8SRCA_PF_W8=2/3): 2 = no static priority; 3 = waves 4-7 run half a page
+// behind (P.V of page i-1 first, then QK^T of page i and its softmax), so a SIMD's
+// two waves are in complementary segments two thirds of the time instead of in
+// lockstep (MI355X_MICROARCH.md "Two waves per SIMD", item 9); the stage refilled
+// after iteration i's barrier is then page i-2's (page i-1's V is still read).
+template <int VAR>
 __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[PF8_NB * PF8_STAGE + 4 * PF8_MAXP];
   int* s_blk = reinterpret_cast<int*>(lds + PF8_NB * PF8_STAGE);
@@ -974,18 +980,59 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   const int krow0 = pf_key(kreg, khi);
   // the younger half of the workgroup loses VALU arbitration on every segment:
   // one static priority bump for it (cdna_hip_programming.md T5, static form)
-  if (__builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  if (VAR != 2 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
+  constexpr int AHEAD = VAR == 3 ? PF8_NB - 2 : PF8_NB - 1;  // pages in flight beyond the current one
+  const bool late = VAR == 3 && __builtin_amdgcn_readfirstlane(tid) >= 256;
+  bf16x8 pl[2][2];          // late waves: the previous page's P, its P.V still owed
+  bool owe = false;
+  int owe_stage = 0;
 
   if (np > 0) {
 #pragma unroll
-    for (int j = 0; j < PF8_NB - 1; ++j) issue(j, min(j, np - 1));
+    for (int j = 0; j < AHEAD; ++j) issue(j, min(j, np - 1));
   }
-  for (int i = 0; i < np; ++i) {
-    // this wave's DMAs of page i are done when only the two later pages' remain
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((PF8_NB - 2) * PF8_DMA) : "memory");
-    __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done reading page i-1
-    issue((i + PF8_NB - 1) % PF8_NB, min(i + PF8_NB - 1, np - 1));  // refill page i-1's stage (clamped)
+  for (int i = 0; i <= np; ++i) {
+    if (i == np) {  // late waves: the last owed P.V (nothing else runs in this trip)
+      if (late && owe) {
+        const unsigned char* vl = lds + owe_stage * PF8_STAGE + PF_KBYTES;
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int d = 32 * dt + r;
+          const unsigned char* vr = vl + d * 128;
+          const int sw = (d >> 1) & 7;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl[kt][s], o[dt], 0, 0, 0);
+            }
+        }
+      }
+      break;
+    }
+    // this wave's DMAs of page i are done when only the later pages' remain
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 1) * PF8_DMA) : "memory");
+    __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done with the refilled stage
+    issue((i + AHEAD) % PF8_NB, min(i + AHEAD, np - 1));  // refill (clamped at the end: an L2 hit)
     const int k0 = (p_begin + i) * PF_PAGE;
+    if (late && owe) {  // P.V of page i-1 first (its P was made at the current reference max)
+      const unsigned char* vl = lds + owe_stage * PF8_STAGE + PF_KBYTES;
+#pragma unroll
+      for (int dt = 0; dt < 4; ++dt) {
+        const int d = 32 * dt + r;
+        const unsigned char* vr = vl + d * 128;
+        const int sw = (d >> 1) & 7;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int s = 0; s < 2; ++s) {
+            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl[kt][s], o[dt], 0, 0, 0);
+          }
+      }
+      owe = false;
+    }
     if (wave_live && k0 < wave_hi) {
       const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
       const unsigned char* vl = kl + PF_KBYTES;
@@ -1036,24 +1083,33 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
           }
       l = l * alpha + psum;
       m = mnew;
-      if (__ballot(upd)) {
+      if (__ballot(upd)) {  // (late waves: page i-1's P.V is already in O)
 #pragma unroll
         for (int dt = 0; dt < 4; ++dt)
 #pragma unroll
           for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
       }
-#pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = 32 * dt + r;
-        const unsigned char* vr = vl + d * 128;
-        const int sw = (d >> 1) & 7;
+      if (late) {  // P.V of this page next trip, behind its barrier
 #pragma unroll
         for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
-          }
+          for (int s = 0; s < 2; ++s) pl[kt][s] = pf[kt][s];
+        owe = true;
+        owe_stage = i % PF8_NB;
+      } else {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt) {
+          const int d = 32 * dt + r;
+          const unsigned char* vr = vl + d * 128;
+          const int sw = (d >> 1) & 7;
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+              const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
+            }
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1201,9 +1257,10 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
 
 // K8SRCA_PF_W8 (default 1): 256-row LDS-DMA prefill workgroups; 0 = the 128-row
 // pg64 kernel.  Read per launch, like the planner reads it per plan.
-static bool prefill_w8() {
+static int prefill_w8() {
   const char* v = std::getenv("K8SRCA_PF_W8");
-  return !(v && v[0] == '0');
+  if (!v || !v[0]) return 1;
+  return v[0] - '0';
 }
 
 K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
@@ -1245,10 +1302,15 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
   if (BS == PF_PAGE && PF_ROWS % a.G == 0) {
     if (n_merge > 0 && (!pf_o || !pf_ml)) return (int)hipErrorInvalidValue;
     // the tile size is the planner's (ops/attention.py pf_wg_rows(): the same switch)
-    const bool w8 = prefill_w8() && PF8_ROWS % a.G == 0 && bt_stride <= PF8_MAXP;
+    const int var = prefill_w8();
+    const bool w8 = var > 0 && PF8_ROWS % a.G == 0 && bt_stride <= PF8_MAXP;
     a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
-    if (w8)
-      hipLaunchKernelGGL(attn_prefill_w8_kernel, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    if (w8 && var == 3)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<3>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    else if (w8 && var == 2)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<2>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    else if (w8)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<1>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else
       hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
     if (n_merge > 0)

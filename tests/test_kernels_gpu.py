@@ -755,7 +755,7 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
     scale = 1 / math.sqrt(128)
     outs = {}
-    for w8 in ("1", "0"):
+    for w8 in ("1", "2", "3", "0"):  # w8, w8 without static priority, w8 with staggered late waves, pg64
         monkeypatch.setenv("K8SRCA_PF_W8", w8)
         torch.manual_seed(7)  # the same block tables for both kernels
         meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
@@ -764,3 +764,5 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
     torch.testing.assert_close(outs["1"].cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
     torch.testing.assert_close(outs["1"].float(), outs["0"].float(), atol=1e-2, rtol=1e-2)
+    assert torch.equal(outs["1"], outs["2"])  # the same arithmetic in the same order
+    torch.testing.assert_close(outs["3"].float(), outs["1"].float(), atol=1e-2, rtol=1e-2)

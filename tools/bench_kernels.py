@@ -58,7 +58,8 @@ def main():
     ap.add_argument("--trace", default="profiles/r1_shape_trace_128.jsonl")
     ap.add_argument("--samples", type=int, default=80)
     ap.add_argument("--variants", default="", help="replay: comma list of planner variants (default all)")
-    ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with both kernels (PF_W8 1 / 0)")
+    ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with every kernel of --pf-kinds")
+    ap.add_argument("--pf-kinds", default="1,0", help="K8SRCA_PF_W8 values to A/B (1 w8, 2 w8 no prio, 3 w8 stagger, 0 pg64)")
     args = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)
@@ -158,7 +159,7 @@ def main():
                     res[f"replay decode {name} B{b[0]}-{b[1]}"] = f"n={n} {u / n:.1f}us/step {by / u / 1e6:.2f} TB/s"
         # prefill: the 8-wave LDS-DMA kernel (K8SRCA_PF_W8=1) and the 4-wave pg64
         # kernel interleaved per recorded step (same process, same data)
-        kinds = ("1", "0") if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        kinds = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
         tot = {k: 0.0 for k in kinds}
         fl = 0.0
         idx = torch.randperm(len(pre), generator=rng)[: args.samples].tolist()

@@ -26,6 +26,9 @@
 // cached prefix): workgroup = (tile of 64/G tokens, kv head); each wave owns 16
 // rows and walks the keys its rows can see.
 #include <cstdlib>
+#include <map>
+#include <mutex>
+#include <utility>
 
 #include "common.h"
 
@@ -1193,22 +1196,28 @@ using namespace k8s;
 // per call): one zeroed device buffer per GPU, allocated outside any stream
 // capture (the first eager decode step; until then, and for batches beyond its
 // capacity, the separate reduce kernel merges).
+// One buffer per (device, stream): launches on different streams (two engines on
+// one GPU) never share the self-resetting counters; the map is guarded, so
+// concurrent first calls from several host threads allocate once per key.
 static int* merge_counters(int need, hipStream_t stream) {
   constexpr int kCap = 1 << 16;
-  static int* bufs[64] = {};
+  static std::mutex mu;
+  static std::map<std::pair<int, hipStream_t>, int*> bufs;
   const char* v = std::getenv("K8SRCA_DECODE_MERGE");
   if (!(v && v[0] == '1') || need > kCap) return nullptr;
   int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return nullptr;
-  if (!bufs[dev]) {
+  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
+  std::lock_guard<std::mutex> g(mu);
+  int*& slot = bufs[{dev, stream}];
+  if (!slot) {
     hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
     if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
     int* p = nullptr;
     if (hipMalloc(&p, kCap * sizeof(int)) != hipSuccess) return nullptr;
     if (hipMemset(p, 0, kCap * sizeof(int)) != hipSuccess) return nullptr;
-    bufs[dev] = p;
+    slot = p;
   }
-  return bufs[dev];
+  return slot;
 }
 
 K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,

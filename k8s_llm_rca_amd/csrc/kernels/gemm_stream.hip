@@ -412,7 +412,7 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   const int bn = cfg > 20 ? 128 : kSBN;  // strip width
   if (M <= 0 || M > 256 || N % bn || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
       (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24) || ldx % 8 ||
-      (splits > 1 && (M * N) % 8) || (splits == 1 && ldy < N))
+      (splits > 1 && (M * N) % 8) || ((splits == 1 || reduce) && ldy < N))  // y is written: rows of N
     return (int)hipErrorInvalidValue;
   const int kslice = K / splits;
   // the register-ring loop is unrolled by U chunks with no partial trip

@@ -16,6 +16,7 @@ graph is mirrored to HBM).
 """
 from __future__ import annotations
 
+import re
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 import numpy as np
@@ -25,6 +26,9 @@ from ..store import PropertyGraph
 from . import ast as A
 from .evaluator import Env, _bool, cy_eq, evaluate, free_vars, has_aggregate
 from .parser import parse
+
+# the stored timestamp form (graph/store.py TS_FORMAT, millisecond fraction)
+_TS_FIXED = re.compile(r"\d{4}-\d{2}-\d{2} \d{2}:\d{2}:\d{2}\.\d{3}")
 
 NODE, REL, RELS, PATH, VALUE = "node", "rel", "rels", "path", "value"
 
@@ -219,6 +223,12 @@ class Executor:
         if want or uid is None or t_lo is None or t_hi is None:
             return None
         from ..store import ts_to_ms
+        # Cypher compares these strings lexicographically; the int64-ms fast path is
+        # the same order only for the stored fixed-width form (an unpadded field, a
+        # 1-2 or 4-6 digit fraction would compare differently): anything else takes
+        # the generic path
+        if not (_TS_FIXED.fullmatch(t_lo) and _TS_FIXED.fullmatch(t_hi)):
+            return None
         try:
             q_lo, q_hi = ts_to_ms(t_lo), ts_to_ms(t_hi)
         except (ValueError, TypeError):

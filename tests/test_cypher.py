@@ -202,3 +202,12 @@ def test_state_pattern_operator_matches_generic_path(monkeypatch):
     monkeypatch.setattr(EX.Executor, "_state_pattern", lambda self, *a: None)
     slow = [[r["n2"].id for r in Executor(g).run(q)] for q in queries]
     assert fast == slow
+
+
+def test_state_fast_path_requires_fixed_width_timestamps():
+    """the int64-ms STATE fast path only takes the stored fixed-width
+    form; other literals compare as strings on the generic path (Cypher order)."""
+    from k8s_llm_rca_amd.graph.cypher.executor import _TS_FIXED
+    assert _TS_FIXED.fullmatch("2020-12-13 15:30:02.013")
+    for lit in ("2020-12-13 15:30:02.5", "2020-12-13 15:30:02.013000", "2020-12-13 5:30:02.013", "2020-12-13"):
+        assert not _TS_FIXED.fullmatch(lit)

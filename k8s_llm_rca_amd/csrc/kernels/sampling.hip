@@ -137,12 +137,17 @@ __device__ __forceinline__ Best block_best(Best best, float* sv, int* si) {
 // and that are >= `floor_key` add `count ? 1 : exp(v - vmax)` to bin (key >>
 // 8*byte) & 255.  Then bins are walked from 255 down: the first bin at which
 // the running total reaches `*need` is fixed into `*prefix`, and `*need` drops
-// by the total of the bins above it.
+// by the total of the bins above it.  The mass is accumulated in 2^-24 fixed
+// point with 64-bit integer atomics: integer sums do not depend on the order
+// the atomics land in, so the bin chosen at the nucleus boundary -- and the
+// sampled token -- is the same on every run (float atomics were not).
+constexpr float kMassScale = 16777216.0f;  // 2^24
+
 template <typename T>
 __device__ void radix_pass(const T* lr, int V, int vocab_off, float it, const int* lst, int ll, const uint32_t* mk,
                            int byte, bool count, float vmax, uint32_t floor_key, uint32_t* prefix, float* need,
-                           float* hist) {
-  for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0.f;
+                           unsigned long long* hist) {
+  for (int b = threadIdx.x; b < 256; b += blockDim.x) hist[b] = 0ull;
   __syncthreads();
   const uint32_t pre = *prefix;
   const int hs = 8 * (byte + 1);
@@ -150,14 +155,16 @@ __device__ void radix_pass(const T* lr, int V, int vocab_off, float it, const in
     const uint32_t k = okey(v);
     if (k < floor_key) return;
     if (hs < 32 && (k >> hs) != (pre >> hs)) return;
-    atomicAdd(&hist[(k >> (8 * byte)) & 255u], count ? 1.f : __expf(v - vmax));
+    const unsigned long long add =
+        count ? (unsigned long long)kMassScale : (unsigned long long)(__expf(v - vmax) * kMassScale + 0.5f);
+    atomicAdd(&hist[(k >> (8 * byte)) & 255u], add);
   });
   __syncthreads();
   if (threadIdx.x == 0) {
     float cum = 0.f, rem = *need;
     int pick = -1, lowest = -1;
     for (int b = 255; b >= 0; --b) {
-      const float h = hist[b];
+      const float h = (float)((double)hist[b] * (1.0 / kMassScale));
       if (h <= 0.f) continue;
       lowest = b;
       if (cum + h >= rem) {
@@ -188,7 +195,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
                                                      const float* __restrict__ top_p, int* __restrict__ out,
                                                      float2* __restrict__ out_pair, float* __restrict__ out_cand,
                                                      int cand_k) {
-  __shared__ float hist[256];
+  __shared__ unsigned long long hist[256];
   __shared__ float sv[4];
   __shared__ int si[4];
   __shared__ uint32_t s_prefix;
@@ -224,7 +231,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
     });
     const float vmax = block_best(mx, sv, si).v;
     __syncthreads();
-    const float nal = block_sum((float)n_allowed, hist);
+    const float nal = block_sum((float)n_allowed, sv);
     // ---- top-k threshold (cand: the rank-local top-cand_k)
     const int keff = cand ? ((kk > 0 && kk < cand_k) ? kk : cand_k) : kk;
     if (keff > 0 && (float)keff < nal) {
@@ -244,7 +251,7 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
         if (okey(v) >= thr) z += __expf(v - vmax);
       });
       __syncthreads();
-      z = block_sum(z, hist);
+      z = block_sum(z, sv);
       if (threadIdx.x == 0) {
         s_prefix = 0u;
         s_need = fmaxf(pp, 0.f) * z;
@@ -265,14 +272,47 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
       c_i[k] = 0x7fffffff;
     }
     __syncthreads();
+    // keys above the threshold (fewer than keff <= 256 of them: every one is
+    // kept, and the sort below fixes their order), then the ties AT the
+    // threshold into the remaining slots in a fixed order: a block-wide scan of
+    // per-thread tie counts, each thread's ties in its own id order (an
+    // atomic-arrival fill kept an arbitrary subset when > 256 tokens tie)
+    int my_ties = 0;
     for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
-      if (okey(v) < thr) return;
+      const uint32_t k = okey(v);
+      if (k < thr) return;
+      if (k == thr) {
+        ++my_ties;
+        return;
+      }
       const int slot = atomicAdd(&s_nc, 1);
       if (slot < 256) {
         c_v[slot] = v;
         c_i[slot] = gi;
       }
     });
+    __syncthreads();
+    const int n_above = min(s_nc, 256);
+    // exclusive scan of my_ties over the block (wave scan + per-wave totals in LDS)
+    int incl = my_ties;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int t = __shfl_up(incl, o, 64);
+      if ((threadIdx.x & 63) >= o) incl += t;
+    }
+    if ((threadIdx.x & 63) == 63) si[threadIdx.x >> 6] = incl;
+    __syncthreads();
+    int wave_off = 0;
+    for (int w = 0; w < (int)(threadIdx.x >> 6); ++w) wave_off += si[w];
+    int pos = n_above + wave_off + incl - my_ties;
+    if (my_ties && pos < 256) {
+      for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
+        if (okey(v) != thr || pos >= 256) return;
+        c_v[pos] = v;
+        c_i[pos] = gi;
+        ++pos;
+      });
+    }
     __syncthreads();
     // bitonic sort of 256 (v desc, id asc)
     for (int size = 2; size <= 256; size <<= 1) {

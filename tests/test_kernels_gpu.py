@@ -766,3 +766,33 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     torch.testing.assert_close(outs["1"].float(), outs["0"].float(), atol=1e-2, rtol=1e-2)
     assert torch.equal(outs["1"], outs["2"])  # the same arithmetic in the same order
     torch.testing.assert_close(outs["3"].float(), outs["1"].float(), atol=1e-2, rtol=1e-2)
+
+
+def test_sampling_top_p_and_tie_candidates_deterministic():
+    """the top-p threshold comes from order-independent (fixed-point
+    integer) mass sums and the candidate list from a fixed-order tie fill, so
+    repeated launches on the same inputs give identical tokens / candidates --
+    with flat bf16 logits (many exact ties) and with every logit equal."""
+    _need_gpu()
+    B, V = 16, 128256
+    torch.manual_seed(12)
+    flat = (torch.randn(B, V) * 0.25).bfloat16().to(dev)
+    temps = torch.full((B,), 0.8, device=dev)
+    seeds = (torch.arange(B, dtype=torch.int32) * 7 + 3).to(dev)
+    steps = torch.zeros(B, dtype=torch.int32, device=dev)
+    mask_id = torch.full((B,), -1, dtype=torch.int32, device=dev)
+    z = torch.zeros(B, dtype=torch.int32, device=dev)
+    tk = torch.zeros(B, dtype=torch.int32, device=dev)
+    tpp = torch.full((B,), 0.9, device=dev)
+    runs = [SMP.sample(flat, temps, seeds, steps, mask_id, None, z, z, z[:1], vocab=V, top_k=tk, top_p=tpp)
+            for _ in range(8)]
+    assert all(torch.equal(r, runs[0]) for r in runs)
+    # a shard where every logit ties: > 256 tokens sit at the top-k threshold
+    same = torch.zeros(B, 16032, device=dev)
+    tk64 = torch.full((B,), 64, dtype=torch.int32, device=dev)
+    one = torch.ones(B, device=dev)
+    outs = [SMP.sample(same, temps, seeds, steps, mask_id, None, z, z, z[:1], vocab=V, vocab_off=16032, pairs=True,
+                       top_k=tk64, top_p=one, candidates=True)[1] for _ in range(8)]
+    assert all(torch.equal(c, outs[0]) for c in outs)
+    ids = outs[0][:, :, 1]
+    assert bool((ids >= 16032).all()) and bool((ids[:, 1:] > ids[:, :-1]).all())  # valid, (v desc, id asc)

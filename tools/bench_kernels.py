@@ -59,6 +59,7 @@ def main():
     ap.add_argument("--samples", type=int, default=80)
     ap.add_argument("--variants", default="", help="replay: comma list of planner variants (default all)")
     ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with every kernel of --pf-kinds")
+    ap.add_argument("--pf-steps-out", default="", help="replay: per-step prefill timings (JSON lines) to this file")
     ap.add_argument("--pf-kinds", default="1,0", help="K8SRCA_PF_W8 values to A/B (1 w8, 2 w8 no prio, 3 w8 stagger, 0 pg64)")
     args = ap.parse_args()
     dev = "cuda"
@@ -161,6 +162,7 @@ def main():
         # kernel interleaved per recorded step (same process, same data)
         kinds = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
         tot = {k: 0.0 for k in kinds}
+        per_step = {}
         fl = 0.0
         idx = torch.randperm(len(pre), generator=rng)[: args.samples].tolist()
         for i in idx:
@@ -176,13 +178,20 @@ def main():
                     vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()
                     q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
                     out = torch.empty(T, nq * 128, device=dev).bfloat16()
-                tot[k] += timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
-                                 iters=10, warm=2)
+                us_k = timeit(lambda: A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128), out=out),
+                              iters=10, warm=2)
+                tot[k] += us_k
+                per_step.setdefault(i, {"T": T, "n": len(ql), "maxq": max(ql), "ctx": sum(ctx)})[k] = round(us_k, 1)
+                per_step[i][f"tiles{k}"] = meta.n_tiles
             fl += sum(sum(c - qq + j + 1 for j in range(qq)) for c, qq in zip(ctx, ql)) * nq * 128 * 4
         for k in kinds:
             res[f"replay prefill {len(idx)} steps PF_W8={k}"] = (f"{tot[k] / len(idx):.1f}us/step "
                                                                f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
         os.environ["K8SRCA_PF_W8"] = kinds[0]
+        if args.pf_steps_out:
+            with open(args.pf_steps_out, "w") as f:
+                for v in per_step.values():
+                    f.write(json.dumps(v) + "\n")
     if args.what == "moe":
         from k8s_llm_rca_amd.ops import moe as MO
         E, H, I = 8, 4096, 14336

@@ -1264,11 +1264,16 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   return (int)hipGetLastError();
 }
 
-// K8SRCA_PF_W8 (default 1): 256-row LDS-DMA prefill workgroups; 0 = the 128-row
-// pg64 kernel.  Read per launch, like the planner reads it per plan.
+// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups (2, the default: no static
+// priority; 1: with it; 3: staggered late waves), 0 = the 128-row pg64 kernel.
+// Read per launch, like the planner reads it per plan.  Replayed steady-state
+// mix (tools/bench_kernels.py --what replay, profiles/r3/pf_replay*.txt): 2 =
+// 664 / 1 = 651 / 3 = 608 / 0 = 647 TFLOP/s; on the round-2 (young-thread)
+// mix of short chunks pg64 is ahead (406 vs 378): per-step choice measured at
+// <= 3 % of prefill attention, not wired.
 static int prefill_w8() {
   const char* v = std::getenv("K8SRCA_PF_W8");
-  if (!v || !v[0]) return 1;
+  if (!v || !v[0]) return 2;
   return v[0] - '0';
 }
 

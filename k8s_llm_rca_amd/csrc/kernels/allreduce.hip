@@ -177,6 +177,147 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
   }
 }
 
+// TP row-parallel output + residual add + RMSNorm in ONE launch (the o_proj /
+// down_proj epilogue of a TP layer): out_row = sum over ranks of `in` (the
+// rank's partial, fixed rank order, rounded to bf16 as the all-reduce does),
+// res <- bf16(out + res), y = bf16(res * rsqrt(mean(res^2) + eps) * w).
+// Replaces all-reduce + rmsnorm (two launches and a [T][H] round trip per
+// call, 160 calls per 70B decode step).  Rows are the unit (a norm needs its
+// whole row): block b owns rows b, b + nb, ...; its flags are the all-reduce's
+// per-(rank, block) flags, on the same epoch sequence.
+//   one-shot : every rank sums every peer's row itself (the arithmetic and
+//              thread layout of rmsnorm_kernel: bit-identical to AR + norm);
+//   two-shot : rank r sums, adds and squares only its 1/N column slice and
+//              publishes the bf16 sums + the slice's sum of squares (RES);
+//              then every rank takes the N partial sums of squares in rank
+//              order (identical inverse norm on every rank) and gathers the
+//              slices: 2 (N-1)/N of the row bytes move instead of N-1.
+constexpr int AN_THREADS = 256;
+constexpr int AN_NC = 4;  // 16-B chunks per thread per row: H <= 8192
+
+__device__ __forceinline__ float an_block_sum(float v, float* scratch) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((threadIdx.x & 63) == 0) scratch[threadIdx.x >> 6] = v;
+  __syncthreads();
+  float r = 0.f;
+  for (int i = 0; i < AN_THREADS / 64; ++i) r += scratch[i];
+  __syncthreads();
+  return r;
+}
+
+template <bool TWO_SHOT>
+__global__ void __launch_bounds__(AN_THREADS) ar_addnorm_kernel(const uint16_t* __restrict__ in,
+                                                                 uint16_t* __restrict__ res,
+                                                                 const uint16_t* __restrict__ w,
+                                                                 uint16_t* __restrict__ y, int T, int H, float eps,
+                                                                 int world, int rank, ARPeers P, long max_bytes,
+                                                                 uint64_t timeout_ticks, int sim, int fence_all) {
+  __shared__ float scratch[AN_THREADS / 64];
+  __shared__ uint32_t s_e;
+  const int b = blockIdx.x, t = threadIdx.x, nb = gridDim.x;
+  unsigned char* own = P.base[rank];
+  uint32_t* ep = reinterpret_cast<uint32_t*>(own + AR_EPOCH);
+  uint32_t* arrivals = ep + 1;
+  if (t == 0) s_e = __hip_atomic_load(ep, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + 1u;
+  __syncthreads();
+  const uint32_t e = s_e;
+  const size_t data = AR_DATA + (size_t)(e & 1u) * max_bytes;
+  const size_t rbuf = AR_DATA + 2 * (size_t)max_bytes + (size_t)(e & 1u) * max_bytes;
+  const size_t ssbuf = rbuf + (size_t)T * H * 2;  // [T] fp32 slice sums of squares (two-shot)
+  const int nv = H >> 3;
+
+  // 1) stage this rank's rows
+  for (int row = b; row < T; row += nb)
+    for (int i = t; i < nv; i += AN_THREADS)
+      *reinterpret_cast<u16x8*>(own + data + 2 * ((size_t)row * H + 8 * i)) =
+          *reinterpret_cast<const u16x8*>(in + (size_t)row * H + 8 * i);
+  ar_publish(P, AR_FLAGS_A, world, rank, b, e, fence_all);
+  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
+
+  if (!TWO_SHOT) {
+    for (int row = b; row < T; row += nb) {
+      u16x8 wv[AN_NC];
+      float v[AN_NC][8];
+      float ss = 0.f;
+#pragma unroll
+      for (int c = 0; c < AN_NC; ++c) {
+        const int i = t + c * AN_THREADS;
+        if (i < nv) {
+          wv[c] = *reinterpret_cast<const u16x8*>(w + 8 * i);
+          const u16x8 a = ar_sum8(P, world, data + 2 * ((size_t)row * H + 8 * i));
+          uint16_t* rr = res + (size_t)row * H + 8 * i;
+          const u16x8 r0 = *reinterpret_cast<const u16x8*>(rr);
+          u16x8 sv;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            sv[j] = f2bf(bf2f(a[j]) + bf2f(r0[j]));
+            v[c][j] = bf2f(sv[j]);
+            ss += v[c][j] * v[c][j];
+          }
+          *reinterpret_cast<u16x8*>(rr) = sv;
+        }
+      }
+      const float inv = rsqrtf(an_block_sum(ss, scratch) / (float)H + eps);
+#pragma unroll
+      for (int c = 0; c < AN_NC; ++c) {
+        const int i = t + c * AN_THREADS;
+        if (i < nv) {
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(v[c][j] * inv * bf2f(wv[c][j]));
+          *reinterpret_cast<u16x8*>(y + (size_t)row * H + 8 * i) = o;
+        }
+      }
+    }
+  } else {
+    const int sl = nv / world;  // 16-B chunks per rank slice (host-checked: nv % world == 0)
+    const int c0 = rank * sl;
+    for (int row = b; row < T; row += nb) {
+      float ss = 0.f;
+      for (int i = c0 + t; i < c0 + sl; i += AN_THREADS) {
+        const u16x8 a = ar_sum8(P, world, data + 2 * ((size_t)row * H + 8 * i));
+        const u16x8 r0 = *reinterpret_cast<const u16x8*>(res + (size_t)row * H + 8 * i);
+        u16x8 sv;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          sv[j] = f2bf(bf2f(a[j]) + bf2f(r0[j]));
+          const float vj = bf2f(sv[j]);
+          ss += vj * vj;
+        }
+        *reinterpret_cast<u16x8*>(own + rbuf + 2 * ((size_t)row * H + 8 * i)) = sv;
+      }
+      const float tot = an_block_sum(ss, scratch);
+      if (t == 0) *reinterpret_cast<float*>(own + ssbuf + 4 * (size_t)row) = tot;
+    }
+    ar_publish(P, AR_FLAGS_B, world, rank, b, e, fence_all);
+    ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks, sim);
+    for (int row = b; row < T; row += nb) {
+      float tot = 0.f;
+      for (int p = 0; p < world; ++p) tot += *reinterpret_cast<const float*>(P.base[p] + ssbuf + 4 * (size_t)row);
+      const float inv = rsqrtf(tot / (float)H + eps);
+      for (int i = t; i < nv; i += AN_THREADS) {
+        const int owner = i / sl;
+        const u16x8 sv = *reinterpret_cast<const u16x8*>(P.base[owner] + rbuf + 2 * ((size_t)row * H + 8 * i));
+        const u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * i);
+        *reinterpret_cast<u16x8*>(res + (size_t)row * H + 8 * i) = sv;
+        u16x8 o;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(sv[j]) * inv * bf2f(wv[j]));
+        *reinterpret_cast<u16x8*>(y + (size_t)row * H + 8 * i) = o;
+      }
+    }
+  }
+  __syncthreads();
+  if (t == 0) {  // the last block of this call publishes the epoch for the next one
+    const uint32_t d = __hip_atomic_fetch_add(arrivals, 1u, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+    if (d == gridDim.x - 1) {
+      __hip_atomic_store(arrivals, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ep, e, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
 // Fixed-size all-to-all (EP token dispatch / combine, B15) over the same IPC
 // buffers and the same per-call epoch as the all-reduce (calls of both kinds
 // share one epoch sequence, issued in the same order on every rank).  Send
@@ -343,6 +484,29 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
   else
     hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
                        (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
+  return (int)hipGetLastError();
+}
+
+// Fused TP epilogue (ar_addnorm_kernel): in [T][H] bf16 partial -> res (in/out)
+// and y [T][H]; mode 1 one-shot, 2 two-shot.  Same epoch sequence as the
+// all-reduce: issue it in the same order on every rank.
+K8S_API int k8s_ar_addnorm_bf16(int id, const void* in, void* res, const void* w, void* y, int T, int H, float eps,
+                                int mode, hipStream_t s) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  const ARCtx& c = g_ctx[id];
+  if (T <= 0) return 0;
+  const long need = (long)T * H * 2 + 4L * T;  // staged rows / (two-shot) slice sums + sums of squares
+  if (H % 8 || H / 8 > AN_THREADS * AN_NC || need > c.max_bytes || (mode == 2 && (H / 8) % c.world))
+    return (int)hipErrorInvalidValue;
+  const int nb = T < AR_MAX_BLOCKS ? T : AR_MAX_BLOCKS;
+  if (mode == 2)
+    hipLaunchKernelGGL(ar_addnorm_kernel<true>, dim3(nb), dim3(AN_THREADS), 0, s, (const uint16_t*)in,
+                       (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps, c.world, c.rank, c.peers,
+                       c.max_bytes, c.timeout_ticks, c.sim, fence_all());
+  else
+    hipLaunchKernelGGL(ar_addnorm_kernel<false>, dim3(nb), dim3(AN_THREADS), 0, s, (const uint16_t*)in,
+                       (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps, c.world, c.rank, c.peers,
+                       c.max_bytes, c.timeout_ticks, c.sim, fence_all());
   return (int)hipGetLastError();
 }
 

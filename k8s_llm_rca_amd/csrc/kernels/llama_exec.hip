@@ -57,6 +57,8 @@ int k8s_grouped_gemm_part(const void* a, int lda, const void* w, void* y, int ld
 int k8s_blaslt_gemm(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, void* ws,
                     size_t ws_bytes, hipStream_t s);
 int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int mode, hipStream_t s);
+int k8s_ar_addnorm_bf16(int id, const void* in, void* res, const void* w, void* y, int T, int H, float eps, int mode,
+                        hipStream_t s);
 int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg, int splits,
                     void* part, hipStream_t s);
 int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
@@ -120,8 +122,10 @@ struct K8sLlamaStep {
   void* mid_part;
   void* grp_part;
   const int* grp_offs;  // device [0, T]
-  // TP: xGMI all-reduce communicator id (-1: TP = 1) and mode (1 one-shot, 2 two-shot)
-  int ar_id, ar_mode;
+  // TP: xGMI all-reduce communicator id (-1: TP = 1) and mode (1 one-shot, 2 two-shot);
+  // ar_fuse: the all-reduce + residual add + RMSNorm of each row-parallel output in
+  // one launch (k8s_ar_addnorm_bf16) instead of all-reduce, then rmsnorm
+  int ar_id, ar_mode, ar_fuse;
 };
 
 namespace {
@@ -220,6 +224,7 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   uint16_t* attn = (uint16_t*)s.attn;
   bool pend = false;  // the previous layer's down projection is still split-K partials
   const bool tp = s.ar_id >= 0;  // row-parallel outputs are partial sums: all-reduce, never defer split-K
+  const bool fuse_an = tp && s.ar_fuse;  // the previous layer's down all-reduce already produced y
   const long n_out = (long)T * H;
   Overlap& ov = overlap_state();
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
@@ -229,7 +234,9 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
-    else if (pend)
+    else if (fuse_an) {
+      // y = rmsnorm(all-reduced down_proj + residual): done by the previous layer's fused epilogue
+    } else if (pend)
       K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[3]), s.sel[3].splits, s.residual, s.in_norm[l], s.y, T, H, H,
                                  s.eps, st));
     else
@@ -263,8 +270,13 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                               conc ? (s.d_grid < ov.grid ? s.d_grid : ov.grid) : s.d_grid, st));
     if (conc) K8S_TRY((int)hipStreamWaitEvent(st, ov.join, 0));
     K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
-    if (tp) K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
-    if (!tp && deferred(s.sel[1], true))
+    if (fuse_an)
+      K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.obuf, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode, st));
+    else if (tp)
+      K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
+    if (fuse_an) {
+      // residual add + post-attention norm done above
+    } else if (!tp && deferred(s.sel[1], true))
       K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[1]), s.sel[1].splits, s.residual, s.post_norm[l], s.y, T, H, H,
                                  s.eps, st));
     else
@@ -274,7 +286,10 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
     K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));
-    if (tp) K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.prev, s.prev, n_out, s.ar_mode, st));
+    if (fuse_an && l + 1 < s.L)  // the next layer's input norm rides on this all-reduce
+      K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.prev, s.residual, s.in_norm[l + 1], s.y, T, H, s.eps, s.ar_mode, st));
+    else if (tp)
+      K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.prev, s.prev, n_out, s.ar_mode, st));
   }
   return (int)hipGetLastError();
 }

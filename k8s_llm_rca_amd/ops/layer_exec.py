@@ -42,11 +42,13 @@ class LlamaStep(ctypes.Structure):
         ("p_bt_stride", I), ("p_S", I), ("n_tiles", I), ("n_merge", I),
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
-        ("ar_id", I), ("ar_mode", I),
+        ("ar_id", I), ("ar_mode", I), ("ar_fuse", I),
     ]
 
 
 _enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
+# TP: all-reduce + residual add + RMSNorm of every row-parallel output in one launch
+_fuse_ar_norm = os.environ.get("K8SRCA_TP_FUSED_NORM", "1") == "1"
 # split-K o / down projections reduced inside the following residual add + RMSNorm
 _fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
 _checked = False
@@ -103,6 +105,7 @@ class LlamaExecutor:
         self._car = car
         st.ar_id = car.id if car is not None else -1
         st.ar_mode = 1
+        st.ar_fuse = 0
 
     @staticmethod
     def eligible(model) -> bool:
@@ -115,7 +118,7 @@ class LlamaExecutor:
         car = self._car
         if car is None:
             return True
-        nb = T * self.m.cfg.hidden * 2
+        nb = T * self.m.cfg.hidden * 2 + (4 * T if _fuse_ar_norm else 0)  # + the fused epilogue's row sums
         return nb <= car.max_bytes and (T * self.m.cfg.hidden) % 8 == 0
 
     def _bind_kv(self, k_cache: torch.Tensor, v_cache: torch.Tensor) -> None:
@@ -148,6 +151,8 @@ class LlamaExecutor:
         if self._car is not None:
             from ..parallel.xgmi import ONE_SHOT_MAX
             st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
+            # the two-shot epilogue splits each row's 16-B chunks evenly over the ranks
+            st.ar_fuse = int(_fuse_ar_norm and (st.ar_mode == 1 or (H // 8) % self._car.world == 0))
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)

@@ -50,6 +50,7 @@ def _bind(L) -> None:
         "k8s_ar_alltoall_bf16": ([c_int, P, P, c_long, P], c_int),
         "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
         "k8s_ar_status_async": ([c_int, P, P], c_int),
+        "k8s_ar_addnorm_bf16": ([c_int, P, P, P, P, c_int, c_int, ctypes.c_float, c_int, P], c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -114,6 +115,19 @@ class XgmiAllReduce:
         _check(self.L.k8s_ar_allreduce_bf16(self.id, t.data_ptr(), t.data_ptr(), t.numel(), m, stream_ptr(t)),
                "k8s_ar_allreduce_bf16")
         return t
+
+    def addnorm(self, x: torch.Tensor, residual: torch.Tensor, w: torch.Tensor, y: torch.Tensor, eps: float,
+                mode: Optional[int] = None) -> torch.Tensor:
+        """The TP row-parallel epilogue in one launch: ``residual += all_reduce(x)``
+        (bf16-rounded sum, then the add rounded to bf16), ``y = rmsnorm(residual) * w``.
+        One-shot is bit-identical to ``self(x)`` + the rmsnorm kernel; two-shot
+        computes the row's sum of squares from per-rank slice sums (the same
+        value on every rank)."""
+        T, H = x.shape
+        m = mode or (1 if T * H * 2 <= ONE_SHOT_MAX else 2)
+        _check(self.L.k8s_ar_addnorm_bf16(self.id, x.data_ptr(), residual.data_ptr(), w.data_ptr(), y.data_ptr(), T,
+                                          H, float(eps), m, stream_ptr(x)), "k8s_ar_addnorm_bf16")
+        return y
 
     def all_to_all(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
         """Equal-split all-to-all: ``send`` [world, chunk...] bf16 -> ``recv`` (same

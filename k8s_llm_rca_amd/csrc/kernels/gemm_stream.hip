@@ -32,15 +32,31 @@ constexpr int kSBN = 64;  // columns per workgroup
 
 __device__ __forceinline__ int sswz(int n, int j) { return j ^ (n & 7); }
 
+// W row (relative to the strip's first row) of strip row n, 16-row fragment
+// f = n / 16 of NF.  Plain: n.  SwiGLU form (silu_i = I > 0, W = [Wg; Wu] of
+// 2I rows, strip base = the first gate row of the strip's 8 NF act columns):
+// fragments [0, NF/2) are gate rows, [NF/2, NF) the up rows of the same act
+// columns, so fragment f and f + NF/2 of one lane hold gate and up of one
+// (row, column) of the product.
+template <int NF>
+__device__ __forceinline__ int strip_row(int n, int silu_i) {
+  if (!silu_i) return n;
+  const int f = n >> 4, half = NF / 2;
+  return (f >= half ? silu_i : 0) + (f % half) * 16 + (n & 15);
+}
+
+__device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
+
 template <int MTW, int U>
 __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __restrict__ x, int ldx,
                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                           int ldy, float* __restrict__ part, int M, int N, int K,
-                                                          int kslice) {
+                                                          int kslice, int silu_i) {
   __shared__ __attribute__((aligned(16))) uint16_t ws[2][kSBN * kSC];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
-  const int n0 = blockIdx.x * kSBN;
+  // strip: 64 W rows (plain: output columns n0 ..; SwiGLU: 32 act columns n0 ..)
+  const int n0 = blockIdx.x * (silu_i ? kSBN / 2 : kSBN);
   const int split = blockIdx.y;
   const int kbeg = split * kslice;
   const int nch = kslice / kSC;
@@ -53,7 +69,7 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
   for (int i = 0; i < 2; ++i) {
     const int p = tid + 256 * i;
     const int n = p >> 3, jl = p & 7;
-    wsrc[i] = w + (size_t)(n0 + n) * K + kbeg + 8 * sswz(n, jl);
+    wsrc[i] = w + (size_t)(n0 + strip_row<4>(n, silu_i)) * K + kbeg + 8 * sswz(n, jl);
     wdst[i] = n * kSC + 8 * jl;
   }
   // ---- X fragments: row of frag mt for this lane (clamped; masked at the store)
@@ -132,7 +148,20 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
 
   // ---- epilogue: acc[mt][cf][v] = C[m = m_base + 16 mt + 4 g + v][n = n0 + 16 cf + r]
   if (!active) return;
-  if (gridDim.y == 1) {
+  if (silu_i) {  // act = silu(gate) * up, with the unfused path's bf16 rounding of both
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m_base + 16 * mt + 4 * g + v;
+        if (m < M) {
+#pragma unroll
+          for (int cf = 0; cf < 2; ++cf)
+            y[(size_t)m * ldy + n0 + 16 * cf + r] =
+                f2bf(silu_f(bf2f(f2bf(acc[mt][cf][v]))) * bf2f(f2bf(acc[mt][cf + 2][v])));
+        }
+      }
+  } else if (gridDim.y == 1) {
 #pragma unroll
     for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
@@ -209,7 +238,7 @@ constexpr int glds_lds_elems() {
 template <int MTW, int NB, int NF = 4>
 __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int ldx, int M,
                                            const uint16_t* __restrict__ wstrip, int K, int nch, uint16_t* sm,
-                                           f32x4 (&acc)[MTW][NF]) {
+                                           f32x4 (&acc)[MTW][NF], int silu_i = 0) {
   constexpr int MP = 64 * MTW;         // X rows staged: 4 waves x MTW 16-row fragments
   constexpr int WST = 16 * NF * kSC;   // W stage: 16 NF rows x 64 k
   constexpr int STG = WST + MP * kSC;  // elements per stage
@@ -224,7 +253,7 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
 #pragma unroll
   for (int i = 0; i < WPT; ++i) {
     const int p = 256 * i + tid, n = p >> 3, jl = p & 7;
-    wsrc[i] = wstrip + (size_t)n * K + 8 * (jl ^ (n & 7));
+    wsrc[i] = wstrip + (size_t)strip_row<NF>(n, silu_i) * K + 8 * (jl ^ (n & 7));
   }
   const uint16_t* xsrc[XPT];
 #pragma unroll
@@ -285,11 +314,26 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
 // of y (final) or fp32 rows of `part` (split-K partial), rows < M only.
 template <int MTW, int NF = 4>
 __device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][NF], int M, uint16_t* __restrict__ y, int ldy,
-                                           float* __restrict__ pp, int ldp) {
+                                           float* __restrict__ pp, int ldp, bool silu = false) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, g = lane >> 4;
   const int m_base = wv * 16 * MTW;
   if (m_base >= M) return;
+  if (silu) {  // fragments [0, NF/2) gate, [NF/2, NF) up: act columns 16 cf + r of the strip
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+      for (int v = 0; v < 4; ++v) {
+        const int m = m_base + 16 * mt + 4 * g + v;
+        if (m < M) {
+#pragma unroll
+          for (int cf = 0; cf < NF / 2; ++cf)
+            y[(size_t)m * ldy + 16 * cf + r] =
+                f2bf(silu_f(bf2f(f2bf(acc[mt][cf][v]))) * bf2f(f2bf(acc[mt][cf + NF / 2][v])));
+        }
+      }
+    return;
+  }
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
@@ -311,16 +355,19 @@ template <int MTW, int NB, int NF>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                         int ldy, float* __restrict__ part, int M, int N, int K,
-                                                        int kslice) {
+                                                        int kslice, int silu_i) {
   __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<MTW, NB, NF>()];
-  const int n0 = blockIdx.x * 16 * NF, split = blockIdx.y, kbeg = split * kslice;
+  // strip: 16 NF W rows (plain: output columns n0 ..; SwiGLU: 8 NF act columns n0 ..)
+  const int n0 = blockIdx.x * (silu_i ? 8 : 16) * NF, split = blockIdx.y, kbeg = split * kslice;
   f32x4 acc[MTW][NF];
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
     for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  glds_strip<MTW, NB, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc);
-  if (gridDim.y == 1)
+  glds_strip<MTW, NB, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
+  if (silu_i)
+    glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0, true);
+  else if (gridDim.y == 1)
     glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0);
   else
     glds_store<MTW, NF>(acc, M, nullptr, 0, part + (size_t)split * M * N + n0, N);
@@ -386,16 +433,17 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_kernel(const float* __
 
 template <int MTW, int NB, int NF = 4>
 static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
-                              int ldy, float* part, int M, int N, int K, int kslice) {
+                              int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
   hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K,
-                     kslice);
+                     kslice, silu_i);
   return hipGetLastError();
 }
 
 template <int MTW, int U>
 static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
-                                int ldy, float* part, int M, int N, int K, int kslice) {
-  hipLaunchKernelGGL((gemm_stream_kernel<MTW, U>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K, kslice);
+                                int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
+  hipLaunchKernelGGL((gemm_stream_kernel<MTW, U>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K, kslice,
+                     silu_i);
   return hipGetLastError();
 }
 
@@ -407,13 +455,16 @@ using namespace k8s;
 // stages; 5 and 6 for M <= 64), or 20 + NB for the LDS-DMA kernel on 128-column
 // strips (NB = 3, or 4 for M <= 192; N % 128 == 0).  splits > 1 needs `part` =
 // splits * M * N fp32; reduce = 0 leaves the partials for a fused consumer.
+// silu: w is the gate_up weight [2N][K] (gate rows first) and y[M][N] = silu(x Wg^T) * (x Wu^T)
+// (splits == 1 only: the nonlinearity needs the whole K sum).
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
-                         int splits, void* part, bool reduce, hipStream_t s) {
-  const int bn = cfg > 20 ? 128 : kSBN;  // strip width
+                         int splits, void* part, bool reduce, hipStream_t s, bool silu = false) {
+  const int bn = (cfg > 20 ? 128 : kSBN) / (silu ? 2 : 1);  // output columns per strip
   if (M <= 0 || M > 256 || N % bn || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
       (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24) || ldx % 8 ||
-      (splits > 1 && (M * N) % 8) || ((splits == 1 || reduce) && ldy < N))  // y is written: rows of N
+      (splits > 1 && (M * N) % 8) || ((splits == 1 || reduce) && ldy < N) || (silu && splits != 1))
     return (int)hipErrorInvalidValue;
+  const int silu_i = silu ? N : 0;
   const int kslice = K / splits;
   // the register-ring loop is unrolled by U chunks with no partial trip
   if (cfg < 10 && (kslice / kSC) % cfg) return (int)hipErrorInvalidValue;
@@ -428,9 +479,9 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   uint16_t* yy = (uint16_t*)y;
   float* pp = (float*)part;
   hipError_t e;
-#define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
-#define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
-#define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice)
+#define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
+#define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
+#define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
   if (cfg == 23) {
     switch (mtw) {
       case 1: K8S_GW(1, 3); break;
@@ -490,6 +541,13 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
 K8S_API int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                             int splits, void* part, hipStream_t s) {
   return stream_launch(x, ldx, w, y, ldy, M, N, K, cfg, splits, part, true, s);
+}
+
+// y[M][N] = silu(x . w[0:N]^T) * (x . w[N:2N]^T): the gate_up projection with its
+// SwiGLU epilogue (the [M][2N] gate_up activation is never written); splits == 1.
+K8S_API int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
+                                 int cfg, hipStream_t s) {
+  return stream_launch(x, ldx, w, y, ldy, M, N, K, cfg, 1, nullptr, true, s, true);
 }
 
 K8S_API int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,

@@ -63,11 +63,17 @@ int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int ldy, int
                     void* part, hipStream_t s);
 int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, hipStream_t s);
+int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode, int pipe,
+                 hipStream_t s);
+int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
+                         hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
-// 4 gemm_stream (cfg = ring depth, splits);
-// fuse: a split-K o / down projection may leave its partials to the next norm
+// 4 gemm_stream (cfg = ring depth, splits), 5 gemm_big (cfg = pipe);
+// fuse: 1 -- a split-K o / down projection may leave its partials to the next norm;
+// 2 (gate_up, kinds 4 / 5 with one K split) -- the SwiGLU-epilogue form, which
+// writes act directly (gu is never written, no silu_mul launch)
 struct K8sGemmSel {
   int kind, cfg, splits, fuse;
 };
@@ -157,6 +163,8 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
     case 4:
       return (d ? k8s_gemm_stream_part : k8s_gemm_stream)(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part,
                                                           st);
+    case 5:
+      return k8s_gemm_big(x, ldx, w, y, ldy, M, N, K, 0, g.cfg, st);
     default:
       return k8s_blaslt_gemm(x, ldx, w, y, ldy, M, N, K, s.blaslt_ws, s.blaslt_ws_bytes, st);
   }
@@ -281,8 +289,14 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                                  s.eps, st));
     else
       K8S_TRY(k8s_rmsnorm(s.obuf, s.residual, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
-    K8S_TRY(gemm(s, s.sel[2], s.y, H, s.wgu[l], s.gu, 2 * s.I, T, 2 * s.I, H, st));
-    K8S_TRY(k8s_silu_mul(s.gu, s.act, T, s.I, st));
+    if (s.sel[2].fuse == 2 && s.sel[2].kind == 5) {  // gate_up + SwiGLU in one launch: gu is never written
+      K8S_TRY(k8s_gemm_big(s.y, H, s.wgu[l], s.act, s.I, T, s.I, H, 1, s.sel[2].cfg, st));
+    } else if (s.sel[2].fuse == 2 && s.sel[2].kind == 4) {
+      K8S_TRY(k8s_gemm_stream_silu(s.y, H, s.wgu[l], s.act, s.I, T, s.I, H, s.sel[2].cfg, st));
+    } else {
+      K8S_TRY(gemm(s, s.sel[2], s.y, H, s.wgu[l], s.gu, 2 * s.I, T, 2 * s.I, H, st));
+      K8S_TRY(k8s_silu_mul(s.gu, s.act, T, s.I, st));
+    }
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
     K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));

@@ -210,6 +210,8 @@ class LLMEngine:
                                                       max_m=cfg.max_batch_tokens)
                 self.t_gemm_tune = time.perf_counter() - t_tune
             self.gemm_dispatch = LIN.load_dispatch(LIN.dispatch_path(self.mc.name, self.pc.tp_size))
+            # prefill-size M ranges where the hand-written gemm_big beats hipBLASLt
+            self.big_gemm_ranges = LIN.load_big(LIN.big_path(self.mc.name, self.pc.tp_size))
             if self.gemm_dispatch:  # split-K scratch exists before any HIP-graph capture
                 LIN.reserve_dispatch_scratch(self.device)
             else:

@@ -28,7 +28,7 @@ import torch.nn.functional as F
 from ..ops import attention as A
 from ..ops import layer_exec as LX
 from ..ops import norm as N
-from ..ops.linear import linear, linear_f32out, linear_silu
+from ..ops.linear import linear, linear_f32out, linear_silu, swiglu_gemm
 from ..parallel.groups import ParallelContext, single
 from .config import ModelConfig
 from . import moe as MOE
@@ -191,6 +191,10 @@ class LlamaModel:
             if self.moe is not None:
                 prev = self.moe.forward(li, y)
             else:
+                act = swiglu_gemm(y, L["w_gu"])  # gate_up + SwiGLU in one launch where measured faster
+                if act is not None:
+                    prev = self.pc.linear_all_reduce(act, L["w_down"], linear_fn=linear)
+                    continue
                 gu = linear(y, L["w_gu"])
                 if self.pc.tp_size == 1:
                     prev = linear_silu(gu, L["w_down"])  # SwiGLU fused into the down GEMM's operand staging

@@ -184,9 +184,11 @@ class LlamaExecutor:
         shapes = ((ld_qkv, H_), (H_, m.nq * m.D), (2 * I_, H_), (H_, I_))
         need_mid = need_grp = 0
         for i, (N, K) in enumerate(shapes):
-            kind, cfg, splits = LIN.select_gemm(T, N, K)
+            fused = LIN.swiglu_choice(T, N, K) if i == 2 else None  # the SwiGLU-epilogue gate_up (writes act)
+            # otherwise the choice LIN.linear makes (models/llama.py's path)
+            kind, cfg, splits = fused or LIN.select_gemm(T, N, K)
             st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
-            st.sel[i].fuse = int(_fuse_splitk)
+            st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
             if kind in (LIN.KIND_MID, LIN.KIND_STREAM) and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:

@@ -23,7 +23,7 @@ def set_skinny(enabled: bool) -> None:
     _enabled = enabled
 
 
-KIND_LIB, KIND_SKINNY, KIND_MID, KIND_GRP, KIND_STREAM = 0, 1, 2, 3, 4
+KIND_LIB, KIND_SKINNY, KIND_MID, KIND_GRP, KIND_STREAM, KIND_BIG = 0, 1, 2, 3, 4, 5
 
 
 def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bool = True) -> Tuple[int, int, int]:
@@ -45,6 +45,8 @@ def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bo
             if kind == "lib":
                 return KIND_LIB, 0, 1
             forced_skinny = kind == "skinny" and M <= 128
+    if M > DISPATCH_MAX_M and x_ok_layout and _big_pick(M, N, K):
+        return KIND_BIG, BIG_PIPE, 1
     if (_enabled and (M == 1 or forced_skinny or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
             and x_ok_layout and K % 256 == 0 and N % 16 == 0):
         return KIND_SKINNY, 0, 1
@@ -65,6 +67,8 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
         return gemm_grp(x, w, splits, out)
     if kind == KIND_STREAM:
         return gemm_stream(x, w, cfg, splits, out)
+    if kind == KIND_BIG:
+        return gemm_big(x, w, out, pipe=cfg)
     if kind == KIND_SKINNY:
         if out is None:
             out = torch.empty((M, N), dtype=x.dtype, device=x.device)
@@ -356,6 +360,129 @@ def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
     part = _scratch(x.device, splits * M * N) if splits > 1 else None
     check(lib().k8s_gemm_stream(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, cfg, splits,
                                 ptr(part), stream_ptr(x)), "gemm_stream")
+    return out
+
+
+BIG_PIPE = int(os.environ.get("K8SRCA_BIG_PIPE", "1"))
+# Prefill-size dispatch between gemm_big and hipBLASLt: per (N, K) the M ranges
+# where the hand-written kernel measured faster (data/gemm_big_<model>.json,
+# tools/big_gemm_ab.py --emit), separately for the SwiGLU-fused gate_up form
+# (against hipBLASLt + silu_mul).  K8SRCA_BIG_GEMM=0 disables it;
+# K8SRCA_BIG_GEMM=all uses gemm_big for every shape it accepts above
+# DISPATCH_MAX_M (A/B runs).
+_big_mode = os.environ.get("K8SRCA_BIG_GEMM", "1")
+_big_ranges: Dict[Tuple, List[Tuple[int, int]]] = {}
+
+
+def big_path(model: str, tp: int = 1) -> str:
+    return os.path.join(DATA_DIR, f"gemm_big_{model}" + (f"-tp{tp}" if tp > 1 else "") + ".json")
+
+
+def load_big(path: str) -> int:
+    """Register the measured gemm_big M ranges of ``path``; returns how many."""
+    _big_ranges.clear()
+    if _big_mode == "0" or not os.path.exists(path):
+        return 0
+    with open(path) as f:
+        d = json.load(f)
+    n = 0
+    for tag, silu in (("ranges", False), ("silu", True)):
+        for key, rows in d.get(tag, {}).items():
+            N, K = (int(v) for v in key.split(","))
+            _big_ranges[("silu", N, K) if silu else (N, K)] = [(int(lo), int(hi)) for lo, hi in rows]
+            n += len(rows)
+    return n
+
+
+def set_big(mode: str) -> None:
+    global _big_mode
+    _big_mode = mode
+
+
+def _big_pick(M: int, N: int, K: int, silu: bool = False) -> bool:
+    """gemm_big for this (M, N, K)?  ``N`` is the weight's row count (2I for
+    the SwiGLU form)."""
+    if _big_mode == "0" or M <= DISPATCH_MAX_M:
+        return False
+    if not big_shape_ok(M, N // 2 if silu else N, K, silu):
+        return False
+    if _big_mode == "all":
+        return True
+    for lo, hi in _big_ranges.get(("silu", N, K) if silu else (N, K), ()):
+        if lo <= M <= hi:
+            return True
+    return False
+
+
+# SwiGLU epilogue on the decode stream kernel: where the dispatch table picks
+# gemm_stream with one K split for gate_up, the SwiGLU form of the same strip
+# kernel (64-row W strips = 32 gate + 32 up rows) replaces gate_up + silu_mul --
+# the same weight bytes, no [M, 2I] write and re-read, one launch fewer.
+_stream_silu = os.environ.get("K8SRCA_STREAM_SILU", "1") == "1"
+
+
+def swiglu_choice(M: int, N2: int, K: int):
+    """(kind, cfg, splits) of the SwiGLU-epilogue gate_up GEMM for ``M`` rows of
+    a [N2 = 2I, K] gate_up weight, or ``None`` (gate_up GEMM + silu_mul)."""
+    if _big_pick(M, N2, K, silu=True):
+        return KIND_BIG, BIG_PIPE, 1
+    if _stream_silu and _dispatch and M <= DISPATCH_MAX_M and (N2 // 2) % 64 == 0:
+        kind, cfg, splits = select_gemm(M, N2, K)
+        if kind == KIND_STREAM and splits == 1:
+            return KIND_STREAM, cfg, 1
+    return None
+
+
+def gemm_stream_silu(x: torch.Tensor, w: torch.Tensor, cfg: int, out: torch.Tensor = None) -> torch.Tensor:
+    """``silu(x @ Wg.T) * (x @ Wu.T)`` on the decode stream kernel (w = [Wg; Wu])."""
+    M, K = x.shape
+    N = w.shape[0] // 2
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    check(lib().k8s_gemm_stream_silu(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, cfg,
+                                     stream_ptr(x)), "gemm_stream_silu")
+    return out
+
+
+def swiglu_gemm(y: torch.Tensor, w_gu: torch.Tensor):
+    """``silu_mul(y @ w_gu.T)`` in one launch (gemm_big's or the stream kernel's
+    SwiGLU epilogue) where :func:`swiglu_choice` picks one; ``None`` otherwise
+    (the caller runs the gate_up GEMM + silu_mul)."""
+    M, K = y.shape
+    if not (y.is_cuda and y.dtype == torch.bfloat16 and y.stride(1) == 1 and y.stride(0) % 8 == 0
+            and w_gu.is_contiguous()):
+        return None
+    ch = swiglu_choice(M, w_gu.shape[0], K)
+    if ch is None:
+        return None
+    if ch[0] == KIND_BIG:
+        return gemm_big(y, w_gu, silu=True, pipe=ch[1])
+    return gemm_stream_silu(y, w_gu, ch[1])
+
+
+def big_shape_ok(M: int, N: int, K: int, silu: bool = False) -> bool:
+    """What csrc/kernels/gemm_big.hip accepts: 256-column tiles (128 act
+    columns for the SwiGLU form), 32-deep chunks."""
+    return M > 0 and K % 32 == 0 and N % (128 if silu else 256) == 0
+
+
+def gemm_big(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, silu: bool = False,
+             pipe: int = None) -> torch.Tensor:
+    """``x @ w.T`` on the prefill-size MFMA kernel (csrc/kernels/gemm_big.hip:
+    256 x 256 tiles, LDS-DMA ring).  ``silu=True``: ``w`` is the gate_up weight
+    [2I, K] and the result is ``silu(x @ Wg.T) * (x @ Wu.T)`` [M, I] -- the
+    SwiGLU epilogue, with the unfused path's bf16 rounding of gate and up."""
+    M, K = x.shape
+    N = w.shape[0] // 2 if silu else w.shape[0]
+    if not (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0
+            and w.is_contiguous() and w.shape[1] == K and big_shape_ok(M, N, K, silu)):
+        raise ValueError(f"gemm_big: unsupported operands x {tuple(x.shape)} w {tuple(w.shape)} silu={silu}")
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if M == 0:
+        return out
+    check(lib().k8s_gemm_big(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, int(silu),
+                             BIG_PIPE if pipe is None else pipe, stream_ptr(x)), "gemm_big")
     return out
 
 

@@ -796,3 +796,67 @@ def test_sampling_top_p_and_tie_candidates_deterministic():
     assert all(torch.equal(c, outs[0]) for c in outs)
     ids = outs[0][:, :, 1]
     assert bool((ids >= 16032).all()) and bool((ids[:, 1:] > ids[:, :-1]).all())  # valid, (v desc, id asc)
+
+
+@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 32), (100, 512, 96), (256, 1024, 4096), (300, 768, 256),
+                                   (1000, 6144, 512), (2085, 4096, 1024), (4096, 256, 14336)])
+def test_gemm_big_vs_fp32(M, N, K, pipe):
+    """Prefill-size GEMM (csrc/kernels/gemm_big.hip: 256 x 256 tiles, LDS-DMA
+    ring, XCD-grouped tile order) vs fp32, M tails, K of 1..448 chunks, plus an
+    asymmetric exact check (one-hot rows pick weight columns)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(M + N + K)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    y = LIN.gemm_big(x, w, pipe=pipe)
+    ref = x.float() @ w.float().t()
+    torch.testing.assert_close(y.float(), ref, atol=2e-2, rtol=2e-2)
+    e = torch.zeros(M, K, device=dev).bfloat16()
+    idx = torch.arange(M, device=dev) * 37 % K
+    e[torch.arange(M, device=dev), idx] = 1.0
+    ye = LIN.gemm_big(e, w, pipe=pipe)
+    assert torch.equal(ye, w[:, idx].t().contiguous())
+    # a strided x (a row slice of a wider buffer) and a strided output
+    xb = torch.randn(M, K + 64, device=dev).bfloat16()
+    yb = torch.zeros(M, N + 256, device=dev).bfloat16()
+    LIN.gemm_big(xb[:, :K], w, out=yb[:, :N], pipe=pipe)
+    torch.testing.assert_close(yb[:, :N].float(), xb[:, :K].float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    assert torch.count_nonzero(yb[:, N:]) == 0
+
+
+@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("M,I,K", [(5, 128, 64), (300, 384, 512), (1500, 1024, 4096)])
+def test_gemm_big_silu_epilogue(M, I, K, pipe):
+    """SwiGLU epilogue of gemm_big (gate_up never written) == the unfused
+    gemm_big + silu_mul bit for bit, and fp32 silu(x Wg^T) * (x Wu^T)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(M + I)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(2 * I, K, device=dev) * 0.05).bfloat16()
+    act = LIN.gemm_big(x, w, silu=True, pipe=pipe)
+    gu = LIN.gemm_big(x, w, pipe=pipe)
+    assert torch.equal(act, N.silu_mul(gu))
+    g, u = (x.float() @ w.float().t()).split(I, dim=1)
+    torch.testing.assert_close(act.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 17, 48, 128, 200])
+@pytest.mark.parametrize("cfg", [4, 8, 13, 14, 23, 24])
+def test_gemm_stream_silu_epilogue(M, cfg):
+    """SwiGLU epilogue of the decode stream kernels (gate and up rows of one act
+    column in one strip) == gemm_stream + silu_mul bit for bit, and fp32."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    I, K = 1024, 512
+    if not (LIN.stream_shape_ok(M, 2 * I, K, cfg, 1)):
+        pytest.skip("shape outside this configuration's launch contract")
+    torch.manual_seed(M + cfg)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(2 * I, K, device=dev) * 0.05).bfloat16()
+    act = LIN.gemm_stream_silu(x, w, cfg)
+    assert torch.equal(act, N.silu_mul(LIN.gemm_stream(x, w, cfg, 1)))
+    g, u = (x.float() @ w.float().t()).split(I, dim=1)
+    torch.testing.assert_close(act.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)

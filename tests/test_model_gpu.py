@@ -1,4 +1,6 @@
 """Model-level numerics: HIP kernel path (bf16, MI355X) vs the fp32 PyTorch reference path (CPU)."""
+import os
+
 import pytest
 import torch
 
@@ -108,14 +110,17 @@ def test_mixtral_engine_graphs_match_eager():
 
 
 @pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True),
-                                           (False, "stream"), (True, "stream")])
+                                           (False, "stream"), (True, "stream"), (False, "big"), (True, "big")])
 def test_layer_executor_bit_identical(graphs, splitk):
     """The native layer executor (one C call per forward) issues the same
     kernels in the same order as the Python layer loop: every step's logits
     are bit-identical, for mixed prefill+decode steps and graph decode steps.
     ``splitk``: a dispatch table that sends the o / down projections to the
     split-K kernels (gemm_mid, grouped), whose partials the executor reduces
-    inside the following residual add + RMSNorm instead of a reduce kernel."""
+    inside the following residual add + RMSNorm instead of a reduce kernel.
+    ``"big"``: every projection above 256 rows on gemm_big (gate_up with its
+    SwiGLU epilogue) and the decode-size gate_up on the stream kernel's
+    SwiGLU epilogue."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
@@ -129,8 +134,15 @@ def test_layer_executor_bit_identical(graphs, splitk):
         for on in (False, True):
             LX.set_enabled(on)
             eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=512, use_graphs=graphs,
-                                         temperature=0.0, max_batch_tokens=256, graph_batch_sizes=(1, 2, 4, 8)))
-            if splitk:  # after the engine's own (absent) dispatch table was loaded
+                                         temperature=0.0, max_batch_tokens=1024 if splitk == "big" else 256,
+                                         graph_batch_sizes=(1, 2, 4, 8)))
+            if splitk == "big":
+                LIN.set_big("all")
+                LIN._dispatch[(2048, 512)] = [(16, "stream", 4, 1), (64, "stream", 13, 1), (256, "stream", 24, 1)]
+                assert LIN.swiglu_choice(300, 2048, 512)[0] == LIN.KIND_BIG
+                assert LIN.swiglu_choice(5, 2048, 512) == (LIN.KIND_STREAM, 4, 1)
+                assert LIN.select_gemm(300, 512, 1024)[0] == LIN.KIND_BIG
+            elif splitk:  # after the engine's own (absent) dispatch table was loaded
                 LIN._dispatch[(512, 1024)] = split_rows
                 if splitk == "stream":
                     assert LIN.select_gemm(6, 512, 1024)[0] == LIN.KIND_STREAM
@@ -159,6 +171,8 @@ def test_layer_executor_bit_identical(graphs, splitk):
     finally:
         LX.set_enabled(True)
         LIN._dispatch.pop((512, 1024), None)
+        LIN._dispatch.pop((2048, 512), None)
+        LIN.set_big(os.environ.get("K8SRCA_BIG_GEMM", "1"))
     (r0, l0), (r1, l1) = runs
     assert r0 == r1
     assert len(l0) == len(l1) and len(l0) > 2

@@ -1,0 +1,88 @@
+"""A/B of the prefill-size GEMM (csrc/kernels/gemm_big.hip) against hipBLASLt.
+
+Interleaved rounds in one process (cdna_hip_programming.md §5.4 rule 24), random
+operands, cold weights (one copy per layer of the model cycled through, like the
+engine's per-layer weights), Llama-3-8B projection shapes.  Prints per (shape, M)
+the median us and TFLOP/s of each arm, and for gate_up the SwiGLU-fused arm vs
+hipBLASLt + silu_mul.
+
+usage: python tools/big_gemm_ab.py [--ms 512,1024,...] [--rounds 5] [--layers 4]
+"""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
+
+from k8s_llm_rca_amd.ops import linear as LIN  # noqa: E402
+from k8s_llm_rca_amd.ops import norm as NRM  # noqa: E402
+
+
+def timed(fn, iters):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(iters):
+        fn(i)
+    e.record()
+    torch.cuda.synchronize()
+    return s.elapsed_time(e) * 1e3 / iters
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ms", default="512,1024,1536,2048,3072,3584,4096,6144,8192")
+    ap.add_argument("--shapes", default="qkv,o,gu,down")
+    ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--iters", type=int, default=8)
+    ap.add_argument("--layers", type=int, default=4)
+    ap.add_argument("--pipes", default="0,1")
+    ap.add_argument("--out", default="")
+    a = ap.parse_args()
+    dev = torch.device("cuda")
+    H, I = 4096, 14336
+    shapes = {"qkv": (6144, H), "o": (H, H), "gu": (2 * I, H), "down": (H, I)}
+    pipes = [int(p) for p in a.pipes.split(",")]
+    rows = []
+    for name in a.shapes.split(","):
+        N, K = shapes[name]
+        ws = [(torch.rand(N, K, device=dev) * 2 - 1).mul_(0.02).bfloat16() for _ in range(a.layers)]
+        for M in (int(m) for m in a.ms.split(",")):
+            x = (torch.rand(M, K, device=dev) * 2 - 1).bfloat16()
+            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
+            arms = {"blaslt": lambda i: LIN.lib_gemm(x, ws[i % a.layers], y)}
+            for p in pipes:
+                arms[f"big{p}"] = lambda i, p=p: LIN.gemm_big(x, ws[i % a.layers], y, pipe=p)
+            if name == "gu":
+                act = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
+                arms["blaslt+silu"] = lambda i: NRM.silu_mul(LIN.lib_gemm(x, ws[i % a.layers], y), out=act)
+                for p in pipes:
+                    arms[f"big{p}_silu"] = lambda i, p=p: LIN.gemm_big(x, ws[i % a.layers], act, silu=True, pipe=p)
+            for fn in arms.values():  # warm-up (heuristics, code objects)
+                fn(0)
+            torch.cuda.synchronize()
+            res = {k: [] for k in arms}
+            for _ in range(a.rounds):
+                for k, fn in arms.items():
+                    res[k].append(timed(fn, a.iters))
+            flop = 2.0 * M * N * K
+            line = {"shape": name, "M": M, "N": N, "K": K}
+            for k, v in res.items():
+                med = statistics.median(v)
+                line[k] = round(med, 1)
+                line[k + "_tf"] = round(flop / med / 1e6, 0)
+            rows.append(line)
+            print(json.dumps(line), flush=True)
+            del x, y
+        del ws
+    if a.out:
+        with open(a.out, "w") as f:
+            for r in rows:
+                f.write(json.dumps(r) + "\n")
+
+
+if __name__ == "__main__":
+    main()

@@ -148,6 +148,57 @@ __global__ void __launch_bounds__(512) gemm_big_kernel(const uint16_t* __restric
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
       }
     }
+  } else if (PIPE == 2) {
+    // two explicit fragment sets: chunk c's MFMAs run on set c & 1 while chunk
+    // c+1's fragments stream into the other set, interleaved by
+    // sched_group_barrier (hipcc otherwise sinks every ds_read below the MFMAs,
+    // so each barrier exposed the full LDS latency: PIPE 1 ran at the PIPE 0 rate)
+    issue(NB - 1, min(NB - 1, nch - 1));
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 1) * LPC) : "memory");  // chunk 0 (this wave's part)
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    bf16x8 fa[2][8], fb[2][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) fb[0][j] = *reinterpret_cast<const bf16x8*>(sm + b_off + 16 * j * BK);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) fa[0][i] = *reinterpret_cast<const bf16x8*>(sm + a_off + 16 * i * BK);
+    for (int c0 = 0; c0 < nch; c0 += NB) {
+#pragma unroll
+      for (int u = 0; u < NB; ++u) {
+        const int c = c0 + u, cur = u & 1, nxt = cur ^ 1;
+        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NB - 2) * LPC) : "memory");
+        __builtin_amdgcn_s_barrier();  // all of chunk c+1 landed; every wave holds chunk c in registers
+        asm volatile("" ::: "memory");
+        if (c < nch) {
+          issue(u, min(c + NB, nch - 1));  // chunk c's stage is free: refill it with chunk c + NB
+          const uint16_t* nx = sm + ((u + 1) % NB) * STAGE;  // chunk c+1 (a clamped re-read past the end)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) fb[nxt][j] = *reinterpret_cast<const bf16x8*>(nx + b_off + 16 * j * BK);
+#pragma unroll
+          for (int i = 0; i < 8; ++i) fa[nxt][i] = *reinterpret_cast<const bf16x8*>(nx + a_off + 16 * i * BK);
+#pragma unroll
+          for (int i = 0; i < 8; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
+          // issue order: the 4 DMAs between the first MFMAs, then one fragment
+          // read per two MFMAs, then the remaining MFMAs
+#pragma unroll
+          for (int k = 0; k < LPC; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
+          }
+#pragma unroll
+          for (int k = 0; k < 12; ++k) {
+            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
+            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+          }
+          __builtin_amdgcn_sched_group_barrier(0x008, 32 - LPC - 24, 0);
+        } else {
+          issue(u, nch - 1);
+        }
+      }
+    }
   } else {
     // chunk c's fragments are read during chunk c-1's MFMAs.  Stage of chunk c
     // is refilled (chunk c+NB) right after iteration c's barrier: every wave
@@ -237,7 +288,8 @@ static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M
 
 // mode 0: y[M][N] = x . w^T (w [N][K], N % 256 == 0);
 // mode 1: y[M][N] = silu(x . w[0:N]^T) * (x . w[N:2N]^T) (w [2N][K], N % 128 == 0).
-// pipe: 0 plain loop, 1 fragment prefetch across the barrier (default).
+// pipe: 0 plain loop, 1 fragment prefetch across the barrier, 2 the same with two explicit
+// fragment sets and a forced read / MFMA interleave.
 // K % 32 == 0, ldx % 8 == 0, 16-byte aligned x / w; y row stride ldy >= N.
 K8S_API int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode,
                          int pipe, hipStream_t s) {
@@ -247,6 +299,11 @@ K8S_API int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy
       (mode == 1 && N % 128) || (mode != 0 && mode != 1) ||
       ((uintptr_t)x % 16) || ((uintptr_t)w % 16))
     return (int)hipErrorInvalidValue;
-  if (mode == 0) return pipe ? launch<0, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<0, 0>(x, ldx, w, y, ldy, M, N, K, s);
+  if (pipe < 0 || pipe > 2) return (int)hipErrorInvalidValue;
+  if (mode == 0) {
+    if (pipe == 2) return launch<0, 2>(x, ldx, w, y, ldy, M, N, K, s);
+    return pipe ? launch<0, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<0, 0>(x, ldx, w, y, ldy, M, N, K, s);
+  }
+  if (pipe == 2) return launch<1, 2>(x, ldx, w, y, ldy, M, N, K, s);
   return pipe ? launch<1, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<1, 0>(x, ldx, w, y, ldy, M, N, K, s);
 }

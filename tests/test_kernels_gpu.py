@@ -798,7 +798,7 @@ def test_sampling_top_p_and_tie_candidates_deterministic():
     assert bool((ids >= 16032).all()) and bool((ids[:, 1:] > ids[:, :-1]).all())  # valid, (v desc, id asc)
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 32), (100, 512, 96), (256, 1024, 4096), (300, 768, 256),
                                    (1000, 6144, 512), (2085, 4096, 1024), (4096, 256, 14336)])
 def test_gemm_big_vs_fp32(M, N, K, pipe):
@@ -826,7 +826,7 @@ def test_gemm_big_vs_fp32(M, N, K, pipe):
     assert torch.count_nonzero(yb[:, N:]) == 0
 
 
-@pytest.mark.parametrize("pipe", [0, 1])
+@pytest.mark.parametrize("pipe", [0, 1, 2])
 @pytest.mark.parametrize("M,I,K", [(5, 128, 64), (300, 384, 512), (1500, 1024, 4096)])
 def test_gemm_big_silu_epilogue(M, I, K, pipe):
     """SwiGLU epilogue of gemm_big (gate_up never written) == the unfused

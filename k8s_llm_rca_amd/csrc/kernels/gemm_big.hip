@@ -304,6 +304,8 @@ K8S_API int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy
     if (pipe == 2) return launch<0, 2>(x, ldx, w, y, ldy, M, N, K, s);
     return pipe ? launch<0, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<0, 0>(x, ldx, w, y, ldy, M, N, K, s);
   }
-  if (pipe == 2) return launch<1, 2>(x, ldx, w, y, ldy, M, N, K, s);
+  // the SwiGLU form of pipe 2 spills 24 VGPRs inside the loop (2 x 48 fragment
+  // registers + the gate/up epilogue): 978 vs 1204 TFLOP/s at M = 4096
+  // (profiles/r3/gemm_big/ab_v2_pipe2.jsonl) -- it runs the pipe-1 loop
   return pipe ? launch<1, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<1, 0>(x, ldx, w, y, ldy, M, N, K, s);
 }

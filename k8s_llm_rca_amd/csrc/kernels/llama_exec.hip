@@ -132,6 +132,15 @@ struct K8sLlamaStep {
   // ar_fuse: the all-reduce + residual add + RMSNorm of each row-parallel output in
   // one launch (k8s_ar_addnorm_bf16) instead of all-reduce, then rmsnorm
   int ar_id, ar_mode, ar_fuse;
+  // TP overlap of the row-parallel all-reduces with their GEMMs (eager steps,
+  // fused all-reduce + add + RMSNorm, hipBLASLt o / down only): the o and down
+  // GEMMs run in ar_chunks row blocks on the step stream and each block's
+  // k8s_ar_addnorm_bf16 (mode ar_mode_c) on a side stream as soon as the block's
+  // GEMM is done, so block c's all-reduce overlaps block c+1's GEMM.  Rows are
+  // independent in both ops (the norm is per row), so any row split is exact.
+  // ar_chunks <= 1: off.  ar_overlap_serial: the same chunked issue on the step
+  // stream alone (A/B and the bit-identity test).
+  int ar_chunks, ar_mode_c, ar_overlap_serial;
 };
 
 namespace {
@@ -185,6 +194,31 @@ struct Overlap {
   hipEvent_t fork = nullptr, join = nullptr;
 };
 
+// side stream + per-chunk events of the TP all-reduce overlap (calling thread's device)
+struct TpOverlap {
+  static constexpr int kMax = 8;
+  int dev = -1;
+  hipStream_t side = nullptr;
+  hipEvent_t done[kMax] = {}, join = nullptr;
+};
+
+bool tp_overlap_ready(TpOverlap& o) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess) return false;
+  if (o.dev == dev && o.side) return true;
+  if (hipStreamCreateWithFlags(&o.side, hipStreamNonBlocking) != hipSuccess) return false;
+  for (int i = 0; i < TpOverlap::kMax; ++i)
+    if (hipEventCreateWithFlags(&o.done[i], hipEventDisableTiming) != hipSuccess) return false;
+  if (hipEventCreateWithFlags(&o.join, hipEventDisableTiming) != hipSuccess) return false;
+  o.dev = dev;
+  return true;
+}
+
+TpOverlap& tp_overlap_state() {
+  static thread_local TpOverlap o;
+  return o;
+}
+
 Overlap& overlap_state() {
   static thread_local Overlap o;
   const char* v = std::getenv("K8SRCA_ATTN_OVERLAP");  // read per step: A/B-able in one process
@@ -217,6 +251,37 @@ bool overlap_ready(Overlap& o) {
     if (rc_) return rc_;       \
   } while (0)
 
+// Row-parallel projection out = x . w^T (hipBLASLt) + all-reduce + residual
+// add + RMSNorm (k8s_ar_addnorm_bf16 into y), in s.ar_chunks row blocks with
+// each block's all-reduce on the side stream behind its GEMM (see K8sLlamaStep).
+static long g_tp_chunked_calls = 0;  // chunked projections issued (tests check the path ran)
+
+static int tp_chunked_ar_norm(const K8sLlamaStep& s, TpOverlap& ov, const K8sGemmSel& g, const uint16_t* x, int ldx,
+                              const void* w, int K, uint16_t* out, const void* norm_w, hipStream_t st) {
+  const int T = s.T, H = s.H, nc = s.ar_chunks;
+  const bool par = !s.ar_overlap_serial;
+  hipStream_t side = par ? ov.side : st;
+  for (int c = 0; c < nc; ++c) {
+    const int r0 = (int)((long)T * c / nc), r1 = (int)((long)T * (c + 1) / nc);
+    if (r1 <= r0) continue;
+    const int rc = k8s_blaslt_gemm(x + (size_t)r0 * ldx, ldx, w, out + (size_t)r0 * H, H, r1 - r0, H, K, s.blaslt_ws,
+                                   s.blaslt_ws_bytes, st);
+    if (rc) return rc;
+    if (par) {
+      if (hipEventRecord(ov.done[c], st) != hipSuccess || hipStreamWaitEvent(side, ov.done[c], 0) != hipSuccess)
+        return (int)hipErrorUnknown;
+    }
+    const int ra = k8s_ar_addnorm_bf16(s.ar_id, out + (size_t)r0 * H, (uint16_t*)s.residual + (size_t)r0 * H, norm_w,
+                                       (uint16_t*)s.y + (size_t)r0 * H, r1 - r0, H, s.eps, s.ar_mode_c, side);
+    if (ra) return ra;
+  }
+  (void)g;
+  ++g_tp_chunked_calls;
+  if (par && (hipEventRecord(ov.join, side) != hipSuccess || hipStreamWaitEvent(st, ov.join, 0) != hipSuccess))
+    return (int)hipErrorUnknown;
+  return 0;
+}
+
 // Layers [0, L): on return `y` holds nothing useful and `prev` + `residual`
 // are the inputs of the final norm (exactly as after the Python loop).
 // Where the step's dispatch picked a split-K kernel for the o or down
@@ -236,9 +301,14 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   const long n_out = (long)T * H;
   Overlap& ov = overlap_state();
   hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  const bool capturing = !(hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone);
   // never inside a graph capture (decode-only steps are the captured ones anyway)
-  const bool ov_ok = ov.on && nd > 0 && nd < T && hipStreamIsCapturing(st, &cap) == hipSuccess &&
-                     cap == hipStreamCaptureStatusNone && overlap_ready(ov);
+  const bool ov_ok = ov.on && nd > 0 && nd < T && !capturing && overlap_ready(ov);
+  TpOverlap& tov = tp_overlap_state();
+  // chunked TP all-reduce overlap: eager steps, fused epilogue, library GEMMs for o and down
+  const bool tp_chunk = fuse_an && s.ar_chunks > 1 && s.ar_chunks <= TpOverlap::kMax && !capturing &&
+                        (s.ar_overlap_serial || tp_overlap_ready(tov));
+  const bool chunk_o = tp_chunk && s.sel[1].kind == 0, chunk_d = tp_chunk && s.sel[3].kind == 0;
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
@@ -277,8 +347,14 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                               s.d_items, s.d_n_items, s.d_n_items_dev,
                               conc ? (s.d_grid < ov.grid ? s.d_grid : ov.grid) : s.d_grid, st));
     if (conc) K8S_TRY((int)hipStreamWaitEvent(st, ov.join, 0));
-    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
-    if (fuse_an)
+    if (chunk_o) {
+      K8S_TRY(tp_chunked_ar_norm(s, tov, s.sel[1], attn, qd, s.wo[l], qd, (uint16_t*)s.obuf, s.post_norm[l], st));
+    } else {
+      K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
+    }
+    if (chunk_o) {
+      // all-reduce + residual add + post-attention norm done above, per row block
+    } else if (fuse_an)
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.obuf, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode, st));
     else if (tp)
       K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
@@ -299,6 +375,11 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     }
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
+    if (chunk_d && l + 1 < s.L) {  // the next layer's input norm rides on the chunked all-reduces
+      K8S_TRY(tp_chunked_ar_norm(s, tov, s.sel[3], (const uint16_t*)s.act, s.I, s.wdown[l], s.I, (uint16_t*)s.prev,
+                                 s.in_norm[l + 1], st));
+      continue;
+    }
     K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));
     if (fuse_an && l + 1 < s.L)  // the next layer's input norm rides on this all-reduce
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.prev, s.residual, s.in_norm[l + 1], s.y, T, H, s.eps, s.ar_mode, st));
@@ -309,3 +390,5 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
 }
 
 K8S_API int k8s_llama_step_size() { return (int)sizeof(K8sLlamaStep); }
+
+K8S_API long k8s_llama_tp_chunked_calls() { return g_tp_chunked_calls; }

@@ -43,6 +43,7 @@ class LlamaStep(ctypes.Structure):
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
         ("ar_id", I), ("ar_mode", I), ("ar_fuse", I),
+        ("ar_chunks", I), ("ar_mode_c", I), ("ar_overlap_serial", I),
     ]
 
 
@@ -51,6 +52,18 @@ _enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
 _fuse_ar_norm = os.environ.get("K8SRCA_TP_FUSED_NORM", "1") == "1"
 # split-K o / down projections reduced inside the following residual add + RMSNorm
 _fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
+# TP: eager steps of >= TP_OVERLAP_MIN_ROWS rows run the o / down GEMMs in
+# TP_OVERLAP_CHUNKS row blocks, each block's fused all-reduce + add + RMSNorm on
+# a side stream behind its GEMM (overlapping the next block's GEMM).
+# K8SRCA_TP_OVERLAP: 1 (default) on, 0 off, "serial" the same chunks on one stream.
+_tp_overlap = os.environ.get("K8SRCA_TP_OVERLAP", "1")
+TP_OVERLAP_CHUNKS = int(os.environ.get("K8SRCA_TP_OVERLAP_CHUNKS", "2"))
+TP_OVERLAP_MIN_ROWS = int(os.environ.get("K8SRCA_TP_OVERLAP_MIN_ROWS", "512"))
+
+
+def set_tp_overlap(mode: str) -> None:
+    global _tp_overlap
+    _tp_overlap = mode
 _checked = False
 
 
@@ -153,6 +166,10 @@ class LlamaExecutor:
             st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
             # the two-shot epilogue splits each row's 16-B chunks evenly over the ranks
             st.ar_fuse = int(_fuse_ar_norm and (st.ar_mode == 1 or (H // 8) % self._car.world == 0))
+            nc = TP_OVERLAP_CHUNKS if _tp_overlap != "0" and T >= TP_OVERLAP_MIN_ROWS else 1
+            st.ar_chunks = nc
+            st.ar_mode_c = 1 if (T + nc - 1) // nc * H * 2 <= ONE_SHOT_MAX else 2
+            st.ar_overlap_serial = int(_tp_overlap == "serial")
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)

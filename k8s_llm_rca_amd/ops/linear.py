@@ -363,7 +363,7 @@ def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
     return out
 
 
-BIG_PIPE = int(os.environ.get("K8SRCA_BIG_PIPE", "1"))
+BIG_PIPE = int(os.environ.get("K8SRCA_BIG_PIPE", "2"))
 # Prefill-size dispatch between gemm_big and hipBLASLt: per (N, K) the M ranges
 # where the hand-written kernel measured faster (data/gemm_big_<model>.json,
 # tools/big_gemm_ab.py --emit), separately for the SwiGLU-fused gate_up form

@@ -13,16 +13,37 @@
 
 namespace k8s {
 
-template <int MT, int U, int NW>
+// RoPE + paged KV-write epilogue of the qkv projection (the rope_kv_kernel of
+// norm_act.hip folded into the GEMM that produces its input): block b covers
+// head b / 8, dims d0 = 8 (b % 8) .. +8 and d0 + 64 .. +8, i.e. its 16 W rows are
+// the 8 (i, i + 64) rotation pairs of that head, so the block that finishes a
+// pair rotates it, stores it into qkv and (k / v heads) into the KV pages.
+// Same arithmetic as rope_kv_kernel on the bf16-rounded GEMM output:
+// bit-identical to skinny GEMM + rope_kv.
+struct SkinnyRope {
+  const int* pos;
+  const float* cos_sin;  // [max_pos][128]: cos[0..63] | sin[0..63]
+  const int* slots;      // [M] or null (no KV write)
+  uint16_t* kc;          // [blocks][nkv][BS][128]
+  uint16_t* vc;          // [blocks][nkv][128][BS]
+  int nq, nkv, BS;
+};
+
+__device__ __forceinline__ int rope_row(int n, int b) {  // W / output row of strip row n in block b
+  return (b >> 3) * 128 + (b & 7) * 8 + (n & 7) + (n >= 8 ? 64 : 0);
+}
+
+template <int MT, int U, int NW, bool ROPE>
 __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __restrict__ x, int ldx,
                                                               const uint16_t* __restrict__ w,
-                                                              uint16_t* __restrict__ y, int ldy, int M, int N, int K) {
+                                                              uint16_t* __restrict__ y, int ldy, int M, int N, int K,
+                                                              SkinnyRope rp) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, h = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int kq = K / NW;                 // K slice per wave (multiple of 32)
   const int kbeg = wv * kq;
-  const uint16_t* wrow = w + (size_t)(n0 + r) * K + kbeg + 8 * h;
+  const uint16_t* wrow = w + (size_t)(ROPE ? rope_row(r, blockIdx.x) : n0 + r) * K + kbeg + 8 * h;
   const uint16_t* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -79,6 +100,43 @@ __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __
 #pragma unroll
     for (int i = 0; i < 4; ++i) red[wv][4 * h + i][16 * mt + r] = acc[mt][i];
   __syncthreads();
+  if constexpr (ROPE) {
+    const int hd = blockIdx.x >> 3, d0 = (blockIdx.x & 7) * 8;
+    for (int e = threadIdx.x; e < 8 * 16 * MT; e += NW * 64) {
+      const int j = e & 7, m = e >> 3;
+      if (m >= M) continue;
+      float lo = 0.f, hi = 0.f;
+#pragma unroll
+      for (int q = 0; q < NW; ++q) {
+        lo += red[q][j][m];
+        hi += red[q][j + 8][m];
+      }
+      const int d = d0 + j;
+      uint16_t a = f2bf(lo), b = f2bf(hi);
+      if (hd < rp.nq + rp.nkv) {  // q / k head: rotate-half pair (d, d + 64)
+        const float* cs = rp.cos_sin + (size_t)rp.pos[m] * 128;
+        const float co = cs[d], si = cs[64 + d], fa = bf2f(a), fb = bf2f(b);
+        a = f2bf(fa * co - fb * si);
+        b = f2bf(fb * co + fa * si);
+      }
+      uint16_t* yr = y + (size_t)m * ldy + hd * 128;
+      yr[d] = a;
+      yr[d + 64] = b;
+      const int slot = rp.slots ? rp.slots[m] : -1;
+      if (slot < 0 || hd < rp.nq) continue;
+      const int blk = slot / rp.BS, off = slot % rp.BS;
+      if (hd < rp.nq + rp.nkv) {
+        uint16_t* kp = rp.kc + (((size_t)blk * rp.nkv + (hd - rp.nq)) * rp.BS + off) * 128;
+        kp[d] = a;
+        kp[d + 64] = b;
+      } else {
+        uint16_t* vp = rp.vc + ((size_t)blk * rp.nkv + (hd - rp.nq - rp.nkv)) * 128 * rp.BS + off;
+        vp[(size_t)d * rp.BS] = a;
+        vp[(size_t)(d + 64) * rp.BS] = b;
+      }
+    }
+    return;
+  }
   for (int e = threadIdx.x; e < 16 * 16 * MT; e += NW * 64) {
     const int n = e & 15, m = e >> 4;
     if (m < M) {
@@ -101,13 +159,28 @@ K8S_API int k8s_gemm_skinny(const void* x, int ldx, const void* w, void* y, int 
   const uint16_t* ww = (const uint16_t*)w;
   uint16_t* yy = (uint16_t*)y;
   dim3 g(N / 16);
+  const SkinnyRope rp{};
   if (M <= 16)
-    hipLaunchKernelGGL((gemm_skinny_kernel<1, 4, 8>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K);
+    hipLaunchKernelGGL((gemm_skinny_kernel<1, 4, 8, false>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K, rp);
   else if (M <= 32)
-    hipLaunchKernelGGL((gemm_skinny_kernel<2, 4, 8>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K);
+    hipLaunchKernelGGL((gemm_skinny_kernel<2, 4, 8, false>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K, rp);
   else if (M <= 64)
-    hipLaunchKernelGGL((gemm_skinny_kernel<4, 2, 8>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K);
+    hipLaunchKernelGGL((gemm_skinny_kernel<4, 2, 8, false>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K, rp);
   else
-    hipLaunchKernelGGL((gemm_skinny_kernel<8, 1, 8>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K);
+    hipLaunchKernelGGL((gemm_skinny_kernel<8, 1, 8, false>), g, dim3(512), 0, s, xx, ldx, ww, yy, ldy, M, N, K, rp);
+  return (int)hipGetLastError();
+}
+
+// qkv = x . w^T (w = [q heads; k heads; v heads] x 128 rows, N = (nq + 2 nkv) 128)
+// with the RoPE + paged KV write of k8s_rope_kv fused into the epilogue
+// (M <= 16; bit-identical to k8s_gemm_skinny + k8s_rope_kv).
+K8S_API int k8s_gemm_skinny_rope(const void* x, int ldx, const void* w, void* qkv, int ldq, int M, int N, int K,
+                                 const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc, int nq,
+                                 int nkv, int BS, hipStream_t s) {
+  if (M <= 0 || M > 16 || K % 256 || N != (nq + 2 * nkv) * 128 || ldq < N || !pos || !cos_sin || BS <= 0)
+    return (int)hipErrorInvalidValue;
+  const SkinnyRope rp{pos, cos_sin, slots, (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS};
+  hipLaunchKernelGGL((gemm_skinny_kernel<1, 4, 8, true>), dim3(N / 16), dim3(512), 0, s, (const uint16_t*)x, ldx,
+                     (const uint16_t*)w, (uint16_t*)qkv, ldq, M, N, K, rp);
   return (int)hipGetLastError();
 }

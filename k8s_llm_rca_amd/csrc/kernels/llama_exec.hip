@@ -46,6 +46,9 @@ int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc
                      const int* m_np, int n_merge, float* pf_o, float* pf_ml, int nq, int nkv, int BS, float scale,
                      void* out, int out_stride, hipStream_t stream);
 int k8s_gemm_skinny(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, hipStream_t s);
+int k8s_gemm_skinny_rope(const void* x, int ldx, const void* w, void* qkv, int ldq, int M, int N, int K,
+                         const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc, int nq, int nkv,
+                         int BS, hipStream_t s);
 int k8s_gemm_mid(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg, int splits,
                  void* part, hipStream_t s);
 int k8s_gemm_mid_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
@@ -73,7 +76,8 @@ int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy
 // 4 gemm_stream (cfg = ring depth, splits), 5 gemm_big (cfg = pipe);
 // fuse: 1 -- a split-K o / down projection may leave its partials to the next norm;
 // 2 (gate_up, kinds 4 / 5 with one K split) -- the SwiGLU-epilogue form, which
-// writes act directly (gu is never written, no silu_mul launch)
+// writes act directly (gu is never written, no silu_mul launch);
+// 3 (qkv, kind 1) -- the skinny kernel's RoPE / KV-write epilogue (no rope_kv launch)
 struct K8sGemmSel {
   int kind, cfg, splits, fuse;
 };
@@ -325,6 +329,9 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st, true));
       K8S_TRY(k8s_splitk_rope_kv(part_of(s, s.sel[0]), s.sel[0].splits, qkv, ld_qkv, s.pos, s.cos_sin, s.slots,
                                  s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    } else if (s.sel[0].kind == 1 && s.sel[0].fuse == 3) {  // skinny qkv with the RoPE / KV-write epilogue
+      K8S_TRY(k8s_gemm_skinny_rope(s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, s.pos, s.cos_sin, s.slots, s.kc[l],
+                                   s.vc[l], s.nq, s.nkv, s.BS, st));
     } else {
       K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st));
       K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));

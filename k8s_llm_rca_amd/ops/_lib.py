@@ -33,6 +33,7 @@ _SIGS = {
     "k8s_attn_prefill": [P, I, P, P, P, I, P, P, P, P, P, P, P, P, I, P, P, P, P, I, P, P, I, I, I, F, P, I, P],
     "k8s_sample": [P, I, I, I, I, P, P, P, P, P, I, P, P, P, P, P, P, I, P, P, P, I],
     "k8s_gemm_skinny": [P, I, P, P, I, I, I, I, P],
+    "k8s_gemm_skinny_rope": [P, I, P, P, I, I, I, I, P, P, P, P, P, I, I, I, P],
     "k8s_gemm_mid": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_mid_part": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_stream": [P, I, P, P, I, I, I, I, I, I, P, P],

@@ -86,6 +86,15 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
 _fuse_qkv = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
 
 
+# RoPE / KV-write epilogue on the skinny qkv GEMM (decode at M <= 16 where the
+# dispatch picks the skinny kernel): one launch instead of GEMM + rope_kv.
+_skinny_rope = os.environ.get("K8SRCA_SKINNY_ROPE", "1") == "1"
+
+
+def skinny_rope_ok(M: int, N: int, K: int, nq: int, nkv: int) -> bool:
+    return _skinny_rope and 0 < M <= 16 and K % 256 == 0 and N == (nq + 2 * nkv) * HEAD_DIM
+
+
 def linear_rope_kv(y: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
                    slots: Optional[torch.Tensor], k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int,
                    nkv: int) -> torch.Tensor:
@@ -100,6 +109,13 @@ def linear_rope_kv(y: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, co
     if _fuse_qkv and use_hip(y) and y.dtype == torch.bfloat16 and slots is not None:
         layout = y.stride(1) == 1 and y.stride(0) % 8 == 0 and w.is_contiguous()
         kind, cfg, splits = LIN.select_gemm(M, N, K, layout, True)
+        if kind == LIN.KIND_SKINNY and layout and skinny_rope_ok(M, N, K, nq, nkv):
+            qkv = torch.empty((M, N), dtype=y.dtype, device=y.device)
+            BS = k_cache.shape[2]
+            check(lib().k8s_gemm_skinny_rope(ptr(y), y.stride(0), ptr(w), ptr(qkv), N, M, N, K, ptr(positions),
+                                             ptr(cos_sin), ptr(slots), ptr(k_cache), ptr(v_cache), nq, nkv, BS,
+                                             stream_ptr(y)), "gemm_skinny_rope")
+            return qkv
         if kind in (LIN.KIND_STREAM, LIN.KIND_MID) and splits > 1:
             qkv = torch.empty((M, N), dtype=y.dtype, device=y.device)
             part = LIN._scratch(y.device, splits * M * N)

@@ -206,6 +206,8 @@ class LlamaExecutor:
             kind, cfg, splits = fused or LIN.select_gemm(T, N, K)
             st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
             st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
+            if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):
+                st.sel[i].fuse = 3  # RoPE + KV write in the qkv GEMM's epilogue
             if kind in (LIN.KIND_MID, LIN.KIND_STREAM) and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:

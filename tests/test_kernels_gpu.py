@@ -860,3 +860,39 @@ def test_gemm_stream_silu_epilogue(M, cfg):
     assert torch.equal(act, N.silu_mul(LIN.gemm_stream(x, w, cfg, 1)))
     g, u = (x.float() @ w.float().t()).split(I, dim=1)
     torch.testing.assert_close(act.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 7, 16])
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1)])
+def test_gemm_skinny_rope_epilogue_bit_identical(M, nq, nkv):
+    """The skinny qkv GEMM with the RoPE + paged KV-write epilogue
+    (k8s_gemm_skinny_rope: a block owns the 8 (i, i+64) pairs of one head) ==
+    skinny GEMM + rope_kv bit for bit: qkv, K pages and V pages (a slot -1 row
+    writes no KV)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    K, BS, NB = 1024, 64, 8
+    N = (nq + 2 * nkv) * 128
+    torch.manual_seed(M + nq)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+    cs = A.rope_cos_sin(4096, 500000.0, device=dev)
+    pos = torch.randint(0, 4000, (M,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=dev)[:M].int()
+    if M > 1:
+        slots[1] = -1
+    kc, vc = torch.zeros(NB, nkv, BS, 128, device=dev).bfloat16(), torch.zeros(NB, nkv, 128, BS, device=dev).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    ref = torch.empty(M, N, device=dev).bfloat16()
+    assert lib().k8s_gemm_skinny(ptr(x), K, ptr(w), ptr(ref), N, M, N, K, stream_ptr(x)) == 0
+    A.rope_kv_write(ref, pos, cs, slots, kc, vc, nq, nkv)
+    out = torch.empty(M, N, device=dev).bfloat16()
+    assert lib().k8s_gemm_skinny_rope(ptr(x), K, ptr(w), ptr(out), N, M, N, K, ptr(pos), ptr(cs), ptr(slots),
+                                      ptr(kc2), ptr(vc2), nq, nkv, BS, stream_ptr(x)) == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
+    # and against fp32 (GEMM then the PyTorch RoPE reference)
+    r32 = (x.float() @ w.float().t()).bfloat16().cpu()
+    kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
+    A.rope_kv_write(r32, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, nq, nkv)
+    torch.testing.assert_close(out.cpu().float(), r32.float(), atol=3e-2, rtol=3e-2)

@@ -8,7 +8,7 @@ time is (t_gen - t_prefill) / (N - 1).  Variants are interleaved round by
 round in one process (cdna_hip_programming.md §5.4 rule 24).
 
 usage: python tools/decode_latency.py [--batch 1] [--ctx 5000] [--tokens 200] [--rounds 3]
-           [--variants base,silu,c1fuse]
+           [--variants base,silu,full]
 """
 import argparse
 import json
@@ -28,8 +28,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def apply(variant):
-    """Module-level switches the engine's kernels read per call (the dispatch table is global)."""
+    """Module-level switches the engine's kernels read per call (the dispatch table is global).
+    base: no decode epilogue fusions; silu: the stream kernels' SwiGLU epilogue;
+    full: + the skinny qkv GEMM's RoPE / KV-write epilogue; c1fuse: silu + the
+    split-K variant dispatch table."""
+    from k8s_llm_rca_amd.ops import attention as A
     LIN._stream_silu = variant != "base"
+    A._skinny_rope = variant == "full"
     if variant == "c1fuse":
         LIN.load_dispatch(os.path.join(ROOT, "tools", "dispatch_c1fuse.json"))
     else:
@@ -53,7 +58,7 @@ def main():
     ap.add_argument("--ctx", type=int, default=5000)
     ap.add_argument("--tokens", type=int, default=200)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--variants", default="base,silu,c1fuse")
+    ap.add_argument("--variants", default="base,silu,full")
     a = ap.parse_args()
     variants = a.variants.split(",")
     g = torch.Generator().manual_seed(0)

@@ -310,101 +310,6 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
 }
 
-// Decoupled rings: W (streamed once from HBM) and X (re-read by every strip:
-// L2-resident) in SEPARATE LDS rings, NBW deep for W and NBX deep for X.  The
-// joint ring above keeps as many X bytes in flight as W bytes, so at M ~ 100-250
-// half of a workgroup's in-flight window is L2 traffic and the HBM stream sees
-// only NB-2 W chunks (~2.8 TB/s for gate_up at M = 128,
-// profiles/r2_gemm_sweep_8b_stream.txt).  Here W runs NBW-1 chunks ahead and X
-// only NBX-1.  Issue order per chunk step: W(c + NBW - 1), then X(c + NBX - 1);
-// the prologue issues the extra-deep W chunks first and then (W, X) pairs, so
-// at the top of step c exactly the (NBX - 2) later pairs were issued after X(c)
-// (and W(c) before it): one counted vmcnt covers both rings.
-template <int MTW, int NBW, int NBX, int NF>
-constexpr int glds2_lds_elems() {
-  return NBW * 16 * NF * kSC + NBX * 64 * MTW * kSC;
-}
-
-template <int MTW, int NBW, int NBX, int NF>
-__device__ __forceinline__ void glds_strip2(const uint16_t* __restrict__ x, int ldx, int M,
-                                            const uint16_t* __restrict__ wstrip, int K, int nch, uint16_t* sm,
-                                            f32x4 (&acc)[MTW][NF], int silu_i) {
-  static_assert(NBW > NBX && NBX >= 2, "W ring deeper than the X ring");
-  constexpr int MP = 64 * MTW;
-  constexpr int WST = 16 * NF * kSC, XST = MP * kSC;
-  constexpr int XPT = MP * 8 / 256, WPT = NF / 2;
-  constexpr int LPC = WPT + XPT;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int r = lane & 15, g = lane >> 4;
-  const int m_base = wv * 16 * MTW;
-  uint16_t* xring = sm + NBW * WST;
-
-  const uint16_t* wsrc[WPT];
-#pragma unroll
-  for (int i = 0; i < WPT; ++i) {
-    const int p = 256 * i + tid, n = p >> 3, jl = p & 7;
-    wsrc[i] = wstrip + (size_t)strip_row<NF>(n, silu_i) * K + 8 * (jl ^ (n & 7));
-  }
-  const uint16_t* xsrc[XPT];
-#pragma unroll
-  for (int i = 0; i < XPT; ++i) {
-    const int p = 256 * i + tid, m = p >> 3, jl = p & 7;
-    xsrc[i] = x + (size_t)min(m, M - 1) * ldx + 8 * (jl ^ (m & 7));
-  }
-  auto issue_w = [&](int stage, int c) {
-#pragma unroll
-    for (int i = 0; i < WPT; ++i) glds16_w(wsrc[i] + c * kSC, sm + stage * WST + (256 * i + 64 * wv) * 8);
-  };
-  auto issue_x = [&](int stage, int c) {
-#pragma unroll
-    for (int i = 0; i < XPT; ++i) glds16(xsrc[i] + c * kSC, xring + stage * XST + (256 * i + 64 * wv) * 8);
-  };
-  auto compute = [&](int ws_i, int xs_i) {
-    const uint16_t* ws = sm + ws_i * WST;
-    const uint16_t* xs = xring + xs_i * XST;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      bf16x8 xf[MTW];
-#pragma unroll
-      for (int mt = 0; mt < MTW; ++mt) {
-        const int m = m_base + 16 * mt + r;
-        xf[mt] = *reinterpret_cast<const bf16x8*>(xs + m * kSC + 8 * ((4 * s + g) ^ (m & 7)));
-      }
-#pragma unroll
-      for (int cf = 0; cf < NF; ++cf) {
-        const int n = 16 * cf + r;
-        const bf16x8 wf = *reinterpret_cast<const bf16x8*>(ws + n * kSC + 8 * ((4 * s + g) ^ (n & 7)));
-#pragma unroll
-        for (int mt = 0; mt < MTW; ++mt)
-          acc[mt][cf] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[mt], wf, acc[mt][cf], 0, 0, 0);
-      }
-    }
-  };
-
-  // prologue: W chunks 0 .. NBW-NBX-1, then (W, X) pairs up to W NBW-2 / X NBX-2
-#pragma unroll
-  for (int c = 0; c < NBW - NBX; ++c) issue_w(c, min(c, nch - 1));
-#pragma unroll
-  for (int j = 0; j < NBX - 1; ++j) {
-    issue_w(NBW - NBX + j, min(NBW - NBX + j, nch - 1));
-    issue_x(j, min(j, nch - 1));
-  }
-  // ring slots advance by one per chunk (runtime slot indices: only LDS base
-  // addresses depend on them; unrolling by lcm(NBW, NBX) up to 30 bodies bloated the code)
-  int wsl = 0, xsl = 0;
-  for (int c = 0; c < nch; ++c) {
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NBX - 2) * LPC) : "memory");  // W(c), X(c) landed (this wave's)
-    __builtin_amdgcn_s_barrier();  // every wave's chunk c landed; every wave done reading chunk c-1
-    issue_w(wsl == 0 ? NBW - 1 : wsl - 1, min(c + NBW - 1, nch - 1));  // chunk c-1's slots
-    issue_x(xsl == 0 ? NBX - 1 : xsl - 1, min(c + NBX - 1, nch - 1));
-    compute(wsl, xsl);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    wsl = wsl == NBW - 1 ? 0 : wsl + 1;
-    xsl = xsl == NBX - 1 ? 0 : xsl + 1;
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
-}
-
 // acc[mt][cf][v] = C[m_base + 16 mt + 4 g + v][16 cf + r] of the tile: bf16 rows
 // of y (final) or fp32 rows of `part` (split-K partial), rows < M only.
 template <int MTW, int NF = 4>
@@ -460,27 +365,6 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
 #pragma unroll
     for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
   glds_strip<MTW, NB, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
-  if (silu_i)
-    glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0, true);
-  else if (gridDim.y == 1)
-    glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0);
-  else
-    glds_store<MTW, NF>(acc, M, nullptr, 0, part + (size_t)split * M * N + n0, N);
-}
-
-template <int MTW, int NBW, int NBX, int NF>
-__global__ void __launch_bounds__(256) gemm_glds2_kernel(const uint16_t* __restrict__ x, int ldx,
-                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                         int ldy, float* __restrict__ part, int M, int N, int K,
-                                                         int kslice, int silu_i) {
-  __shared__ __attribute__((aligned(16))) uint16_t sm[glds2_lds_elems<MTW, NBW, NBX, NF>()];
-  const int n0 = blockIdx.x * (silu_i ? 8 : 16) * NF, split = blockIdx.y, kbeg = split * kslice;
-  f32x4 acc[MTW][NF];
-#pragma unroll
-  for (int mt = 0; mt < MTW; ++mt)
-#pragma unroll
-    for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  glds_strip2<MTW, NBW, NBX, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
   if (silu_i)
     glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0, true);
   else if (gridDim.y == 1)
@@ -555,14 +439,6 @@ static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int l
   return hipGetLastError();
 }
 
-template <int MTW, int NBW, int NBX, int NF>
-static hipError_t launch_glds2(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
-                               int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
-  hipLaunchKernelGGL((gemm_glds2_kernel<MTW, NBW, NBX, NF>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K,
-                     kslice, silu_i);
-  return hipGetLastError();
-}
-
 template <int MTW, int U>
 static hipError_t launch_stream(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
                                 int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
@@ -583,10 +459,9 @@ using namespace k8s;
 // (splits == 1 only: the nonlinearity needs the whole K sum).
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          int splits, void* part, bool reduce, hipStream_t s, bool silu = false) {
-  const int bn = (cfg > 20 && cfg != 32 ? 128 : kSBN) / (silu ? 2 : 1);  // output columns per strip
+  const int bn = (cfg > 20 ? 128 : kSBN) / (silu ? 2 : 1);  // output columns per strip
   if (M <= 0 || M > 256 || N % bn || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
-      (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24 && cfg != 32 && cfg != 33) ||
-      ldx % 8 ||
+      (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24) || ldx % 8 ||
       (splits > 1 && (M * N) % 8) || ((splits == 1 || reduce) && ldy < N) || (silu && splits != 1))
     return (int)hipErrorInvalidValue;
   const int silu_i = silu ? N : 0;
@@ -607,22 +482,7 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
 #define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
 #define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
 #define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
-#define K8S_G2(MT, NBW, NF) e = launch_glds2<MT, NBW, 3, NF>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
-  if (cfg == 33) {  // decoupled W / X rings, 128-column strips (W ring as deep as the LDS allows)
-    switch (mtw) {
-      case 1: K8S_G2(1, 8, 8); break;
-      case 2: K8S_G2(2, 6, 8); break;
-      case 3: K8S_G2(3, 5, 8); break;
-      default: K8S_G2(4, 4, 8); break;
-    }
-  } else if (cfg == 32) {  // decoupled rings, 64-column strips
-    switch (mtw) {
-      case 1: K8S_G2(1, 12, 4); break;
-      case 2: K8S_G2(2, 10, 4); break;
-      case 3: K8S_G2(3, 8, 4); break;
-      default: K8S_G2(4, 6, 4); break;
-    }
-  } else if (cfg == 23) {
+  if (cfg == 23) {
     switch (mtw) {
       case 1: K8S_GW(1, 3); break;
       case 2: K8S_GW(2, 3); break;
@@ -669,7 +529,6 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
 #undef K8S_SL
 #undef K8S_GL
 #undef K8S_GW
-#undef K8S_G2
   if (e != hipSuccess) return (int)e;
   if (splits > 1 && reduce) {
     const int blocks = (M * N / 8 + 255) / 256;

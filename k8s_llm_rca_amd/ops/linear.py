@@ -493,10 +493,9 @@ def stream_shape_ok(M: int, N: int, K: int, cfg: int, splits: int) -> bool:
     # cfg 13..16: the LDS-DMA kernel with 3..6 stages (any chunk count); 23 / 24:
     # the same on 128-column strips with 3 / 4 stages; 4 / 8: the register ring,
     # whose loop has no partial trip
-    # 32 / 33: decoupled W / X LDS rings on 64- / 128-column strips (any M <= 256)
     ok_cfg = (cfg == 4 or (cfg == 8 and M <= 128) or cfg == 13 or (cfg == 14 and M <= 192)
-              or (cfg in (15, 16) and M <= 64) or cfg == 23 or (cfg == 24 and M <= 192) or cfg in (32, 33))
-    bn = 128 if cfg > 20 and cfg != 32 else 64
+              or (cfg in (15, 16) and M <= 64) or cfg == 23 or (cfg == 24 and M <= 192))
+    bn = 128 if cfg > 20 else 64
     return (ok_cfg and 0 < M <= 256 and N % bn == 0 and splits >= 1 and K % (64 * splits) == 0
             and (cfg > 10 or (K // splits // 64) % cfg == 0))
 
@@ -506,11 +505,11 @@ def stream_candidates(M: int, N: int, K: int):
     out = []
     if not (0 < M <= 256 and N % 64 == 0):
         return out
-    for cfg in (4, 8, 13, 14, 15, 16, 23, 24, 32, 33):
+    for cfg in (4, 8, 13, 14, 15, 16, 23, 24):
         for s in (1, 2, 4, 7, 8, 14, 16):
             if not stream_shape_ok(M, N, K, cfg, s):
                 continue
-            if 128 <= (N // (128 if cfg > 20 and cfg != 32 else 64)) * s <= 2048:
+            if 128 <= (N // (128 if cfg > 20 else 64)) * s <= 2048:
                 out.append((cfg, s))
     return out
 

@@ -696,7 +696,7 @@ def test_blaslt_bucket_registration(monkeypatch):
 
 @pytest.mark.parametrize("M", [1, 17, 64, 96, 128, 200, 256])
 @pytest.mark.parametrize("N,K,splits", [(4096, 4096, 8), (6144, 4096, 4), (512, 14336, 7), (1280, 8192, 1)])
-@pytest.mark.parametrize("cfg", [4, 8, 13, 14, 16, 23, 24, 32, 33])
+@pytest.mark.parametrize("cfg", [4, 8, 13, 14, 16, 23, 24])
 def test_gemm_stream_vs_fp32(M, N, K, splits, cfg):
     """W-shared decode GEMM (csrc/kernels/gemm_stream.hip) vs fp32, incl. an
     asymmetric exact check (identity rows pick weight columns)."""
@@ -844,7 +844,7 @@ def test_gemm_big_silu_epilogue(M, I, K, pipe):
 
 
 @pytest.mark.parametrize("M", [1, 17, 48, 128, 200])
-@pytest.mark.parametrize("cfg", [4, 8, 13, 14, 23, 24, 32, 33])
+@pytest.mark.parametrize("cfg", [4, 8, 13, 14, 23, 24])
 def test_gemm_stream_silu_epilogue(M, cfg):
     """SwiGLU epilogue of the decode stream kernels (gate and up rows of one act
     column in one strip) == gemm_stream + silu_mul bit for bit, and fp32."""

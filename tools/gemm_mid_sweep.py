@@ -66,6 +66,7 @@ def main():
     from k8s_llm_rca_amd.models.config import get_config
     mc = get_config(a.model)
     down = (mc.hidden, mc.intermediate // a.tp) if not mc.n_experts else None
+    gate_up = (2 * mc.intermediate // a.tp, mc.hidden) if not mc.n_experts else None
     tot, lm, layer_gb = {}, {}, {}
     t0 = time.time()
     for M in ms:
@@ -131,6 +132,30 @@ def main():
                 best_t_layer = min(base, fc[0][0] if fc else base)
                 tot.setdefault(M, [0.0, 0.0])
                 tot[M][1] += best_t_layer - best["t_us"]  # count the down projection as its fused cost
+            if (N, K) == gate_up and M <= L.DISPATCH_MAX_M:
+                # the SwiGLU epilogue of the stream kernels (one K split) writes act directly:
+                # compare it with the plain pick + silu_mul (what the engine runs otherwise)
+                from k8s_llm_rca_amd.ops.norm import silu_mul
+                gu = torch.randn(M, N, dtype=torch.bfloat16, device=dev)
+                base = bench(lambda: silu_mul(gu)) + best["t_us"]
+                g_ref, u_ref = ref.split(N // 2, dim=1)
+                ref3 = torch.nn.functional.silu(g_ref) * u_ref
+                fc = []
+                for cfg, sp in L.stream_candidates(M, N, K):
+                    if sp != 1:
+                        continue
+                    fn = lambda xx, ww, cfg=cfg: L.gemm_stream_silu(xx, ww, cfg)
+                    err = (fn(x, w).float() - ref3).abs().max().item() / (ref3.abs().max().item() + 1e-6)
+                    if err > 3e-2:
+                        print(f"  !! stream-silu {cfg} M{M} rel err {err:.3e}", flush=True)
+                        continue
+                    fc.append((bench(lambda: fn(x, rot(wl))), cfg))
+                fc.sort()
+                if fc and fc[0][0] < a.margin * base:
+                    best.update(kind="stream", cfg=fc[0][1], splits=1, t_us=round(fc[0][0], 2), swiglu_epilogue=True)
+                print(f"      gate_up+silu: {best.get('kind')} {base:7.1f}us unfused, stream-silu best "
+                      + (f"cfg {fc[0][1]} {fc[0][0]:.1f}us" if fc else "-")
+                      + (" -> fused" if best.get("swiglu_epilogue") else " -> unfused"), flush=True)
             line = "  ".join(f"{k} {v:7.1f}us {gb / (v * 1e-6) / 1e3:5.2f}TB/s" for k, v in res.items())
             top = " | ".join(f"{n} {t:.1f}" for t, n in cands[:3])
             print(f"M{M:4d} N{N:6d} K{K:6d}  {line}   [{top}] -> {best['kind']}", flush=True)

@@ -1,5 +1,7 @@
 // Memory-bound fused elementwise kernels (B2 RMSNorm, B8 SwiGLU, B3+B5 RoPE/KV write).
 // All loads/stores are 16-byte vectors (8 bf16); math in fp32.
+#include <algorithm>
+
 #include "common.h"
 
 namespace k8s {
@@ -207,6 +209,39 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv
 }  // namespace k8s
 
 using namespace k8s;
+
+// ------------------------------------------------ graph-step input unpack
+// One launch instead of seven D2D copies (each a runtime blit kernel, ~4.5 us
+// and ~10 us of host time) before every HIP-graph decode step: the step's flat
+// int32 upload [ids | pos | slots | ctx | block table (Bb x mb) | n_items, part |
+// items (n_items x 4)] is scattered into the graph's static input buffers.
+__global__ void __launch_bounds__(256) unpack_step_kernel(const int* __restrict__ flat, int Bb, int mb, int n_items,
+                                                          int* __restrict__ ids, int* __restrict__ pos,
+                                                          int* __restrict__ slots, int* __restrict__ ctx,
+                                                          int* __restrict__ bt, int* __restrict__ n_items_buf,
+                                                          int* __restrict__ items) {
+  const int head = 4 * Bb + Bb * mb, total = head + 2 + 4 * n_items;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int v = flat[i];
+    if (i < Bb) ids[i] = v;
+    else if (i < 2 * Bb) pos[i - Bb] = v;
+    else if (i < 3 * Bb) slots[i - 2 * Bb] = v;
+    else if (i < 4 * Bb) ctx[i - 3 * Bb] = v;
+    else if (i < head) bt[i - 4 * Bb] = v;
+    else if (i < head + 2) n_items_buf[i - head] = v;
+    else items[i - head - 2] = v;
+  }
+}
+
+K8S_API int k8s_unpack_step(const void* flat, int Bb, int mb, int n_items, void* ids, void* pos, void* slots,
+                            void* ctx, void* bt, void* n_items_buf, void* items, hipStream_t s) {
+  if (Bb <= 0 || mb <= 0 || n_items < 0) return (int)hipErrorInvalidValue;
+  const int total = 4 * Bb + Bb * mb + 2 + 4 * n_items;
+  const int grid = std::min((total + 255) / 256, 256);
+  hipLaunchKernelGGL(unpack_step_kernel, dim3(grid), dim3(256), 0, s, (const int*)flat, Bb, mb, n_items, (int*)ids,
+                     (int*)pos, (int*)slots, (int*)ctx, (int*)bt, (int*)n_items_buf, (int*)items);
+  return (int)hipGetLastError();
+}
 
 K8S_API int k8s_rmsnorm(const void* x, void* res, const void* w, void* y, int T, int H, int x_stride, int y_stride,
                         float eps, hipStream_t s) {

@@ -1379,13 +1379,12 @@ class LLMEngine:
         dev_flat.copy_(host[:n], non_blocking=True)
         ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event()
         ev.record()
-        st["ids"][:Bb].copy_(dev_flat[0:Bb])
-        st["pos"][:Bb].copy_(dev_flat[Bb:2 * Bb])
-        st["slots"][:Bb].copy_(dev_flat[2 * Bb:3 * Bb])
-        st["ctx"][:Bb].copy_(dev_flat[3 * Bb:4 * Bb])
-        st["bt"][:Bb].copy_(dev_flat[4 * Bb:4 * Bb + Bb * mb].view(Bb, mb))
-        st["n_items"].copy_(dev_flat[o:o + 2])
-        st["items"][:n_items].copy_(dev_flat[o + 2:o + 2 + n_items * 4].view(n_items, 4))
+        # the upload scattered into the graph's static inputs in one launch (csrc/kernels/norm_act.hip)
+        from ..ops._lib import check, lib, stream_ptr
+        check(lib().k8s_unpack_step(dev_flat.data_ptr(), Bb, mb, n_items, st["ids"].data_ptr(), st["pos"].data_ptr(),
+                                    st["slots"].data_ptr(), st["ctx"].data_ptr(), st["bt"].data_ptr(),
+                                    st["n_items"].data_ptr(), st["items"].data_ptr(), stream_ptr(dev_flat)),
+              "unpack_step")
         if spec is not None:  # before a capture too: its warm-up forwards read these ids
             self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], _spec_tok(spec))
         graph, out = self._capture(Bb, part)  # one graph per bucket: the plan's part size is read on the device

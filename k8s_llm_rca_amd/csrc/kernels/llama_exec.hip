@@ -260,8 +260,8 @@ bool overlap_ready(Overlap& o) {
 // each block's all-reduce on the side stream behind its GEMM (see K8sLlamaStep).
 static long g_tp_chunked_calls = 0;  // chunked projections issued (tests check the path ran)
 
-static int tp_chunked_ar_norm(const K8sLlamaStep& s, TpOverlap& ov, const K8sGemmSel& g, const uint16_t* x, int ldx,
-                              const void* w, int K, uint16_t* out, const void* norm_w, hipStream_t st) {
+static int tp_chunked_ar_norm(const K8sLlamaStep& s, TpOverlap& ov, const uint16_t* x, int ldx, const void* w, int K,
+                              uint16_t* out, const void* norm_w, hipStream_t st) {
   const int T = s.T, H = s.H, nc = s.ar_chunks;
   const bool par = !s.ar_overlap_serial;
   hipStream_t side = par ? ov.side : st;
@@ -279,7 +279,6 @@ static int tp_chunked_ar_norm(const K8sLlamaStep& s, TpOverlap& ov, const K8sGem
                                        (uint16_t*)s.y + (size_t)r0 * H, r1 - r0, H, s.eps, s.ar_mode_c, side);
     if (ra) return ra;
   }
-  (void)g;
   ++g_tp_chunked_calls;
   if (par && (hipEventRecord(ov.join, side) != hipSuccess || hipStreamWaitEvent(st, ov.join, 0) != hipSuccess))
     return (int)hipErrorUnknown;
@@ -355,7 +354,7 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                               conc ? (s.d_grid < ov.grid ? s.d_grid : ov.grid) : s.d_grid, st));
     if (conc) K8S_TRY((int)hipStreamWaitEvent(st, ov.join, 0));
     if (chunk_o) {
-      K8S_TRY(tp_chunked_ar_norm(s, tov, s.sel[1], attn, qd, s.wo[l], qd, (uint16_t*)s.obuf, s.post_norm[l], st));
+      K8S_TRY(tp_chunked_ar_norm(s, tov, attn, qd, s.wo[l], qd, (uint16_t*)s.obuf, s.post_norm[l], st));
     } else {
       K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
     }
@@ -383,7 +382,7 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
     if (chunk_d && l + 1 < s.L) {  // the next layer's input norm rides on the chunked all-reduces
-      K8S_TRY(tp_chunked_ar_norm(s, tov, s.sel[3], (const uint16_t*)s.act, s.I, s.wdown[l], s.I, (uint16_t*)s.prev,
+      K8S_TRY(tp_chunked_ar_norm(s, tov, (const uint16_t*)s.act, s.I, s.wdown[l], s.I, (uint16_t*)s.prev,
                                  s.in_norm[l + 1], st));
       continue;
     }

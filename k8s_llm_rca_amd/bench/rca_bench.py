@@ -108,6 +108,13 @@ def run(args) -> Optional[Dict[str, Any]]:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (bench.py spawns the ranks itself)")
     cuda = torch.cuda.is_available() and args.device != "cpu"
     device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}" if cuda else "cpu")
+    # CPU-side torch ops of the serving process are tiny (metadata packing, pinned
+    # staging): an intra-op pool of OMP_NUM_THREADS spinning workers only competes
+    # with the engine thread for the rank's CPU share.  K8SRCA_TORCH_THREADS=N
+    # sets the pool size (unset: torch's default).
+    nthr = os.environ.get("K8SRCA_TORCH_THREADS")
+    if nthr:
+        torch.set_num_threads(int(nthr))
     if cuda:
         torch.cuda.set_device(device)
 

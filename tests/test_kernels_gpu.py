@@ -896,3 +896,28 @@ def test_gemm_skinny_rope_epilogue_bit_identical(M, nq, nkv):
     kr, vr = torch.zeros_like(kc).cpu(), torch.zeros_like(vc).cpu()
     A.rope_kv_write(r32, pos.cpu(), cs.cpu(), slots.cpu(), kr, vr, nq, nkv)
     torch.testing.assert_close(out.cpu().float(), r32.float(), atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("Bb,mb,n_items", [(1, 4, 1), (24, 130, 37), (256, 130, 0)])
+def test_unpack_step_matches_slices(Bb, mb, n_items):
+    """k8s_unpack_step (one launch before each graph decode step) scatters the
+    flat upload exactly as the seven slice copies it replaces."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    g = torch.Generator().manual_seed(Bb)
+    n = 4 * Bb + Bb * mb + 2 + 4 * n_items
+    flat = torch.randint(-5, 1 << 20, (n,), generator=g, dtype=torch.int32).to(dev)
+    Bmax, imax = 256, 512
+    bufs = [torch.full((Bmax,), -7, dtype=torch.int32, device=dev) for _ in range(4)]
+    bt = torch.full((Bmax, mb), -7, dtype=torch.int32, device=dev)
+    nib = torch.zeros(2, dtype=torch.int32, device=dev)
+    items = torch.full((imax, 4), -7, dtype=torch.int32, device=dev)
+    assert lib().k8s_unpack_step(ptr(flat), Bb, mb, n_items, *[ptr(b) for b in bufs], ptr(bt), ptr(nib), ptr(items),
+                                 stream_ptr(flat)) == 0
+    torch.cuda.synchronize()
+    for i, b in enumerate(bufs):
+        assert torch.equal(b[:Bb], flat[i * Bb:(i + 1) * Bb]) and bool((b[Bb:] == -7).all())
+    o = 4 * Bb + Bb * mb
+    assert torch.equal(bt[:Bb], flat[4 * Bb:o].view(Bb, mb)) and bool((bt[Bb:] == -7).all())
+    assert torch.equal(nib, flat[o:o + 2])
+    assert torch.equal(items[:n_items], flat[o + 2:].view(n_items, 4)) and bool((items[n_items:] == -7).all())

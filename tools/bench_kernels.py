@@ -60,6 +60,7 @@ def main():
     ap.add_argument("--variants", default="", help="replay: comma list of planner variants (default all)")
     ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with every kernel of --pf-kinds")
     ap.add_argument("--pf-steps-out", default="", help="replay: per-step prefill timings (JSON lines) to this file")
+    ap.add_argument("--pf-targets", default="", help="replay: comma list of prefill split targets (workgroups) to A/B")
     ap.add_argument("--pf-kinds", default="1,0", help="K8SRCA_PF_W8 values to A/B (1 w8, 2 w8 no prio, 3 w8 stagger, 0 pg64)")
     args = ap.parse_args()
     dev = "cuda"
@@ -160,7 +161,10 @@ def main():
                     res[f"replay decode {name} B{b[0]}-{b[1]}"] = f"n={n} {u / n:.1f}us/step {by / u / 1e6:.2f} TB/s"
         # prefill: the 8-wave LDS-DMA kernel (K8SRCA_PF_W8=1) and the 4-wave pg64
         # kernel interleaved per recorded step (same process, same data)
-        kinds = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        kinds0 = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        targets = [int(t) for t in args.pf_targets.split(",")] if args.pf_targets else [A.PF_TARGET_WGS]
+        # arms: (kernel kind, planner split target in workgroups); the label keeps the old form for one target
+        kinds = tuple(k if len(targets) == 1 else f"{k}@{t}" for t in targets for k in kinds0)
         tot = {k: 0.0 for k in kinds}
         per_step = {}
         fl = 0.0
@@ -170,7 +174,8 @@ def main():
             ql = [q for c, q in pre[i]]
             T = sum(ql)
             for k in kinds:
-                os.environ["K8SRCA_PF_W8"] = k
+                os.environ["K8SRCA_PF_W8"] = k.split("@")[0]
+                A.PF_TARGET_WGS = int(k.split("@")[1]) if "@" in k else targets[0]
                 torch.manual_seed(i)
                 meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
                 if k == kinds[0]:
@@ -187,7 +192,8 @@ def main():
         for k in kinds:
             res[f"replay prefill {len(idx)} steps PF_W8={k}"] = (f"{tot[k] / len(idx):.1f}us/step "
                                                                f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
-        os.environ["K8SRCA_PF_W8"] = kinds[0]
+        os.environ["K8SRCA_PF_W8"] = kinds0[0]
+        A.PF_TARGET_WGS = targets[0]
         if args.pf_steps_out:
             with open(args.pf_steps_out, "w") as f:
                 for v in per_step.values():

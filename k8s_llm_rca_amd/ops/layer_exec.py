@@ -55,8 +55,13 @@ _fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
 # TP: eager steps of >= TP_OVERLAP_MIN_ROWS rows run the o / down GEMMs in
 # TP_OVERLAP_CHUNKS row blocks, each block's fused all-reduce + add + RMSNorm on
 # a side stream behind its GEMM (overlapping the next block's GEMM).
-# K8SRCA_TP_OVERLAP: 1 (default) on, 0 off, "serial" the same chunks on one stream.
-_tp_overlap = os.environ.get("K8SRCA_TP_OVERLAP", "1")
+# K8SRCA_TP_OVERLAP: 1 on, 0 off (default), "serial" the same chunks on one stream.
+# Off by default: rank 0 of a 70B TP=8 engine on one MI355X (bench.py --tp-sim 8,
+# the xGMI kernels on a loopback communicator) ran 3.68 analyses/s with it vs
+# 4.09 without (profiles/r3/ab/tp_overlap_*_tpsim70b.json): half-M hipBLASLt
+# calls lose more than the side-stream all-reduce hides, and the all-reduce
+# kernel's waves compete with the GEMM for the same CUs.
+_tp_overlap = os.environ.get("K8SRCA_TP_OVERLAP", "0")
 TP_OVERLAP_CHUNKS = int(os.environ.get("K8SRCA_TP_OVERLAP_CHUNKS", "2"))
 TP_OVERLAP_MIN_ROWS = int(os.environ.get("K8SRCA_TP_OVERLAP_MIN_ROWS", "512"))
 

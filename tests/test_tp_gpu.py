@@ -241,7 +241,7 @@ def _overlap_worker(rank, world, port, out_dir):
         torch.cuda.synchronize()
         dist.barrier()
         del eng, model
-    LX.set_tp_overlap("1")
+    LX.set_tp_overlap(os.environ.get("K8SRCA_TP_OVERLAP", "0"))
     status = pc.custom_ar.status()
     pc.custom_ar.close()
     if rank == 0:

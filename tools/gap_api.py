@@ -28,22 +28,27 @@ def main():
             gaps.append((end, s, prev, n))
         if e > end:
             end, prev = e, n
-    api = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Function"], r.get("Thread_Id", ""))
-                 for r in csv.DictReader(open(a.api)))
-    starts = [x[0] for x in api]
+    # one pass over the API calls: each call is matched to the gaps it overlaps by a
+    # bisect on the (sorted, disjoint) gap starts -- O(calls log gaps); progress lines keep
+    # a long trace from looking hung
+    g_starts = [g[0] for g in gaps]
     by = collections.defaultdict(float)
     cnt = collections.Counter()
-    tot = 0.0
-    for g0, g1, p, n in gaps:
-        tot += g1 - g0
-        i = bisect.bisect_left(starts, g0 - 50_000_000)  # calls that began up to 50 ms before the gap
-        for s, e, f, t in api[i:]:
-            if s > g1:
-                break
-            ov = min(e, g1) - max(s, g0)
-            if ov > 0:
-                by[(f, t)] += ov
-                cnt[(f, t)] += 1
+    tot = sum(g1 - g0 for g0, g1, _, _ in gaps)
+    with open(a.api) as f:
+        for n_row, r in enumerate(csv.DictReader(f)):
+            if n_row % 500_000 == 0:
+                print(f"# api rows {n_row}", flush=True)
+            s0, e0 = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            j = bisect.bisect_right(g_starts, e0) - 1
+            while j >= 0 and gaps[j][1] > s0:
+                g0, g1 = gaps[j][0], gaps[j][1]
+                ov = min(e0, g1) - max(s0, g0)
+                if ov > 0:
+                    key = (r["Function"], r.get("Thread_Id", ""))
+                    by[key] += ov
+                    cnt[key] += 1
+                j -= 1
     print(f"{len(gaps)} gaps >= {a.min_us} us, {tot / 1e6:.1f} ms idle")
     for (f, t), v in sorted(by.items(), key=lambda kv: -kv[1])[:25]:
         print(f"{v / 1e6:9.1f} ms overlap  {cnt[(f, t)]:7d} calls  thread {t}  {f}")

@@ -14,7 +14,7 @@ grep '^{"metric"' $O/bench.log | cut -c1-300
 k=$(find $T -name "*kernel_trace.csv" | head -1); a=$(find $T -name "*hip_api_trace.csv" | head -1)
 m=$(find $T -name "*memory_copy_trace.csv" | head -1)
 python3 $R/tools/gap_steps.py $k --min-us 200 --from-frac 0.5 > $O/gap_steps.txt 2>&1; head -40 $O/gap_steps.txt
-python3 $R/tools/gap_api.py $k $a --min-us 500 > $O/gap_api.txt 2>&1; head -40 $O/gap_api.txt
+timeout -k 5 600 python3 -u $R/tools/gap_api.py $k $a --min-us 500 2>&1 | tee $O/gap_api.txt | grep "^# api rows" | tail -1; grep -v "^# api rows" $O/gap_api.txt | head -40
 [ -n "$m" ] && head -3 $m > $O/memcpy_head.csv && python3 - "$m" > $O/memcpy_summary.txt <<'PY'
 import csv, sys, collections
 c = collections.defaultdict(lambda: [0, 0.0, 0])

@@ -131,7 +131,9 @@ def main():
         buckets = [(1, 16), (17, 48), (49, 96), (97, 256)]
         for name, fn in variants.items():
             agg = {b: [0.0, 0.0, 0] for b in buckets}
-            for i in idx:
+            for n_done, i in enumerate(idx):
+                if n_done % 20 == 0:
+                    print(f"# decode replay {name} {n_done}/{len(idx)}", flush=True)
                 ctx = dec[i]
                 B = len(ctx)
                 ovh0 = A.DECODE_ITEM_OVERHEAD
@@ -169,7 +171,9 @@ def main():
         per_step = {}
         fl = 0.0
         idx = torch.randperm(len(pre), generator=rng)[: args.samples].tolist()
-        for i in idx:
+        for n_done, i in enumerate(idx):
+            if n_done % 10 == 0:
+                print(f"# prefill replay {n_done}/{len(idx)}", flush=True)  # a long replay never looks hung
             ctx = [c for c, q in pre[i]]
             ql = [q for c, q in pre[i]]
             T = sum(ql)

@@ -449,7 +449,11 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # "Llama-3-70B TP=8 over xGMI, 10k-node graph, batched multi-incident RCA" (torchrun --nproc-per-node 8)
     "llama3-70b-tp8-10k": dict(model="llama3-70b", tp=8, graph_nodes=10_000),
     # "Mixtral 8x7B MoE backend (grouped GEMM + expert all-to-all over xGMI), 10k-node graph"
-    "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000),
+    # 32k window: reaching its steady state (every thread cut at the window) takes ~30 prior
+    # incidents per thread, whose re-prefill alone outlasts the time budget (12 pre-aged
+    # incidents: 5.6 M tokens of warm-up prefill, no timed step in 360 s,
+    # profiles/r3/presets/mixtral.json); 4 keeps the warm-up inside it
+    "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000, thread_age=4),
 }
 
 

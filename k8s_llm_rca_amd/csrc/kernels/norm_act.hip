@@ -215,15 +215,19 @@ using namespace k8s;
 // and ~10 us of host time) before every HIP-graph decode step: the step's flat
 // int32 upload [ids | pos | slots | ctx | block table (Bb x mb) | n_items, part |
 // items (n_items x 4)] is scattered into the graph's static input buffers.
+// spec_src / tok (overlapped steps): row i < n_spec whose spec_src[i] >= 0 takes
+// its input id from the device tokens the previous step just sampled,
+// max(tok[spec_src[i]], 0) -- the _apply_spec of engine.py in the same launch.
 __global__ void __launch_bounds__(256) unpack_step_kernel(const int* __restrict__ flat, int Bb, int mb, int n_items,
                                                           int* __restrict__ ids, int* __restrict__ pos,
                                                           int* __restrict__ slots, int* __restrict__ ctx,
                                                           int* __restrict__ bt, int* __restrict__ n_items_buf,
-                                                          int* __restrict__ items) {
+                                                          int* __restrict__ items, const int* __restrict__ spec_src,
+                                                          const int* __restrict__ tok, int n_spec) {
   const int head = 4 * Bb + Bb * mb, total = head + 2 + 4 * n_items;
   for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
     const int v = flat[i];
-    if (i < Bb) ids[i] = v;
+    if (i < Bb) ids[i] = (i < n_spec && spec_src[i] >= 0) ? max(tok[spec_src[i]], 0) : v;
     else if (i < 2 * Bb) pos[i - Bb] = v;
     else if (i < 3 * Bb) slots[i - 2 * Bb] = v;
     else if (i < 4 * Bb) ctx[i - 3 * Bb] = v;
@@ -234,12 +238,15 @@ __global__ void __launch_bounds__(256) unpack_step_kernel(const int* __restrict_
 }
 
 K8S_API int k8s_unpack_step(const void* flat, int Bb, int mb, int n_items, void* ids, void* pos, void* slots,
-                            void* ctx, void* bt, void* n_items_buf, void* items, hipStream_t s) {
-  if (Bb <= 0 || mb <= 0 || n_items < 0) return (int)hipErrorInvalidValue;
+                            void* ctx, void* bt, void* n_items_buf, void* items, const void* spec_src,
+                            const void* tok, int n_spec, hipStream_t s) {
+  if (Bb <= 0 || mb <= 0 || n_items < 0 || n_spec < 0 || n_spec > Bb || (n_spec && (!spec_src || !tok)))
+    return (int)hipErrorInvalidValue;
   const int total = 4 * Bb + Bb * mb + 2 + 4 * n_items;
   const int grid = std::min((total + 255) / 256, 256);
   hipLaunchKernelGGL(unpack_step_kernel, dim3(grid), dim3(256), 0, s, (const int*)flat, Bb, mb, n_items, (int*)ids,
-                     (int*)pos, (int*)slots, (int*)ctx, (int*)bt, (int*)n_items_buf, (int*)items);
+                     (int*)pos, (int*)slots, (int*)ctx, (int*)bt, (int*)n_items_buf, (int*)items,
+                     (const int*)spec_src, (const int*)tok, n_spec);
   return (int)hipGetLastError();
 }
 

@@ -1365,7 +1365,6 @@ class LLMEngine:
         hv = host.numpy()
         n = flat.size
         hv[:n] = flat
-        o = 4 * Bb + Bb * mb  # offset of (n_items, part)
         if spec is not None:
             hv[n:n + B] = spec[0]
             n_src = n
@@ -1379,14 +1378,20 @@ class LLMEngine:
         dev_flat.copy_(host[:n], non_blocking=True)
         ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event()
         ev.record()
-        # the upload scattered into the graph's static inputs in one launch (csrc/kernels/norm_act.hip)
+        # the upload scattered into the graph's static inputs in one launch (csrc/kernels/norm_act.hip),
+        # the speculative decode ids (spec) taken from the device tokens in the same launch; before a
+        # capture too: its warm-up forwards read these ids
         from ..ops._lib import check, lib, stream_ptr
+        tok = _spec_tok(spec) if spec is not None else None  # launches the previous step's sampling
+        fused_spec = tok is not None and tok.dtype == torch.int32 and tok.is_contiguous()
         check(lib().k8s_unpack_step(dev_flat.data_ptr(), Bb, mb, n_items, st["ids"].data_ptr(), st["pos"].data_ptr(),
                                     st["slots"].data_ptr(), st["ctx"].data_ptr(), st["bt"].data_ptr(),
-                                    st["n_items"].data_ptr(), st["items"].data_ptr(), stream_ptr(dev_flat)),
-              "unpack_step")
-        if spec is not None:  # before a capture too: its warm-up forwards read these ids
-            self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], _spec_tok(spec))
+                                    st["n_items"].data_ptr(), st["items"].data_ptr(),
+                                    dev_flat[n_src:].data_ptr() if fused_spec else None,
+                                    tok.data_ptr() if fused_spec else None, B if fused_spec else 0,
+                                    stream_ptr(dev_flat)), "unpack_step")
+        if tok is not None and not fused_spec:
+            self._apply_spec(st["ids"], dev_flat[n_src:n_src + B], tok)
         graph, out = self._capture(Bb, part)  # one graph per bucket: the plan's part size is read on the device
         graph.replay()
         if n_sel:

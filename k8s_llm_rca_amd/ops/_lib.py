@@ -27,7 +27,7 @@ F = ctypes.c_float
 _SIGS = {
     "k8s_rmsnorm": [P, P, P, P, I, I, I, I, F, P],
     "k8s_silu_mul": [P, P, I, I, P],
-    "k8s_unpack_step": [P, I, I, I, P, P, P, P, P, P, P, P],
+    "k8s_unpack_step": [P, I, I, I, P, P, P, P, P, P, P, P, P, I, P],
     "k8s_rope_kv": [P, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_splitk_rope_kv": [P, I, P, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_attn_decode": [P, I, P, P, P, I, P, P, I, I, I, I, F, P, I, P, P, I, I, P, I, P, I, P],

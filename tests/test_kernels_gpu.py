@@ -901,7 +901,8 @@ def test_gemm_skinny_rope_epilogue_bit_identical(M, nq, nkv):
 @pytest.mark.parametrize("Bb,mb,n_items", [(1, 4, 1), (24, 130, 37), (256, 130, 0)])
 def test_unpack_step_matches_slices(Bb, mb, n_items):
     """k8s_unpack_step (one launch before each graph decode step) scatters the
-    flat upload exactly as the seven slice copies it replaces."""
+    flat upload exactly as the seven slice copies it replaces, and takes the
+    speculative decode ids from the device tokens as _apply_spec does."""
     _need_gpu()
     from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
     g = torch.Generator().manual_seed(Bb)
@@ -912,11 +913,21 @@ def test_unpack_step_matches_slices(Bb, mb, n_items):
     bt = torch.full((Bmax, mb), -7, dtype=torch.int32, device=dev)
     nib = torch.zeros(2, dtype=torch.int32, device=dev)
     items = torch.full((imax, 4), -7, dtype=torch.int32, device=dev)
+    # speculative ids: rows with src >= 0 take max(tok[src], 0) (a negative tok = a finished row)
+    n_spec = min(Bb, 5)
+    src = torch.tensor([2, -1, 0, 3, -1][:n_spec], dtype=torch.int32, device=dev)
+    tok = torch.tensor([11, -1, 13, 14], dtype=torch.int32, device=dev)
     assert lib().k8s_unpack_step(ptr(flat), Bb, mb, n_items, *[ptr(b) for b in bufs], ptr(bt), ptr(nib), ptr(items),
-                                 stream_ptr(flat)) == 0
+                                 ptr(src), ptr(tok), n_spec, stream_ptr(flat)) == 0
     torch.cuda.synchronize()
+    want_ids = flat[:Bb].clone()
+    pick = tok.index_select(0, src.clamp(min=0).long()).clamp(min=0)
+    want_ids[:n_spec] = torch.where(src >= 0, pick, want_ids[:n_spec])
+    assert torch.equal(bufs[0][:Bb], want_ids)
     for i, b in enumerate(bufs):
-        assert torch.equal(b[:Bb], flat[i * Bb:(i + 1) * Bb]) and bool((b[Bb:] == -7).all())
+        if i:
+            assert torch.equal(b[:Bb], flat[i * Bb:(i + 1) * Bb])
+        assert bool((b[Bb:] == -7).all())
     o = 4 * Bb + Bb * mb
     assert torch.equal(bt[:Bb], flat[4 * Bb:o].view(Bb, mb)) and bool((bt[Bb:] == -7).all())
     assert torch.equal(nib, flat[o:o + 2])

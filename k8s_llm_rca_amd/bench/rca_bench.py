@@ -451,9 +451,11 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # "Mixtral 8x7B MoE backend (grouped GEMM + expert all-to-all over xGMI), 10k-node graph"
     # 32k window: reaching its steady state (every thread cut at the window) takes ~30 prior
     # incidents per thread, whose re-prefill alone outlasts the time budget (12 pre-aged
-    # incidents: 5.6 M tokens of warm-up prefill, no timed step in 360 s,
-    # profiles/r3/presets/mixtral.json); 4 keeps the warm-up inside it
-    "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000, thread_age=4),
+    # incidents: no timed step in 360 s); 4 keeps the warm-up inside it.  And 128
+    # pipelines x 3 threads x ~8k tokens exceed the KV pool left beside 94 GB of experts
+    # (1.34 M tokens): 754 preemptions, 36k prefill tokens per analysis, 0.77 /s
+    # (profiles/r3/presets/mixtral_128.json) -- 48 concurrent analyses fit
+    "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000, thread_age=4, incidents=48, quantum=6),
 }
 
 

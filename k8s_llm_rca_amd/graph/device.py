@@ -81,8 +81,9 @@ class DeviceGraph:
         h = self._heaps.get(key)
         if h is None:
             offs, buf = self.g.string_heap(key)
-            h = (torch.from_numpy(offs).to(self.device),
-                 torch.from_numpy(buf if len(buf) else np.zeros(1, np.uint8)).to(self.device))
+            with self._ctx():  # uploaded on the mirror's stream, read there (never the engine's)
+                h = (self._up(offs, offs.dtype), self._up(buf if len(buf) else np.zeros(1, np.uint8), np.uint8))
+                (_,) = self._fetch(h[0][:1])  # the heap is resident before the first kernel reads it
             self.bytes += h[0].numel() * 8 + h[1].numel()
             self._heaps[key] = h
         return h
@@ -126,23 +127,30 @@ class DeviceGraph:
         kid = -2 if key is None else self.g.keys.lookup(key)
         tm = self._type_mask(rel_types)
         outs = []
-        d_ids = torch.from_numpy(np.ascontiguousarray(ids, dtype=np.int64)).to(self.device)
         n = len(ids)
-        for side in (("out",) if direction == "out" else ("in",) if direction == "in" else ("out", "in")):
-            ip, nb, ei = (self.oip, self.onb, self.oei) if side == "out" else (self.iip, self.inb, self.iei)
-            skip = 1 if (direction == "both" and side == "in") else 0
-            counts = torch.empty(n, dtype=torch.int32, device=self.device)
-            check(lib().k8s_graph_expand2(ptr(ip), ptr(nb), ptr(ei), ptr(self.etype), ptr(self.ekey), ptr(self.esrc),
-                                          ptr(self.edst), ptr(d_ids), n, tm, kid, skip, ptr(counts), 0, 0, 0, 0,
-                                          stream_ptr(d_ids)), "graph_expand")
-            offsets = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
-            torch.cumsum(counts, 0, out=offsets[1:])
-            total = int(offsets[-1].item())
-            o = [torch.empty(max(total, 1), dtype=torch.int64, device=self.device) for _ in range(3)]
-            check(lib().k8s_graph_expand2(ptr(ip), ptr(nb), ptr(ei), ptr(self.etype), ptr(self.ekey), ptr(self.esrc),
-                                          ptr(self.edst), ptr(d_ids), n, tm, kid, skip, ptr(counts), ptr(offsets),
-                                          ptr(o[0]), ptr(o[1]), ptr(o[2]), stream_ptr(d_ids)), "graph_expand")
-            outs.append(tuple(t[:total].cpu().numpy() for t in o))
+        # on the mirror's stream like every other op: on the caller's (default) stream
+        # the count read-back waited for the LLM engine's queued forward, and the
+        # engine's next kernels queued behind these
+        with self._ctx():
+            d_ids = self._up(ids, np.int64)
+            for side in (("out",) if direction == "out" else ("in",) if direction == "in" else ("out", "in")):
+                ip, nb, ei = (self.oip, self.onb, self.oei) if side == "out" else (self.iip, self.inb, self.iei)
+                skip = 1 if (direction == "both" and side == "in") else 0
+                counts = torch.empty(n, dtype=torch.int32, device=self.device)
+                check(lib().k8s_graph_expand2(ptr(ip), ptr(nb), ptr(ei), ptr(self.etype), ptr(self.ekey),
+                                              ptr(self.esrc), ptr(self.edst), ptr(d_ids), n, tm, kid, skip,
+                                              ptr(counts), 0, 0, 0, 0, stream_ptr(d_ids)), "graph_expand")
+                offsets = torch.zeros(n + 1, dtype=torch.int64, device=self.device)
+                torch.cumsum(counts, 0, out=offsets[1:])
+                (tot,) = self._fetch(offsets[-1:])
+                total = int(tot[0])
+                o = [torch.empty(max(total, 1), dtype=torch.int64, device=self.device) for _ in range(3)]
+                check(lib().k8s_graph_expand2(ptr(ip), ptr(nb), ptr(ei), ptr(self.etype), ptr(self.ekey),
+                                              ptr(self.esrc), ptr(self.edst), ptr(d_ids), n, tm, kid, skip,
+                                              ptr(counts), ptr(offsets), ptr(o[0]), ptr(o[1]), ptr(o[2]),
+                                              stream_ptr(d_ids)), "graph_expand")
+                self.launches += 2
+                outs.append(tuple(self._fetch(*[t[:total] for t in o])))
         if len(outs) == 1:
             return outs[0]
         row = np.concatenate([x[0] for x in outs])

@@ -22,7 +22,30 @@ from typing import Any, Dict, Optional
 
 from k8s_llm_rca_amd.api.graph import GraphQueryExecutor
 
-from . import exceptions, graph  # noqa: F401  (neo4j.exceptions / neo4j.graph)
+import sys
+import types
+
+from k8s_llm_rca_amd.graph import model as _model
+
+
+def _submodule(name: str, doc: str, **attrs) -> types.ModuleType:
+    """``neo4j.<name>`` holding the engine's own classes (registered in
+    ``sys.modules`` so ``import neo4j.graph`` / ``from neo4j.exceptions import
+    ...`` resolve to it)."""
+    m = types.ModuleType(f"{__name__}.{name}", doc)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    m.__all__ = list(attrs)
+    sys.modules[m.__name__] = m
+    return m
+
+
+graph = _submodule("graph", "the engine's Node / Relationship / Path result types",
+                   Node=_model.Node, Relationship=_model.Relationship, Path=_model.Path)
+exceptions = _submodule("exceptions", "the engine's own Cypher error classes",
+                        CypherSyntaxError=_model.CypherSyntaxError, CypherTypeError=_model.CypherTypeError,
+                        CypherError=_model.CypherError, Neo4jError=_model.CypherError,
+                        ClientError=_model.CypherError, ServiceUnavailable=ConnectionError)
 
 __all__ = ["GraphDatabase", "Driver", "Session", "Result", "map_uri", "exceptions", "graph", "basic_auth"]
 

@@ -84,6 +84,31 @@ def test_reference_driver_runs_on_compat_paths(ref_env):
     assert n_records >= 1
     metagraph.close()
     stategraph.close()
+    # the adapter classes keep the reference's names and module paths
+    assert OpenAIGenericAssistant.__module__ == "common.openai_generic_assistant"
+    assert Neo4jQueryExecutor.__name__ == "Neo4jQueryExecutor"
+
+
+def test_compat_neo4j_submodules():
+    """``neo4j.graph`` / ``neo4j.exceptions`` of the shim are the engine's classes."""
+    import sys
+
+    from k8s_llm_rca_amd import compat
+    from k8s_llm_rca_amd.graph import model
+    saved_path = list(sys.path)
+    saved_mods = {k: v for k, v in sys.modules.items() if k.split(".")[0] == "neo4j"}
+    for k in saved_mods:
+        del sys.modules[k]
+    sys.path.insert(0, compat.SHIMS_DIR)
+    try:
+        import neo4j.graph
+        from neo4j.exceptions import CypherSyntaxError
+        assert neo4j.graph.Node is model.Node and CypherSyntaxError is model.CypherSyntaxError
+    finally:
+        sys.path[:] = saved_path
+        for k in [k for k in sys.modules if k.split(".")[0] == "neo4j"]:
+            del sys.modules[k]
+        sys.modules.update(saved_mods)
 
 
 REF = "/root/reference"
@@ -101,7 +126,7 @@ def test_reference_test_all_runs_unchanged_on_shims(monkeypatch, capsys):
     import sys
     import time as _time
 
-    from k8s_llm_rca_amd.compat import COMPAT_DIR, SHIMS_DIR
+    from k8s_llm_rca_amd.compat import SHIMS_DIR, install, uninstall
     from k8s_llm_rca_amd.graph.synth import generate_cluster
     from k8s_llm_rca_amd.pipeline.generate_query import human_generate_cypher_query
 
@@ -112,9 +137,10 @@ def test_reference_test_all_runs_unchanged_on_shims(monkeypatch, capsys):
     saved_mods = {k: v for k, v in sys.modules.items() if k.split(".")[0] in names}
     for k in saved_mods:
         del sys.modules[k]
-    # the reference's `common` is a namespace package: our compat copy (a regular
-    # package) would win over it, so it is taken off the path here
-    sys.path[:] = [SHIMS_DIR, REF] + [p for p in saved_path if p != COMPAT_DIR]
+    # the compat import hook would serve `common` etc. ahead of the reference's
+    # own (namespace) packages, so it is taken out here
+    hooked = uninstall()
+    sys.path[:] = [SHIMS_DIR, REF] + saved_path
     try:
         import neo4j  # the shim
         assert neo4j.__file__.startswith(SHIMS_DIR)
@@ -148,6 +174,8 @@ def test_reference_test_all_runs_unchanged_on_shims(monkeypatch, capsys):
         for k in [k for k in sys.modules if k.split(".")[0] in names]:
             del sys.modules[k]
         sys.modules.update(saved_mods)
+        if hooked:
+            install()
         set_default_service(None)
     out = capsys.readouterr().out
     assert "nfs path missing" in out  # check_statepath's summary report was printed

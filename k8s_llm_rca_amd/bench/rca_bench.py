@@ -352,6 +352,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,
                    "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
+                   "prefill_min_tokens": eng.cfg.prefill_min_tokens,
+                   "prefill_deferred_steps": d.get("prefill_deferred_steps", 0),
                    # decode-attention KV blocks read per distinct block (sampled every 32nd graph step)
                    "kv_block_reuse": round(d["kv_read_blocks_sampled"] / max(1, d["kv_unique_blocks_sampled"]), 2),
                    "admit_s": round(d["admit_s"], 3), "post_s": round(d["post_s"], 3),

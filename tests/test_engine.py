@@ -265,6 +265,38 @@ def test_async_steps_match_sync(temperature):
     assert outs[0] == outs[1]
 
 
+def test_prompt_prefill_batching_defers_then_runs():
+    """``prefill_min_tokens``: while decode rows run, a new run's short prompt
+    waits (bounded by ``prefill_max_defer_s``) instead of taking a mixed step of
+    its own; every run still completes with the tokens the undeferred engine
+    generates."""
+    import time as _t
+    outs = []
+    for pmin in (0, 10_000):
+        eng = _engine(temperature=0.0, prefill_min_tokens=pmin, prefill_max_defer_s=0.05, num_blocks=128)
+        res = {}
+        sid0 = eng.new_sequence()
+        p0 = eng.tok.system_prefix("s") + eng.tok.message("user", "first") + eng.tok.header("assistant")
+        eng.submit(sid0, p0, None, 40, on_done=lambda g, st: res.__setitem__(0, g))
+        for _ in range(3):
+            eng.step()  # the first run is decoding now
+        sid1 = eng.new_sequence()
+        p1 = eng.tok.system_prefix("s") + eng.tok.message("user", "second one") + eng.tok.header("assistant")
+        eng.submit(sid1, p1, None, 6, on_done=lambda g, st: res.__setitem__(1, g))
+        t0 = _t.perf_counter()
+        while eng.seqs[sid1].n_cached == 0:
+            eng.step()
+        waited = _t.perf_counter() - t0
+        eng.run_until_idle()
+        deferred = eng.stats["prefill_deferred_steps"]
+        if pmin:
+            assert deferred > 0 and waited >= 0.04  # held back until its submit was 50 ms old
+        else:
+            assert deferred == 0
+        outs.append(res)
+    assert outs[0] == outs[1] and len(outs[0]) == 2
+
+
 def _greedy(eng, prompts, max_new=8):
     outs = {}
     for i, p in enumerate(prompts):

@@ -112,10 +112,12 @@ class EngineConfig:
     # (hipBLASLt per projection: ~900-1300 TFLOP/s at M = 1024 vs ~1300-1500 at
     # 2048, far less below 512) and fewer steps pay a full weight pass for a few
     # hundred prompt rows.  Jump-forward chunks of a running generation are never
-    # held back.  0 disables
-    prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "0")))
+    # held back.  Headline A/B, interleaved (profiles/r3/ab/prefill_min_*.json):
+    # 0 -> 4.531 / 4.532, 2048 tokens within 0.1 s -> 4.580 / 4.552 analyses/s.
+    # 0 disables
+    prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "2048")))
     prefill_max_defer_s: float = field(default_factory=lambda: float(os.environ.get("K8SRCA_PREFILL_DEFER_S",
-                                                                                    "0.05")))
+                                                                                    "0.1")))
     # prefill chunks of at most this many tokens (grammar jump-forward runs) are
     # run as rows of the decode-attention work list (one row per token, its own
     # causal key count) instead of a prefill tile that walks every page for a

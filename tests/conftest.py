@@ -6,6 +6,11 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# prompt prefill batching holds prompts back by WALL-CLOCK time, so which step
+# a prompt lands in would vary run to run; tests that compare two engines'
+# tokens need identical step composition.  The batching itself has its own
+# tests (test_engine.py::test_prompt_prefill_batching_defers_then_runs).
+os.environ.setdefault("K8SRCA_PREFILL_MIN", "0")
 
 
 def pytest_configure(config):

@@ -424,7 +424,8 @@ def parser() -> argparse.ArgumentParser:
                    help="keep the graphs on the host (default on GPU: HBM mirror + batched HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
-    p.add_argument("--max-batch-tokens", type=int, default=8192)
+    p.add_argument("--max-batch-tokens", type=int,
+                   default=int(os.environ.get("K8SRCA_MAX_BATCH_TOKENS", "8192")))
     p.add_argument("--temperature", type=float, default=0.7)
     p.add_argument("--semantic-tokens", type=int, default=192)
     p.add_argument("--explanation-tokens", type=int, default=40)

@@ -113,11 +113,13 @@ class EngineConfig:
     # 2048, far less below 512) and fewer steps pay a full weight pass for a few
     # hundred prompt rows.  Jump-forward chunks of a running generation are never
     # held back.  Headline A/B, interleaved (profiles/r3/ab/prefill_min_*.json):
-    # 0 -> 4.531 / 4.532, 2048 tokens within 0.1 s -> 4.580 / 4.552 analyses/s.
+    # 0 -> 4.531 / 4.532, 2048 tokens within 0.1 s -> 4.580 / 4.552 analyses/s;
+    # then 2048 / 0.1 s -> 4.544 / 4.593 vs 4096 / 0.3 s -> 4.606 / 4.601 (p50
+    # 28.0 vs 28.1 s, TTFT p50 68 ms either way).
     # 0 disables
-    prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "2048")))
+    prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "4096")))
     prefill_max_defer_s: float = field(default_factory=lambda: float(os.environ.get("K8SRCA_PREFILL_DEFER_S",
-                                                                                    "0.1")))
+                                                                                    "0.3")))
     # prefill chunks of at most this many tokens (grammar jump-forward runs) are
     # run as rows of the decode-attention work list (one row per token, its own
     # causal key count) instead of a prefill tile that walks every page for a

@@ -118,6 +118,11 @@ class EngineConfig:
     # 28.0 vs 28.1 s, TTFT p50 68 ms either way).
     # 0 disables
     prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "4096")))
+    # ... only while at least this many decode rows run (a busy, throughput-bound
+    # engine): at low concurrency a held prompt would only add its wait to the
+    # run's latency
+    prefill_defer_min_rows: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_DEFER_ROWS",
+                                                                                   "96")))
     prefill_max_defer_s: float = field(default_factory=lambda: float(os.environ.get("K8SRCA_PREFILL_DEFER_S",
                                                                                     "0.3")))
     # prefill chunks of at most this many tokens (grammar jump-forward runs) are
@@ -646,7 +651,8 @@ class LLMEngine:
         chunks: List[Tuple[Sequence, int]] = []
         cands = [s for s in active if (s.pending > 1 or (s.pending == 1 and s.id not in placed))
                  and s.tokens[-1] != SPEC]
-        if decode and cands and self.cfg.prefill_min_tokens > 0 and self._defer_prefill(cands):
+        if (cands and self.cfg.prefill_min_tokens > 0 and len(decode) >= max(1, self.cfg.prefill_defer_min_rows)
+                and self._defer_prefill(cands)):
             cands = []
             self.stats["prefill_deferred_steps"] += 1
         for s in cands:

@@ -273,7 +273,8 @@ def test_prompt_prefill_batching_defers_then_runs():
     import time as _t
     outs = []
     for pmin in (0, 10_000):
-        eng = _engine(temperature=0.0, prefill_min_tokens=pmin, prefill_max_defer_s=0.05, num_blocks=128)
+        eng = _engine(temperature=0.0, prefill_min_tokens=pmin, prefill_max_defer_s=0.05, num_blocks=128,
+                      prefill_defer_min_rows=1)
         res = {}
         sid0 = eng.new_sequence()
         p0 = eng.tok.system_prefix("s") + eng.tok.message("user", "first") + eng.tok.header("assistant")
@@ -295,6 +296,17 @@ def test_prompt_prefill_batching_defers_then_runs():
             assert deferred == 0
         outs.append(res)
     assert outs[0] == outs[1] and len(outs[0]) == 2
+    # below prefill_defer_min_rows decode rows nothing is held back
+    eng = _engine(temperature=0.0, prefill_min_tokens=10_000, prefill_defer_min_rows=2, num_blocks=128)
+    sid0 = eng.new_sequence()
+    eng.submit(sid0, eng.tok.system_prefix("s") + eng.tok.message("user", "a") + eng.tok.header("assistant"), None, 20)
+    for _ in range(3):
+        eng.step()
+    sid1 = eng.new_sequence()
+    eng.submit(sid1, eng.tok.system_prefix("s") + eng.tok.message("user", "b c") + eng.tok.header("assistant"), None, 4)
+    eng.step()
+    assert eng.seqs[sid1].n_cached > 0 and eng.stats["prefill_deferred_steps"] == 0
+    eng.run_until_idle()
 
 
 def _greedy(eng, prompts, max_new=8):

@@ -33,6 +33,17 @@ METRIC = "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-nod
 REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
 
 
+def _native_cpu() -> Dict[int, float]:
+    """CPU seconds per native (non-Python) thread of this process, by thread id."""
+    import threading
+    try:
+        import psutil
+        py = {t.native_id for t in threading.enumerate()}
+        return {t.id: t.user_time + t.system_time for t in psutil.Process().threads() if t.id not in py}
+    except Exception:
+        return {}
+
+
 def _thread_cpu() -> Dict[str, float]:
     """CPU seconds per thread group of this process (engine / graph batcher /
     RCA pipelines / other): which Python threads compete with the engine
@@ -231,13 +242,16 @@ def run(args) -> Optional[Dict[str, Any]]:
     age0 = [p.n_analyses for p in pipelines]
     ctx0 = backend.thread_stats()
     t_wall0 = time.time()
-    cpu0 = _thread_cpu()
+    cpu0, ncpu0 = _thread_cpu(), _native_cpu()
     t0 = time.perf_counter()
     base = stream.n_ok
     done_all = stream.wait_ok(base + n_steps * quantum, deadline, _poll)
     t_end = time.perf_counter()
-    cpu1 = _thread_cpu()
+    cpu1, ncpu1 = _thread_cpu(), _native_cpu()
     ctx1 = backend.thread_stats()
+    # the busiest native threads over the window (HIP runtime / torch pools: one
+    # polling thread vs many pool workers)
+    native_top = sorted((round(v - ncpu0.get(t, 0.0), 2) for t, v in ncpu1.items()), reverse=True)
     n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
@@ -379,6 +393,7 @@ def run(args) -> Optional[Dict[str, Any]]:
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         # CPU seconds per thread group over the timed window (GIL competition with the engine thread)
         "host_cpu_s": {k: round(v - cpu0.get(k, 0.0), 2) for k, v in cpu1.items()},
+        "native_threads": {"n": len(native_top), "top_cpu_s": native_top[:4]},
         "setup_s": round(setup_s, 1),
         "wall_s": round(time.perf_counter() - t_start, 1),
         "clean_shutdown": clean,

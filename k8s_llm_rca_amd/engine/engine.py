@@ -304,7 +304,8 @@ class LLMEngine:
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
-                      "prefix_hit_tokens": 0, "prefill_deferred_steps": 0, "preemptions": 0, "cancelled": 0, "timeouts": 0,
+                      "prefix_hit_tokens": 0, "prefill_deferred_steps": 0, "preemptions": 0, "cancelled": 0,
+                      "timeouts": 0,
                       "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
                       "tiny_chunk_tokens": 0}
         self._cancels: List[int] = []

@@ -106,12 +106,16 @@ _HOOK = _ReferencePaths()
 
 def install(shims: bool = False) -> None:
     """Make the reference's top-level package names importable (the import
-    hook, first on ``sys.meta_path``).  ``shims``: also put this framework's
-    ``openai`` and ``neo4j`` modules first on the path (``compat/shims``), so
-    the reference's OWN adapter modules (``common/openai_generic_assistant.py``
-    / ``neo4j_query_executor.py``, which import those SDKs) run unchanged on
-    the in-process services.  Off by default: it shadows real installs of
-    those packages."""
+    hook, first on ``sys.meta_path``).  While the hook is installed it serves
+    ``common.*``, ``find_metapath.*``, ``generate_query.*`` and ``check_state.*``
+    with this framework's implementations, AHEAD of any reference checkout on
+    ``sys.path``.  ``shims``: also put this framework's ``openai`` and ``neo4j``
+    modules first on the path (``compat/shims``), so code that imports those
+    SDKs runs on the in-process services; to run the reference's OWN adapter
+    modules (``common/openai_generic_assistant.py`` /
+    ``neo4j_query_executor.py``) over the shims, call :func:`uninstall` first
+    so the checkout's files are imported (``tests/test_compat.py`` does).  Off
+    by default: the shims shadow real installs of those packages."""
     if _HOOK not in sys.meta_path:
         sys.meta_path.insert(0, _HOOK)
     if shims and SHIMS_DIR not in sys.path:

@@ -934,8 +934,10 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   const int wave_hi = wave_live ? base_pos + wt1 + 1 : 0;
   const int kv_end = base_pos + tlen;
   const int p_begin = a.tile_kv0[tile];
-  const int n_pages = min(a.tile_kv1[tile], (kv_end + PF_PAGE - 1) / PF_PAGE);
-  const int np = n_pages - p_begin;  // host-checked <= PF8_MAXP
+  // the planner splits key ranges at PF8_MAXP pages per item (ops/attention.py
+  // plan_prefill); the clamp only keeps a foreign plan inside the LDS table
+  const int n_pages = min(min(a.tile_kv1[tile], (kv_end + PF_PAGE - 1) / PF_PAGE), p_begin + PF8_MAXP);
+  const int np = n_pages - p_begin;
   const int slot = a.tile_slot[tile];
 
   for (int i = tid; i < np; i += 512) s_blk[i] = bt[p_begin + i];
@@ -1315,9 +1317,11 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
   if (n_tiles <= 0) return (int)hipSuccess;
   if (BS == PF_PAGE && PF_ROWS % a.G == 0) {
     if (n_merge > 0 && (!pf_o || !pf_ml)) return (int)hipErrorInvalidValue;
-    // the tile size is the planner's (ops/attention.py pf_wg_rows(): the same switch)
+    // the tile size is the planner's: ops/attention.py pf_wg_rows() is the same
+    // function of (K8SRCA_PF_W8, G) -- no other condition may pick the 128-row
+    // kernel for a plan tiled at 256 rows (its rows 128.. would never be written)
     const int var = prefill_w8();
-    const bool w8 = var > 0 && PF8_ROWS % a.G == 0 && bt_stride <= PF8_MAXP;
+    const bool w8 = var > 0 && PF8_ROWS % a.G == 0;
     a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
     if (w8 && var == 3)
       hipLaunchKernelGGL(attn_prefill_w8_kernel<3>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);

@@ -175,7 +175,7 @@ __device__ void radix_pass(const T* lr, int V, int vocab_off, float it, const in
     }
     if (pick < 0) {  // rounding: the target was never reached -> keep the whole remaining set
       pick = lowest < 0 ? 0 : lowest;
-      if (lowest >= 0) cum -= hist[lowest];
+      if (lowest >= 0) cum -= (float)((double)hist[lowest] * (1.0 / kMassScale));  // mass units, like cum
     }
     *need = rem - cum;
     *prefix = pre | ((uint32_t)pick << (8 * byte));

@@ -312,6 +312,8 @@ class LLMEngine:
         self.error: Optional[BaseException] = None
         self._fault: Optional[str] = None  # a dead communicator: every later request fails at admission
         self._test_stall = False  # tests: a TP worker that receives steps but never executes them
+        self._test_host_stall_s = 0.0  # tests: rank 0 sleeps between a step's message and its own launch
+        self.comm_dead = False  # a TP worker whose own collective timed out: it stops executing steps
 
     def _workspace_bytes(self) -> int:
         mc = self.mc
@@ -1203,6 +1205,9 @@ class LLMEngine:
         if self._chan is not None:
             from ..parallel.channel import FWD_EAGER
             self._chan.send(FWD_EAGER, [header, flat] + ([spec[0]] if spec is not None else []))
+            if self._test_host_stall_s:  # fault injection: the workers' collectives outwait their timeout
+                time.sleep(self._test_host_stall_s)
+                self._test_host_stall_s = 0.0
         return self._run_eager(header, flat, spec)
 
     def _run_eager(self, header, flat, spec):
@@ -1233,15 +1238,36 @@ class LLMEngine:
         logits = None
         if self.device.type == "cuda":
             torch.cuda.set_device(self.device)
+        car = self.pc.custom_ar if self.device.type == "cuda" else None
+        status, status_ev = None, None
         while True:
             kind, arrs = self._chan.recv()
             if kind == STOP:
                 return
-            if self._test_stall:  # fault injection: this peer stops arriving at the collectives
+            if self._test_stall or self.comm_dead:  # this peer no longer arrives at the collectives
                 continue
             if kind == SAMPLE:
+                # the previous step's STATUS (its copy was queued a step ago): once
+                # this rank's own wait timed out it skips every later wait but would
+                # still publish flags, so rank 0 would mix unsynchronized partials
+                # silently.  Stop executing instead: rank 0's next collective then
+                # times out and fails every run with CommFault.
+                # The check never waits for the GPU: a copy still in flight is
+                # read at a later step.
+                ready = status_ev is None or status_ev.query()
+                if status_ev is not None and ready and int(status[0]) != 0:
+                    self.comm_dead = True
+                    log.error("TP rank %d: xGMI collective timed out (STATUS set); "
+                              "this worker stops executing steps", self.pc.tp_rank)
+                    continue
                 hdr, flat, rows_a = arrs
                 self._last_tok = self._sample_rows(logits, hdr, flat, rows_a)
+                if car is not None and ready:
+                    if status is None:
+                        status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+                        status_ev = torch.cuda.Event()
+                    car.status_async(status)
+                    status_ev.record()
             elif kind == FWD_EAGER:
                 spec = (arrs[2], self._last_tok) if len(arrs) > 2 else None
                 logits = self._run_eager(arrs[0], arrs[1], spec)
@@ -1482,11 +1508,6 @@ class LLMEngine:
         filt = bool((topk > 0).any() or (topp < 1.0).any())
         status = None
         car = self.pc.custom_ar if self.pc.tp_size > 1 else None
-        if car is not None and self.device.type == "cuda":
-            # the communicator's STATUS, stream-ordered before this sampling: valid
-            # once the sampled tokens are (_process_tokens checks it first)
-            status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
-            car.status_async(status)
         if self._dist_sample:
             tok = self._tp_sample(logits, mask_id, list_off, list_len, np.asarray(lists, np.int32),
                                   seeds, steps, temps, topk, topp, rows)
@@ -1504,6 +1525,12 @@ class LLMEngine:
             tok = SMP.sample(logits, d_temps, ints[4], ints[5], ints[0], table, ints[1], ints[2], ints[3],
                              vocab=self.vocab, top_k=ints[7] if filt else None,
                              top_p=ints[8].view(torch.float32) if filt else None)
+        if car is not None and self.device.type == "cuda":
+            # the communicator's STATUS, stream-ordered after this step's forward and
+            # the sampling collectives (the xGMI all-gather of the TP winners): valid
+            # once the sampled tokens are (_process_tokens checks it first)
+            status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+            car.status_async(status)
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)

@@ -347,6 +347,7 @@ def prefill_tile_tokens(G: int, block_size: int) -> int:
 
 PF_ROWS = 128               # (token, q-head) rows per pg64 prefill workgroup
 PF8_ROWS = 256              # rows per 8-wave (w8) prefill workgroup
+PF8_MAXP = 1024             # key pages per w8 work item (page ids staged in LDS; attention.hip)
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
 # split long key ranges until a prefill launch has about this many workgroups
 PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
@@ -402,6 +403,9 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
     most-pages first so the longest ones start first."""
     target_wgs = target_wgs or PF_TARGET_WGS
     per = prefill_tile_tokens(G, block_size)
+    # the 8-wave kernel stages a tile's page ids in LDS: at most PF8_MAXP pages
+    # per item (ctx > 64k tokens: the key range is split, never truncated)
+    max_part = PF8_MAXP if block_size == 64 and pf_wg_rows(G) == PF8_ROWS else None
     tiles = []
     for s in range(len(q_start_host) - 1):
         a, b = q_start_host[s], q_start_host[s + 1]
@@ -410,7 +414,8 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
             n = min(per, b - t)
             tiles.append((base + (t - a) + n, s, t, n))
     plan = PrefillPlan(*[[] for _ in range(10)])
-    split = block_size == 64 and ctx_lens_host is not None and PF_ROWS % G == 0
+    too_long = max_part is not None and any((end + 63) // 64 > max_part for end, _, _, _ in tiles)
+    split = block_size == 64 and PF_ROWS % G == 0 and (ctx_lens_host is not None or too_long)
     # sequences with the most work first; inside a sequence, longest tile first
     work = {}
     for end, s, _, n in tiles:
@@ -427,7 +432,12 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
     total = sum(pages)
     # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
     part = max(pages) if pages and len(tiles) * nkv >= target_wgs // 2 else max(4, -(-total * nkv // target_wgs))
+    if max_part is not None:
+        part = min(part, max_part)
     while sum(-(-p // part) for p in pages if p > part) > max_slots:
+        if max_part is not None and part * 2 > max_part:
+            raise ValueError(f"prefill plan needs more than {max_slots} split-KV slots at "
+                             f"{max_part} pages per item (context too long for the workspace)")
         part *= 2
     items = []
     slot = 0

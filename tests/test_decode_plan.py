@@ -52,3 +52,30 @@ def test_groups_break_on_partition_count_and_sequence():
     assert lead.tolist() == [0, 4] and nt.tolist() == [4, 2]
     lead, nt = A.decode_groups(ctx, np.arange(6), None, 4)
     assert nt.tolist() == [1] * 6
+
+
+def test_prefill_plan_caps_w8_items_at_lds_page_table(monkeypatch):
+    """with the 8-wave prefill kernel every work item spans at
+    most PF8_MAXP key pages (the kernel's LDS page table), whatever the block
+    table width; each tile's items tile its key range exactly once."""
+    monkeypatch.setenv("K8SRCA_PF_W8", "2")
+    for ctx, qlen, known in (([70_000, 500], [96, 40], True), ([66_000, 300], [66_000, 300], False)):
+        qs = [0]
+        for n in qlen:
+            qs.append(qs[-1] + n)
+        plan = A.plan_prefill(qs, 4, 64, list(ctx) if known else None, nkv=8)
+        spans = {}
+        for s, t, n, k0, k1, sl in zip(plan.seq, plan.tok0, plan.length, plan.kv0, plan.kv1, plan.slot):
+            assert k1 - k0 <= A.PF8_MAXP or k1 >= 1 << 30
+            spans.setdefault((s, t), []).append((k0, k1, sl))
+        for (s, t), sp in spans.items():
+            sp.sort()
+            base = ctx[s] - qlen[s]
+            end_pages = -(-(base + (t - qs[s]) + min(64, qs[s + 1] - t)) // 64)
+            if len(sp) > 1:
+                assert sp[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
+                assert sp[-1][1] >= min(end_pages, sp[-1][1])
+    # the 4-wave kernel has no page table: no cap without a split plan
+    monkeypatch.setenv("K8SRCA_PF_W8", "0")
+    plan = A.plan_prefill([0, 66_000], 4, 64, None, nkv=8)
+    assert plan.n_merge == 0

@@ -768,6 +768,50 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     torch.testing.assert_close(outs["3"].float(), outs["1"].float(), atol=1e-2, rtol=1e-2)
 
 
+@pytest.mark.parametrize("split", [False, True])
+def test_prefill_w8_long_context_block_table(split, monkeypatch):
+    """a block table wider than the 8-wave kernel's LDS page
+    table (bt_stride > 1024 pages, ctx > 64k tokens) must still run the kernel
+    the planner tiled for (256-row tiles), with every item's key range cut at
+    PF8_MAXP pages -- against the fp32 reference, both with a long cached
+    prefix (ctx_lens known: split-KV plan) and without one."""
+    _need_gpu()
+    torch.manual_seed(11)
+    monkeypatch.setenv("K8SRCA_PF_W8", "2")
+    BS, nq, nkv = 64, 8, 1
+    ctx = [70_000 if split else 66_000, 500]
+    qlen = [96, 40] if split else [66_000, 500]
+    if not split:
+        ctx = list(qlen)
+    NB = sum((c + BS - 1) // BS for c in ctx) + 4
+    kc, vc = _setup_cache(nkv, BS, NB, dev)
+    q = torch.randn(sum(qlen), (nq + 2 * nkv) * 128, device=dev).bfloat16()
+    scale = 1 / math.sqrt(128)
+    meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
+    assert meta.block_tables.shape[1] > A.PF8_MAXP
+    qs = meta.q_start_host
+    plan = A.plan_prefill(qs, nq // nkv, BS, list(ctx) if split else None, nkv=nkv)
+    assert max(b - a for a, b in zip(plan.kv0, plan.kv1) if b < (1 << 30)) <= A.PF8_MAXP
+    A.attach_plan(meta, plan, dev)
+    out = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
+    if split:
+        ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
+        torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    else:
+        # 66k-token causal prefill: check the last 256 rows of the long sequence
+        # (tiles past the first 1024 pages) and the short sequence, in fp32
+        rows = list(range(qlen[0] - 256, qlen[0])) + list(range(qlen[0], qlen[0] + qlen[1]))
+        K = kc[meta.block_tables[0, :(ctx[0] + 63) // 64].long(), 0].reshape(-1, 128)[:ctx[0]].float()
+        V = vc[meta.block_tables[0, :(ctx[0] + 63) // 64].long(), 0].transpose(1, 2).reshape(-1, 128)[:ctx[0]].float()
+        Q = q[qlen[0] - 256:qlen[0], :nq * 128].float().view(256, nq, 128)
+        S = torch.einsum("tgd,nd->gtn", Q, K) * scale
+        pos = torch.arange(ctx[0] - 256, ctx[0], device=dev)[:, None]
+        S = S.masked_fill(torch.arange(ctx[0], device=dev)[None, :] > pos, float("-inf"))
+        O = torch.einsum("gtn,nd->tgd", torch.softmax(S, -1), V).reshape(256, nq * 128)
+        torch.testing.assert_close(out[qlen[0] - 256:qlen[0]].float(), O, atol=2e-2, rtol=2e-2)
+        assert torch.isfinite(out[rows].float()).all()
+
+
 def test_sampling_top_p_and_tie_candidates_deterministic():
     """the top-p threshold comes from order-independent (fixed-point
     integer) mass sums and the candidate list from a fixed-order tie fill, so

@@ -164,6 +164,78 @@ def test_tp2_stalled_peer_fails_runs():
     assert all(failed and "timed out" in err for failed, err in res["late"]), res["late"]
 
 
+def _host_stall_worker(rank, world, port, out_dir):
+    """rank 0's host stalls between sending an eager step
+    and launching its own half, so the WORKER's collective is the one that
+    times out.  The worker must notice its own STATUS and stop executing (so
+    rank 0's next collective times out too) instead of skipping every later
+    wait while still publishing flags -- which would let rank 0 mix
+    unsynchronized partials into its outputs for good."""
+    import time
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    from k8s_llm_rca_amd.parallel.xgmi import CommFault, XgmiAllReduce
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0)
+    cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
+                       temperature=0.0, use_graphs=True)
+    model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")
+    eng = LLMEngine(cfg, pc, model=model)
+    if rank > 0:
+        eng.serve_worker()       # the healthy request
+        eng.serve_worker()       # the stalled ones: this rank's wait times out
+        torch.cuda.synchronize()
+        torch.save({"dead": eng.comm_dead, "status": pc.custom_ar.status()}, os.path.join(out_dir, "w.pt"))
+    else:
+        def run(n, tag):
+            done = {}
+            for i in range(n):
+                sid = eng.new_sequence()
+                toks = eng.tok.system_prefix("sys") + eng.tok.message("user", f"{tag} {i} " * 6) + \
+                    eng.tok.header("assistant")
+                eng.submit(sid, toks, None, 24, seed=3, on_done=lambda g, st, i=i: done.__setitem__(i, (g, st)))
+            t0 = time.time()
+            while len(done) < n and time.time() - t0 < 120:
+                time.sleep(0.05)
+            return done
+        eng.start()
+        ok = run(1, "healthy")
+        eng.stop()
+        eng.stop_workers()
+        eng._test_host_stall_s = 3.0  # 3x the workers' timeout, before rank 0 launches its half
+        eng.start()
+        bad = run(2, "stalled")
+        eng.stop()
+        eng.stop_workers()
+        res = {"ok": [g is not None and len(g) == 24 for g, _ in ok.values()],
+               "bad": [(g is None, st.get("error", "")) for g, st in bad.values()] if len(bad) == 2 else None,
+               "fault": isinstance(eng.error, CommFault), "status": pc.custom_ar.status()}
+        torch.save(res, os.path.join(out_dir, "stall.pt"))
+    torch.cuda.synchronize()
+    dist.barrier()
+    pc.custom_ar.close()
+    dist.destroy_process_group()
+
+
+def test_tp2_worker_timeout_stops_worker_and_fails_runs():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_host_stall_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        res = torch.load(os.path.join(d, "stall.pt"), weights_only=True)
+        wres = torch.load(os.path.join(d, "w.pt"), weights_only=True)
+    assert res["ok"] == [True]
+    assert wres["dead"] and wres["status"] == 1
+    assert res["fault"] and res["status"] == 1
+    assert res["bad"] is not None and all(failed for failed, _ in res["bad"]), res["bad"]
+
+
 def test_tp_sim_rank0_runs_real_kernels_with_standin_collectives():
     """bench --tp-sim: rank 0 of a TP=4 engine on one GPU (shard shapes, the
     native executor, HIP graphs, the xGMI kernels on a loopback communicator)

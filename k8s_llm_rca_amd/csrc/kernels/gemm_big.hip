@@ -4,308 +4,501 @@
 //   act[M][I] = silu(X . Wg^T) * (X . Wu^T),  W = [Wg; Wu] ([2I][K], gate rows first)
 // so the [M][2I] gate_up activation is never written nor re-read.
 //
-// Structure (cdna_hip_programming.md §5, "glds vs register staging" and
-// "Pipelining across barriers"):
-//   * 256 x 256 output tile per 512-thread workgroup (8 waves as 2 (M) x 4 (N),
-//     128 x 64 per wave: 8 x 4 accumulators of v_mfma_f32_16x16x32_bf16), one
-//     workgroup per CU (128 KB of LDS).
-//   * K in 32-deep chunks; chunk c = A[256][32] + B[256][32] (32 KB), staged by
-//     global_load_lds (16-byte LDS-DMA, lane-linear) into a 4-stage ring: two
-//     chunks are in flight while one is computed.  One __shared__ array, a
-//     counted `s_waitcnt vmcnt` and a raw s_barrier per chunk (never
-//     __syncthreads, whose fence would drain the DMAs in flight).
-//   * LDS image: 64-byte rows of 4 16-byte pieces, piece p of row n stored in
-//     slot p ^ g((n >> 2) & 3), g = {0, 2, 3, 1}.  Applied on the DMA SOURCE
-//     address (the LDS side is lane-linear) and on the fragment read; with the
-//     ds_read_b128 lane groups of MI355X_MICROARCH.md §LDS ({0-3,12-15,20-27},
-//     {4-11,16-19,28-31}, ...) every 16-lane group of a fragment read hits 16
-//     distinct 16-byte bank slots.
-//   * PIPE = 1: the fragments of chunk c+1 are read from LDS while chunk c's
-//     MFMAs issue (one register set per operand plus a second B set), so the
-//     barrier of chunk c+1 finds its operands already in registers; PIPE = 0 is
-//     the plain form (read after the barrier).  Both are kept for A/B.
-//   * Tile order: XCD-aware bijective remap of the workgroup id (each XCD's L2
-//     sees a contiguous range of tiles), then groups of 4 M tiles x all N tiles
-//     so the ~32 tiles an XCD runs at once share 4 X panels and 8 W panels.
+// Structure: the 256 x 256 x 64 eight-phase schedule of
+// cdna_hip_programming.md §5 ("The 256² 8-phase template", T1-T5), built
+// for this engine's operand layouts and epilogues:
+//   * one 512-thread workgroup per CU, 256 x 256 output tile, K in 64-deep
+//     tiles.  LDS = 2 buffers x {X rows 0-127, X rows 128-255, W rows 0-127,
+//     W rows 128-255} half-tiles of 128 x 64 bf16 (16 KB each) = 128 KB, one
+//     __shared__ array.
+//   * a K-tile is four phases, one per 128 x 128 C quadrant (q = (X half,
+//     W half) = (0,0) (0,1) (1,1) (1,0)); in every phase each of the 8 waves
+//     (2 along M x 4 along N inside the quadrant) issues 16
+//     v_mfma_f32_16x16x32_bf16 for its 64 x 32 piece of the quadrant.  The
+//     fragments of a quadrant are read in the phase's load segment (X half: 8
+//     ds_read_b128, W half: 4), so over a K-tile a wave reads every fragment
+//     once (24 reads): the X half of the previous quadrant and the W halves
+//     stay in registers.
+//   * ping-pong: waves 4-7 (the second wave of every SIMD) run one barrier
+//     behind waves 0-3, so on each SIMD one wave issues its MFMA cluster while
+//     its partner reads fragments and issues DMAs (MI355X_MICROARCH.md "Two
+//     waves per SIMD"); the MFMA cluster sits between s_setprio(1)/(0) (T5).
+//   * every phase stages one half-tile by 16-byte LDS-DMA (global_load_lds,
+//     2 per thread): W half 1 / X half 1 of tile u+1 in phases 1 / 2, X half 0
+//     / W half 0 of tile u+2 in phases 3 / 4 -- each at least two phases after
+//     its buffer's last fragment read (the WAR rule, with the stagger), and a
+//     counted `s_waitcnt vmcnt(8)` (four half-tiles in flight, never 0 in the
+//     loop) in the load segment of the phase before the first read (the RAW
+//     rule: wait, then a barrier both groups pass, then read).  Raw s_barrier
+//     only: __syncthreads' fence would drain the DMAs in flight.
+//   * LDS image: 128-byte rows of 8 16-byte chunks, chunk c of row r stored at
+//     c ^ ((r >> 1) & 7).  The swizzle is applied on the DMA SOURCE address
+//     (the LDS side is lane-linear, rule 21) and on the fragment read; every
+//     16-lane group of a ds_read_b128 then hits 16 distinct 16-byte bank slots.
+//   * the MFMA computes Y^T (A operand = W fragment, B = X fragment), so a lane
+//     holds 4 consecutive output COLUMNS of one row; W rows are staged in a
+//     permuted order so that the lane's two N fragments are columns 8g .. 8g+7:
+//     the epilogue stores 16 contiguous bytes per lane (8 for SwiGLU), no LDS.
+//     In the SwiGLU form the two fragments are the gate and up rows of the
+//     same 4 act columns.
+//   * tile order: XCD-aware bijective remap of the workgroup id (each XCD's L2
+//     sees a contiguous range of tiles), then groups of GM M tiles x all N tiles
+//     (the ~32 tiles an XCD runs at once share 4 X panels and 8 W panels).
+//   * split tail (stream-K's role): when the tile count leaves a partial last
+//     wave (T = 256 f + r, r < 256), the r tiles of that wave run as r x S work
+//     units of K / S each (S <= 4, r S <= 256), so the last wave takes 1/S of a
+//     tile's time instead of a whole one.  A unit writes its fp32 partial tile
+//     (256 KB, lane-contiguous) to a workspace; the last of a tile's S units to
+//     arrive (agent-scope release -> ticket add; acquire -> read the other S-1
+//     partials, cdna_hip_programming.md "Projection GEMM at M = 256" item 2)
+//     sums them in slice order -- deterministic -- and runs the normal
+//     epilogue (SwiGLU included); it resets the ticket for the next launch.
+//     The S units of a tile are consecutive after an XCD remap of the units
+//     (same XCD, same L2 under round-robin placement; speed only).
+//   * split-K (MODE 0, grids of less than one wave: M <= 2048 at N = 4096):
+//     `splits` workgroups per tile, consecutive after the remap (one XCD), each
+//     over K / splits, writing fp32 partials [splits][M][N] (32 contiguous bytes
+//     per lane) that the consumer reduces: the following residual add + RMSNorm
+//     or RoPE / KV write in the layer executor (k8s_splitk_addnorm /
+//     k8s_splitk_rope_kv, as for the other split-K kernels), else the reduce
+//     kernel below.
 //
 // Rows past M are clamped on load (an L2 hit) and never stored.
 // Reference parity: replaces the hipBLASLt call on the prefill path of
 // models/llama.py (the reference's GPT-4 prompt processing of the whole thread
 // history, /root/reference/common/openai_generic_assistant.py:45-51).
+#include <type_traits>
+
 #include "common.h"
 
 namespace k8s {
 namespace big {
 
-constexpr int BM = 256, BN = 256, BK = 32, NB = 4;
-constexpr int STAGE = (BM + BN) * BK;  // bf16 elements per stage (32 KB)
-constexpr int LPC = STAGE * 2 / (512 * 16);  // DMAs per thread per chunk (4)
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int HALF_B = 128 * BK * 2;  // bytes per half-tile (16 KB)
+constexpr int BUF_B = 4 * HALF_B;     // one K-tile (64 KB)
+constexpr int OX0 = 0, OX1 = HALF_B, OW0 = 2 * HALF_B, OW1 = 3 * HALF_B;
 constexpr int GM = 4;  // M tiles per tile group
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 
-__device__ __forceinline__ void glds16(const uint16_t* src, uint16_t* lds_dst) {
+__device__ __forceinline__ void glds16(const uint16_t* src, unsigned char* lds_dst) {
   __builtin_amdgcn_global_load_lds(src, (lds_void_t*)lds_dst, 16, 0, 0);
 }
 
-// slot XOR of a 64-byte row n: g((n >> 2) & 3), g = {0, 2, 3, 1}
-__device__ __forceinline__ int gx(int q) { return (0x78 >> (2 * q)) & 3; }
-
 __device__ __forceinline__ float silu(float g) { return g / (1.f + __expf(-g)); }
 
+__device__ __forceinline__ void bar() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <int N>
+using ic = std::integral_constant<int, N>;
+
 // MODE 0: plain (N output columns = W rows); MODE 1: SwiGLU (N = I output
-// columns, W has 2I rows).  In MODE 1 an output tile covers 128 act columns
-// j0 .. j0+127: wave column wc's 64 B rows are gate rows j0 + 32 wc + [0, 32)
-// (fragments 0, 1) and the matching up rows (fragments 2, 3), so fragment f and
-// f + 2 of one lane hold gate and up of the same (row, column).
-template <int MODE, int PIPE>
-__global__ void __launch_bounds__(512) gemm_big_kernel(const uint16_t* __restrict__ x, int ldx,
-                                                       const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
-                                                       int ldy, int M, int N, int K, int n_mt, int n_nt) {
-  __shared__ __attribute__((aligned(16))) uint16_t sm[NB * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+// act columns, W has 2I rows, I = N).  VAR bit 0: ping-pong stagger of waves
+// 4-7; bit 1: s_setprio(1) around the MFMA clusters (1 = the default).
+template <int MODE, int VAR>
+__global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __restrict__ x, int ldx,
+                                                          const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
+                                                          int ldy, int M, int N, int K, int n_mt, int n_nt, int splits,
+                                                          float* __restrict__ part, int tail_tiles, int tail_split,
+                                                          float* __restrict__ tws, int* __restrict__ tick) {
+  __shared__ __attribute__((aligned(1024))) unsigned char sm[2 * BUF_B];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wv >> 2, wc = wv & 3;
 
   // ---- tile of this workgroup: XCD-contiguous remap, then grouped order
-  const int nwg = n_mt * n_nt;
-  int t;
+  int tm, tn, slice, nsl = splits, tt = -1;  // tt: tail tile index (split tail), else -1
   {
-    const int b = blockIdx.x, xcd = b & 7, q = nwg >> 3, r = nwg & 7;
-    t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    // bijective XCD remap of id b within [0, n): blocks b, b+8, ... (one XCD under
+    // round-robin placement) get a contiguous id range
+    auto remap = [](int b, int n) {
+      const int xcd = b & 7, q = n >> 3, r = n & 7;
+      return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    };
+    const int T = n_mt * n_nt, F = T - tail_tiles, b = blockIdx.x;
+    int t;
+    if (splits > 1) {  // uniform split-K: units of one tile consecutive
+      const int t0 = remap(b, T * splits);
+      slice = t0 % splits;
+      t = t0 / splits;
+    } else if (b < F) {
+      t = remap(b, F);
+      slice = 0;
+      nsl = 1;
+    } else {
+      const int u = remap(b - F, tail_tiles * tail_split);
+      tt = u / tail_split;
+      slice = u % tail_split;
+      nsl = tail_split;
+      t = F + tt;
+    }
+    const int gsz = GM * n_nt, gid = t / gsz, first_m = gid * GM;
+    const int gm = min(n_mt - first_m, GM);
+    tm = first_m + (t % gsz) % gm;
+    tn = (t % gsz) / gm;
   }
-  const int gsz = GM * n_nt, gid = t / gsz, first_m = gid * GM;
-  const int gm = min(n_mt - first_m, GM);
-  const int tm = first_m + (t % gsz) % gm, tn = (t % gsz) / gm;
   const int m0 = tm * BM;
 
-  // ---- DMA sources: instruction i of this wave stages combined rows
-  // [16 ci, 16 ci + 16) of the [A; B] stage image, ci = 8 i + wv
-  const int piece = (lane & 3) ^ gx(lane >> 4);
-  const uint16_t* src[LPC];
+  // ---- DMA sources: instruction i of this wave stages half-tile rows
+  // 16 wv + 8 i + (lane >> 3), lane's LDS chunk (lane & 7) <- source chunk
+  // (lane & 7) ^ ((row >> 1) & 7)
+  const uint16_t* xs[2][2];
+  const uint16_t* wsrc[2][2];
 #pragma unroll
-  for (int i = 0; i < LPC; ++i) {
-    const int ci = 8 * i + wv;
-    const int row = 16 * ci + (lane >> 2);
-    if (row < BM) {
-      src[i] = x + (size_t)min(m0 + row, M - 1) * ldx + 8 * piece;
-    } else {
-      const int rb = row - BM;
-      int gn;
-      if (MODE == 0) {
-        gn = tn * BN + rb;
-      } else {
-        const int f = (rb >> 4) & 3;
-        gn = (f >= 2 ? N : 0) + tn * 128 + (rb >> 6) * 32 + (f & 1) * 16 + (rb & 15);
-      }
-      src[i] = w + (size_t)gn * K + 8 * piece;
+  for (int i = 0; i < 2; ++i) {
+    const int R = 16 * wv + 8 * i + (lane >> 3);
+    const int lch = (lane & 7) ^ ((R >> 1) & 7);
+    const int slab = R >> 5, rho = R & 31;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      xs[h][i] = x + (size_t)min(m0 + 128 * h + R, M - 1) * ldx + 8 * lch;
+      int n;
+      if (MODE == 0)  // lane group g of the fragment pair <- columns 8g .. 8g+7
+        n = tn * BN + 128 * h + 32 * slab + 8 * ((rho >> 2) & 3) + 4 * (rho >> 4) + (rho & 3);
+      else  // fragment 0: gate rows, fragment 1: the up rows of the same act columns
+        n = (rho >> 4 ? N : 0) + tn * 128 + 64 * h + 16 * slab + (rho & 15);
+      wsrc[h][i] = w + (size_t)n * K + 8 * lch;
     }
   }
-  auto issue = [&](int stage, int c) {
-    uint16_t* st = sm + stage * STAGE;
+  const int nt = K / BK / nsl, kt0 = slice * nt;  // this workgroup's K tiles
+  auto issue = [&](const uint16_t* const* src, int lds_off, int kt) {
 #pragma unroll
-    for (int i = 0; i < LPC; ++i) glds16(src[i] + c * BK, st + (8 * i + wv) * 512);
+    for (int i = 0; i < 2; ++i) glds16(src[i] + (kt0 + kt) * BK, sm + lds_off + (2 * wv + i) * 1024);
   };
 
-  // ---- fragment reads: lane's row (r = lane & 15) and swizzled piece
-  const int foff = (lane & 15) * BK + 8 * ((lane >> 4) ^ gx((lane >> 2) & 3));
-  const int a_off = (wr * 128) * BK + foff;
-  const int b_off = (BM + wc * 64) * BK + foff;
+  // ---- fragment reads: row (lane & 15) of a 16-row block, chunk (lane >> 4) + 4 ks
+  const int sw = (lane >> 1) & 7;
+  const int f0 = (lane & 15) * 128 + 16 * ((lane >> 4) ^ sw);
+  const int f1 = f0 ^ 64;
+  const int xoff = 64 * wr * 128, woff = 32 * wc * 128;
 
-  f32x4 acc[8][4];
+  f32x4 acc[4][4][2];
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+  for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[q][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 xf[4][2], wf0[2][2], wf1[2][2];
 
-  const int nch = K / BK;
-  // prologue: chunks 0 .. NB-2 in flight (clamped: short K re-reads its last chunk)
-#pragma unroll
-  for (int c = 0; c < NB - 1; ++c) issue(c, min(c, nch - 1));
+  // prologue: tile 0 whole, tile 1's X half 0 and W half 0 (the main loop's issue order)
+  issue(xs[0], OX0, 0);
+  issue(wsrc[0], OW0, 0);
+  issue(wsrc[1], OW1, 0);
+  issue(xs[1], OX1, 0);
+  issue(xs[0], BUF_B + OX0, 1);
+  issue(wsrc[0], BUF_B + OW0, 1);
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // this wave's part of X0h(0), W0h(0)
+  bar();
+  if ((VAR & 1) && wr == 1) bar();  // waves 4-7 run one barrier behind
 
-  if (PIPE == 0) {
-    // iteration c: wait for chunk c, barrier, refill chunk c-1's stage, compute c
-    for (int c0 = 0; c0 < nch; c0 += NB) {
+  auto phase = [&](auto PHc, auto BUFc, int u) {
+    constexpr int PH = decltype(PHc)::value, BUF = decltype(BUFc)::value;
+    constexpr int B0 = BUF * BUF_B, B1 = (BUF ^ 1) * BUF_B;
+    // ---- load segment: this quadrant's new fragments, one half-tile of DMAs
+    if constexpr (PH == 1) {
 #pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        const int c = c0 + u;
-        // this wave's DMAs of chunk c are done when only the NB-2 later chunks' remain
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 2) * LPC) : "memory");
-        __builtin_amdgcn_s_barrier();  // all of chunk c landed; all waves done reading chunk c-1
-        asm volatile("" ::: "memory");
-        issue((u + NB - 1) % NB, min(c + NB - 1, nch - 1));  // refill chunk c-1's stage
-        if (c < nch) {
-          const uint16_t* st = sm + u * STAGE;
-          bf16x8 fb[4];
-#pragma unroll
-          for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(st + b_off + 16 * j * BK);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) {
-            const bf16x8 fa = *reinterpret_cast<const bf16x8*>(st + a_off + 16 * i * BK);
-#pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa, fb[j], acc[i][j], 0, 0, 0);
-          }
-        }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      for (int j = 0; j < 2; ++j) {
+        wf0[j][0] = *reinterpret_cast<const bf16x8*>(sm + B0 + OW0 + woff + 16 * j * 128 + f0);
+        wf0[j][1] = *reinterpret_cast<const bf16x8*>(sm + B0 + OW0 + woff + 16 * j * 128 + f1);
       }
-    }
-  } else if (PIPE == 2) {
-    // two explicit fragment sets: chunk c's MFMAs run on set c & 1 while chunk
-    // c+1's fragments stream into the other set, interleaved by
-    // sched_group_barrier (hipcc otherwise sinks every ds_read below the MFMAs,
-    // so each barrier exposed the full LDS latency: PIPE 1 ran at the PIPE 0 rate)
-    issue(NB - 1, min(NB - 1, nch - 1));
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 1) * LPC) : "memory");  // chunk 0 (this wave's part)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    bf16x8 fa[2][8], fb[2][4];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[0][j] = *reinterpret_cast<const bf16x8*>(sm + b_off + 16 * j * BK);
-#pragma unroll
-    for (int i = 0; i < 8; ++i) fa[0][i] = *reinterpret_cast<const bf16x8*>(sm + a_off + 16 * i * BK);
-    for (int c0 = 0; c0 < nch; c0 += NB) {
-#pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        const int c = c0 + u, cur = u & 1, nxt = cur ^ 1;
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NB - 2) * LPC) : "memory");
-        __builtin_amdgcn_s_barrier();  // all of chunk c+1 landed; every wave holds chunk c in registers
-        asm volatile("" ::: "memory");
-        if (c < nch) {
-          issue(u, min(c + NB, nch - 1));  // chunk c's stage is free: refill it with chunk c + NB
-          const uint16_t* nx = sm + ((u + 1) % NB) * STAGE;  // chunk c+1 (a clamped re-read past the end)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) fb[nxt][j] = *reinterpret_cast<const bf16x8*>(nx + b_off + 16 * j * BK);
-#pragma unroll
-          for (int i = 0; i < 8; ++i) fa[nxt][i] = *reinterpret_cast<const bf16x8*>(nx + a_off + 16 * i * BK);
-#pragma unroll
-          for (int i = 0; i < 8; ++i)
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[cur][i], fb[cur][j], acc[i][j], 0, 0, 0);
-          // issue order: the 4 DMAs between the first MFMAs, then one fragment
-          // read per two MFMAs, then the remaining MFMAs
-#pragma unroll
-          for (int k = 0; k < LPC; ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x020, 1, 0);  // VMEM read (LDS-DMA)
-          }
-#pragma unroll
-          for (int k = 0; k < 12; ++k) {
-            __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);  // MFMA
-            __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
-          }
-          __builtin_amdgcn_sched_group_barrier(0x008, 32 - LPC - 24, 0);
-        } else {
-          issue(u, nch - 1);
-        }
+      for (int i = 0; i < 4; ++i) {
+        xf[i][0] = *reinterpret_cast<const bf16x8*>(sm + B0 + OX0 + xoff + 16 * i * 128 + f0);
+        xf[i][1] = *reinterpret_cast<const bf16x8*>(sm + B0 + OX0 + xoff + 16 * i * 128 + f1);
       }
+      issue(wsrc[1], B1 + OW1, min(u + 1, nt - 1));
+    } else if constexpr (PH == 2) {
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        wf1[j][0] = *reinterpret_cast<const bf16x8*>(sm + B0 + OW1 + woff + 16 * j * 128 + f0);
+        wf1[j][1] = *reinterpret_cast<const bf16x8*>(sm + B0 + OW1 + woff + 16 * j * 128 + f1);
+      }
+      issue(xs[1], B1 + OX1, min(u + 1, nt - 1));
+    } else if constexpr (PH == 3) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        xf[i][0] = *reinterpret_cast<const bf16x8*>(sm + B0 + OX1 + xoff + 16 * i * 128 + f0);
+        xf[i][1] = *reinterpret_cast<const bf16x8*>(sm + B0 + OX1 + xoff + 16 * i * 128 + f1);
+      }
+      issue(xs[0], B0 + OX0, min(u + 2, nt - 1));
+    } else {
+      issue(wsrc[0], B0 + OW0, min(u + 2, nt - 1));
     }
-  } else {
-    // chunk c's fragments are read during chunk c-1's MFMAs.  Stage of chunk c
-    // is refilled (chunk c+NB) right after iteration c's barrier: every wave
-    // finished reading it (lgkmcnt(0) before that barrier).  At the top of
-    // iteration c chunks c+1 .. c+NB-1 are in flight, so the last stage is
-    // filled in the prologue too.
-    issue(NB - 1, min(NB - 1, nch - 1));
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NB - 1) * LPC) : "memory");  // chunk 0 (this wave's part)
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-    bf16x8 fa[8], fb[4];
+    // RAW: the half-tile the next phase reads first (X0h/W0h of tile u+1 in
+    // phase 4, W1h(u) in phase 1, X1h(u) in phase 2) has landed once at most
+    // the four later half-tiles of this wave are in flight
+    if constexpr (PH != 3) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    bar();
+    // ---- compute segment: quadrant (X half, W half) = (0,0) (0,1) (1,1) (1,0)
+    constexpr int Q = PH - 1;
+    if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int j = 0; j < 4; ++j) fb[j] = *reinterpret_cast<const bf16x8*>(sm + b_off + 16 * j * BK);
+    for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int i = 0; i < 8; ++i) fa[i] = *reinterpret_cast<const bf16x8*>(sm + a_off + 16 * i * BK);
-    for (int c0 = 0; c0 < nch; c0 += NB) {
+      for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int u = 0; u < NB; ++u) {
-        const int c = c0 + u;
-        // chunk c's fragments are in registers; chunk c+1 has landed (this wave's part)
-        asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"((NB - 2) * LPC) : "memory");
-        __builtin_amdgcn_s_barrier();  // all of chunk c+1 landed; every wave holds chunk c in registers
-        asm volatile("" ::: "memory");
-        issue(u, min(c + NB, nch - 1));  // chunk c's stage is free: refill it with chunk c + NB
-        if (c < nch) {
-          const uint16_t* nx = sm + ((u + 1) % NB) * STAGE;  // chunk c+1 (a clamped re-read past the end)
-          bf16x8 fbn[4];
+        for (int j = 0; j < 2; ++j) {
+          const bf16x8 wfr = (PH == 1 || PH == 4) ? wf0[j][ks] : wf1[j][ks];
+          acc[Q][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wfr, xf[i][ks], acc[Q][i][j], 0, 0, 0);
+        }
+    if constexpr (VAR & 2) __builtin_amdgcn_s_setprio(0);
+    bar();
+  };
+
+  for (int u = 0; u < nt; u += 2) {
+    phase(ic<1>{}, ic<0>{}, u);
+    phase(ic<2>{}, ic<0>{}, u);
+    phase(ic<3>{}, ic<0>{}, u);
+    phase(ic<4>{}, ic<0>{}, u);
+    phase(ic<1>{}, ic<1>{}, u + 1);
+    phase(ic<2>{}, ic<1>{}, u + 1);
+    phase(ic<3>{}, ic<1>{}, u + 1);
+    phase(ic<4>{}, ic<1>{}, u + 1);
+  }
+  if ((VAR & 1) && wr == 0) bar();                          // equal barrier counts in both groups
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
+
+  // ---- epilogue: acc[q][i][j][v] = Y[row m][col]: m = m0 + 128 qx + 64 wr + 16 i + (lane & 15),
+  // col (MODE 0) = tn*256 + 128 qw + 32 wc + 8 g + 4 j + v, g = lane >> 4
+  const int g = lane >> 4;
+  if (tt >= 0) {
+    // split tail: publish this unit's partial; the last of the tile's units sums them
+    const size_t lane_off = (size_t)(wv * 16 * 64 + lane) * 8;  // + (Q * 4 + i) * 64 * 8
+    float* mine = tws + ((size_t)tt * nsl + slice) * (BM * BN) + lane_off;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) fbn[j] = *reinterpret_cast<const bf16x8*>(nx + b_off + 16 * j * BK);
+    for (int Q = 0; Q < 4; ++Q)
 #pragma unroll
-          for (int i = 0; i < 8; ++i) {
+      for (int i = 0; i < 4; ++i) {
+        float* o = mine + (Q * 4 + i) * 64 * 8;
+        *reinterpret_cast<f32x4*>(o) = acc[Q][i][0];
+        *reinterpret_cast<f32x4*>(o + 4) = acc[Q][i][1];
+      }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    int* flag = reinterpret_cast<int*>(sm);
+    if (tid == 0) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const int old = __hip_atomic_fetch_add(tick + tt, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == nsl - 1;
+      if (last) {
+        __hip_atomic_store(tick + tt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      flag[0] = last;
+    }
+    __syncthreads();
+    if (!flag[0]) return;
+    // every partial (this unit's too, from memory: one uniform path) summed in
+    // slice order; 16 independent 32-byte loads in flight per slice and half
+    // (a per-slice "register or load" branch would wait for each load alone)
+    const float* base = tws + (size_t)tt * nsl * (BM * BN) + lane_off;
 #pragma unroll
-            for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-            fa[i] = *reinterpret_cast<const bf16x8*>(nx + a_off + 16 * i * BK);
+    for (int hq = 0; hq < 2; ++hq) {
+#pragma unroll
+      for (int Q = 2 * hq; Q < 2 * hq + 2; ++Q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) acc[Q][i][0] = acc[Q][i][1] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int sl = 0; sl < nsl; ++sl) {
+        f32x4 t[2][4][2];
+#pragma unroll
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            const float* p = base + (size_t)sl * (BM * BN) + ((2 * hq + q) * 4 + i) * 64 * 8;
+            t[q][i][0] = *reinterpret_cast<const f32x4*>(p);
+            t[q][i][1] = *reinterpret_cast<const f32x4*>(p + 4);
           }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) fb[j] = fbn[j];
-        }
+        for (int q = 0; q < 2; ++q)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) {
+            acc[2 * hq + q][i][0] += t[q][i][0];
+            acc[2 * hq + q][i][1] += t[q][i][1];
+          }
       }
     }
   }
-  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
-
-  // ---- epilogue: acc[i][j][v] = C[row 128 wr + 16 i + 4 (lane >> 4) + v][col 64 wc + 16 j + (lane & 15)]
-  const int rbase = m0 + wr * 128 + 4 * (lane >> 4);
-  if (MODE == 0) {
-    uint16_t* yb = y + tn * BN + wc * 64 + (lane & 15);
+  if (MODE == 0 && part != nullptr) {  // split-K: fp32 partials [splits][M][N]
+    float* pb = part + (size_t)slice * M * N;
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+    for (int Q = 0; Q < 4; ++Q) {
+      const int qx = (Q == 2 || Q == 3) ? 1 : 0, qw = (Q == 1 || Q == 2) ? 1 : 0;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = rbase + 16 * i + v;
-        if (m < M) {
-#pragma unroll
-          for (int j = 0; j < 4; ++j) yb[(size_t)m * ldy + 16 * j] = f2bf(acc[i][j][v]);
-        }
+      for (int i = 0; i < 4; ++i) {
+        const int m = m0 + 128 * qx + 64 * wr + 16 * i + (lane & 15);
+        if (m >= M) continue;
+        float* o = pb + (size_t)m * N + tn * BN + 128 * qw + 32 * wc + 8 * g;
+        *reinterpret_cast<f32x4*>(o) = acc[Q][i][0];
+        *reinterpret_cast<f32x4*>(o + 4) = acc[Q][i][1];
       }
-  } else {
-    uint16_t* yb = y + tn * 128 + wc * 32 + (lane & 15);
+    }
+    return;
+  }
 #pragma unroll
-    for (int i = 0; i < 8; ++i)
+  for (int Q = 0; Q < 4; ++Q) {
+    const int qx = (Q == 2 || Q == 3) ? 1 : 0, qw = (Q == 1 || Q == 2) ? 1 : 0;
 #pragma unroll
-      for (int v = 0; v < 4; ++v) {
-        const int m = rbase + 16 * i + v;
-        if (m < M) {
+    for (int i = 0; i < 4; ++i) {
+      const int m = m0 + 128 * qx + 64 * wr + 16 * i + (lane & 15);
+      if (m >= M) continue;
+      if (MODE == 0) {
+        u16x8 o;
 #pragma unroll
-          for (int j = 0; j < 2; ++j) {
-            // the unfused path's rounding: gate and up rounded to bf16 first (silu_mul_kernel)
-            const float g = bf2f(f2bf(acc[i][j][v])), u = bf2f(f2bf(acc[i][j + 2][v]));
-            yb[(size_t)m * ldy + 16 * j] = f2bf(silu(g) * u);
-          }
+        for (int v = 0; v < 4; ++v) {
+          o[v] = f2bf(acc[Q][i][0][v]);
+          o[4 + v] = f2bf(acc[Q][i][1][v]);
         }
+        *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + tn * BN + 128 * qw + 32 * wc + 8 * g) = o;
+      } else {
+        u16x4 o;
+#pragma unroll
+        for (int v = 0; v < 4; ++v) {
+          // the unfused path's rounding: gate and up rounded to bf16 first (silu_mul_kernel)
+          const float gt = bf2f(f2bf(acc[Q][i][0][v])), up = bf2f(f2bf(acc[Q][i][1][v]));
+          o[v] = f2bf(silu(gt) * up);
+        }
+        *reinterpret_cast<u16x4*>(y + (size_t)m * ldy + tn * 128 + 64 * qw + 16 * wc + 4 * g) = o;
       }
+    }
   }
 }
 
-template <int MODE, int PIPE>
-static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, hipStream_t s) {
+// Y[m][n] = bf16(sum_s part[s][m][n]) (slice order); 8 outputs per thread.
+__global__ void __launch_bounds__(256) big_reduce_kernel(const float* __restrict__ part, int splits,
+                                                         uint16_t* __restrict__ y, int ldy, int M, int N) {
+  const long idx = ((long)blockIdx.x * 256 + threadIdx.x) * 8;
+  if (idx >= (long)M * N) return;
+  const int m = (int)(idx / N), n = (int)(idx % N);
+  const size_t MN = (size_t)M * N;
+  f32x4 a0 = *reinterpret_cast<const f32x4*>(part + idx);
+  f32x4 a1 = *reinterpret_cast<const f32x4*>(part + idx + 4);
+  for (int s = 1; s < splits; ++s) {
+    a0 += *reinterpret_cast<const f32x4*>(part + s * MN + idx);
+    a1 += *reinterpret_cast<const f32x4*>(part + s * MN + idx + 4);
+  }
+  u16x8 o;
+#pragma unroll
+  for (int v = 0; v < 4; ++v) {
+    o[v] = f2bf(a0[v]);
+    o[v + 4] = f2bf(a1[v]);
+  }
+  *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + n) = o;
+}
+
+// Split-tail workspace (per device, set once by the host: k8s_gemm_big_set_ws):
+// 256 partial tiles of 256 KB + 256 tickets, zeroed at allocation.  One GEMM at
+// a time per workspace: the engine issues every projection on one stream.
+constexpr int kTailUnits = 256;
+constexpr size_t kTailWsBytes = (size_t)kTailUnits * BM * BN * 4 + kTailUnits * 4;
+static void* g_tail_ws[16] = {};
+
+// (tail tiles r, split S) for T tiles of nt K-tiles on 256 CUs: the last partial
+// wave's r tiles in r x S units (S in {4, 2}: r S <= 256, nt % (2 S) == 0, >= 8 K-tiles each).
+static void tail_plan(int T, int nt, int& r, int& S) {
+  r = T % 256;
+  S = 1;
+  if (r == 0) return;
+  for (int c : {4, 2})
+    if (r * c <= kTailUnits && nt % (2 * c) == 0 && nt / c >= 8) {
+      S = c;
+      break;
+    }
+  if (S == 1) r = 0;
+}
+
+template <int MODE, int VAR>
+static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int splits,
+                  float* part, hipStream_t s) {
   const int n_mt = (M + BM - 1) / BM, n_nt = MODE == 0 ? N / BN : N / 128;
-  hipLaunchKernelGGL((gemm_big_kernel<MODE, PIPE>), dim3(n_mt * n_nt), dim3(512), 0, s, (const uint16_t*)x, ldx,
-                     (const uint16_t*)w, (uint16_t*)y, ldy, M, N, K, n_mt, n_nt);
+  const int T = n_mt * n_nt;
+  int tr = 0, ts = 1;
+  float* tws = nullptr;
+  int* tick = nullptr;
+  if (splits == 1) {
+    int dev = 0;
+    if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16 && g_tail_ws[dev]) {
+      tail_plan(T, K / BK, tr, ts);
+      tws = (float*)g_tail_ws[dev];
+      tick = (int*)((char*)g_tail_ws[dev] + (size_t)kTailUnits * BM * BN * 4);
+    }
+  }
+  const int grid = splits > 1 ? T * splits : T - tr + tr * ts;
+  hipLaunchKernelGGL((gemm_big_kernel<MODE, VAR>), dim3(grid), dim3(512), 0, s, (const uint16_t*)x, ldx,
+                     (const uint16_t*)w, (uint16_t*)y, ldy, M, N, K, n_mt, n_nt, splits, part, tr, ts, tws, tick);
   return (int)hipGetLastError();
 }
 
 }  // namespace big
 }  // namespace k8s
 
-// mode 0: y[M][N] = x . w^T (w [N][K], N % 256 == 0);
-// mode 1: y[M][N] = silu(x . w[0:N]^T) * (x . w[N:2N]^T) (w [2N][K], N % 128 == 0).
-// pipe: 0 plain loop, 1 fragment prefetch across the barrier, 2 the same with two explicit
-// fragment sets and a forced read / MFMA interleave.
-// K % 32 == 0, ldx % 8 == 0, 16-byte aligned x / w; y row stride ldy >= N.
-K8S_API int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode,
-                         int pipe, hipStream_t s) {
+static int big_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode,
+                      int var, int splits, float* part, bool reduce, hipStream_t s) {
   using namespace k8s::big;
   if (M <= 0) return 0;
-  if (K % BK || K < BK || ldx % 8 || ldx < K || ldy < N || N <= 0 || (mode == 0 && N % BN) ||
-      (mode == 1 && N % 128) || (mode != 0 && mode != 1) ||
-      ((uintptr_t)x % 16) || ((uintptr_t)w % 16))
+  if (splits < 1 || K % (2 * BK * splits) || K < 2 * BK || ldx % 8 || ldx < K || ldy < N || N <= 0 ||
+      (mode == 0 && N % BN) || (mode == 1 && N % 128) || (mode != 0 && mode != 1) || ((uintptr_t)x % 16) ||
+      ((uintptr_t)w % 16) || (mode == 0 && (ldy % 8 || (uintptr_t)y % 16)) ||
+      (mode == 1 && (ldy % 4 || (uintptr_t)y % 8)) || (splits > 1 && (mode != 0 || part == nullptr)))
     return (int)hipErrorInvalidValue;
-  if (pipe < 0 || pipe > 2) return (int)hipErrorInvalidValue;
+  if (var < 0 || var > 3) return (int)hipErrorInvalidValue;
+  float* pp = splits > 1 ? part : nullptr;
+  int rc;
   if (mode == 0) {
-    if (pipe == 2) return launch<0, 2>(x, ldx, w, y, ldy, M, N, K, s);
-    return pipe ? launch<0, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<0, 0>(x, ldx, w, y, ldy, M, N, K, s);
+    switch (var) {
+      case 0: rc = launch<0, 0>(x, ldx, w, y, ldy, M, N, K, splits, pp, s); break;
+      case 1: rc = launch<0, 1>(x, ldx, w, y, ldy, M, N, K, splits, pp, s); break;
+      case 2: rc = launch<0, 2>(x, ldx, w, y, ldy, M, N, K, splits, pp, s); break;
+      default: rc = launch<0, 3>(x, ldx, w, y, ldy, M, N, K, splits, pp, s); break;
+    }
+  } else {
+    rc = var == 3 ? launch<1, 3>(x, ldx, w, y, ldy, M, N, K, 1, nullptr, s)
+                  : launch<1, 1>(x, ldx, w, y, ldy, M, N, K, 1, nullptr, s);
   }
-  // the SwiGLU form of pipe 2 spills 24 VGPRs inside the loop (2 x 48 fragment
-  // registers + the gate/up epilogue): 978 vs 1204 TFLOP/s at M = 4096
-  // (profiles/r3/gemm_big/ab_v2_pipe2.jsonl) -- it runs the pipe-1 loop
-  return pipe ? launch<1, 1>(x, ldx, w, y, ldy, M, N, K, s) : launch<1, 0>(x, ldx, w, y, ldy, M, N, K, s);
+  if (rc || splits == 1 || !reduce) return rc;
+  const long blocks = ((long)M * N / 8 + 255) / 256;
+  hipLaunchKernelGGL(big_reduce_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const float*)part, splits,
+                     (uint16_t*)y, ldy, M, N);
+  return (int)hipGetLastError();
+}
+
+// Split-tail workspace of the calling thread's current device: `ws` (device
+// memory of k8s_gemm_big_ws_bytes() bytes, ZEROED) or nullptr to disable.
+K8S_API long k8s_gemm_big_ws_bytes() { return (long)k8s::big::kTailWsBytes; }
+K8S_API int k8s_gemm_big_set_ws(void* ws) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return (int)hipErrorInvalidValue;
+  k8s::big::g_tail_ws[dev] = ws;
+  return 0;
+}
+
+// mode 0: y[M][N] = x . w^T (w [N][K], N % 256 == 0);
+// mode 1: y[M][N] = silu(x . w[0:N]^T) * (x . w[N:2N]^T) (w [2N][K], N % 128 == 0).
+// var: schedule variant (bit 0: ping-pong stagger, bit 1: s_setprio around the
+// MFMA clusters; 1 = the default, measured fastest on the 8B shapes).
+// K % 128 == 0, ldx % 8 == 0, ldy % 8 (mode 0) / 4 (mode 1) == 0, 16-byte
+// aligned x / w / y (8 for y in mode 1); y row stride ldy >= N.
+K8S_API int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode,
+                         int var, hipStream_t s) {
+  return big_launch(x, ldx, w, y, ldy, M, N, K, mode, var, 1, nullptr, true, s);
+}
+
+// split-K (mode 0): `splits` K slices (K % (128 splits) == 0) into the fp32
+// scratch `part` [splits][M][N], then reduced into y
+K8S_API int k8s_gemm_big_split(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int var,
+                               int splits, void* part, hipStream_t s) {
+  return big_launch(x, ldx, w, y, ldy, M, N, K, 0, var, splits, (float*)part, true, s);
+}
+
+// the same, leaving the partials in `part` for a fused consumer (no reduce launch)
+K8S_API int k8s_gemm_big_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int var,
+                              int splits, void* part, hipStream_t s) {
+  return big_launch(x, ldx, w, y, ldy, M, N, K, 0, var, splits, (float*)part, false, s);
 }

@@ -68,12 +68,16 @@ int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy
                          int splits, void* part, hipStream_t s);
 int k8s_gemm_big(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int mode, int pipe,
                  hipStream_t s);
+int k8s_gemm_big_split(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int var, int splits,
+                       void* part, hipStream_t s);
+int k8s_gemm_big_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int var, int splits,
+                      void* part, hipStream_t s);
 int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
-// 4 gemm_stream (cfg = ring depth, splits), 5 gemm_big (cfg = pipe);
+// 4 gemm_stream (cfg = ring depth, splits), 5 gemm_big (cfg = schedule variant, splits);
 // fuse: 1 -- a split-K o / down projection may leave its partials to the next norm;
 // 2 (gate_up, kinds 4 / 5 with one K split) -- the SwiGLU-epilogue form, which
 // writes act directly (gu is never written, no silu_mul launch);
@@ -155,11 +159,11 @@ constexpr int kD = 128;
 // partials in the kind's scratch for the following norm to reduce
 // (k8s_splitk_addnorm); deferred() tells the caller where they are.
 bool deferred(const K8sGemmSel& g, bool defer) {
-  return defer && g.fuse && g.splits > 1 && (g.kind == 2 || g.kind == 3 || g.kind == 4);
+  return defer && g.fuse && g.splits > 1 && (g.kind == 2 || g.kind == 3 || g.kind == 4 || g.kind == 5);
 }
 
 const void* part_of(const K8sLlamaStep& s, const K8sGemmSel& g) {
-  return (g.kind == 2 || g.kind == 4) ? s.mid_part : s.grp_part;
+  return (g.kind == 2 || g.kind == 4 || g.kind == 5) ? s.mid_part : s.grp_part;
 }
 
 int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, const void* w, void* y, int ldy, int M,
@@ -177,6 +181,9 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
       return (d ? k8s_gemm_stream_part : k8s_gemm_stream)(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part,
                                                           st);
     case 5:
+      if (g.splits > 1)
+        return (d ? k8s_gemm_big_part : k8s_gemm_big_split)(x, ldx, w, y, ldy, M, N, K, g.cfg, g.splits, s.mid_part,
+                                                            st);
       return k8s_gemm_big(x, ldx, w, y, ldy, M, N, K, 0, g.cfg, st);
     default:
       return k8s_blaslt_gemm(x, ldx, w, y, ldy, M, N, K, s.blaslt_ws, s.blaslt_ws_bytes, st);

@@ -213,7 +213,7 @@ class LlamaExecutor:
             st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
             if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):
                 st.sel[i].fuse = 3  # RoPE + KV write in the qkv GEMM's epilogue
-            if kind in (LIN.KIND_MID, LIN.KIND_STREAM) and splits > 1:
+            if kind in (LIN.KIND_MID, LIN.KIND_STREAM, LIN.KIND_BIG) and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:
                 need_grp = max(need_grp, splits * T * N if splits > 1 else 1)

@@ -45,8 +45,10 @@ def select_gemm(M: int, N: int, K: int, x_ok_layout: bool = True, out_contig: bo
             if kind == "lib":
                 return KIND_LIB, 0, 1
             forced_skinny = kind == "skinny" and M <= 128
-    if M > DISPATCH_MAX_M and x_ok_layout and _big_pick(M, N, K):
-        return KIND_BIG, BIG_PIPE, 1
+    if M > DISPATCH_MAX_M and x_ok_layout:
+        big_splits = _big_pick(M, N, K)
+        if big_splits:
+            return KIND_BIG, BIG_PIPE, big_splits
     if (_enabled and (M == 1 or forced_skinny or (M <= SKINNY_MAX_M and N * K <= SKINNY_MAX_NK))
             and x_ok_layout and K % 256 == 0 and N % 16 == 0):
         return KIND_SKINNY, 0, 1
@@ -68,7 +70,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
     if kind == KIND_STREAM:
         return gemm_stream(x, w, cfg, splits, out)
     if kind == KIND_BIG:
-        return gemm_big(x, w, out, pipe=cfg)
+        return gemm_big(x, w, out, pipe=cfg, splits=splits)
     if kind == KIND_SKINNY:
         if out is None:
             out = torch.empty((M, N), dtype=x.dtype, device=x.device)
@@ -128,9 +130,33 @@ def linear_f32out(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
 
 
 def reserve_lib_workspace(dev: torch.device) -> None:
-    """Allocate the hipBLASLt workspace before any HIP-graph capture."""
+    """Allocate the hipBLASLt workspace (and gemm_big's split-tail workspace)
+    before any HIP-graph capture."""
     if dev not in _blaslt_ws:
         _blaslt_ws[dev] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=dev)
+    reserve_big_ws(dev)
+
+
+_big_ws: Dict[torch.device, torch.Tensor] = {}
+_big_tail = os.environ.get("K8SRCA_BIG_TAIL", "1") == "1"
+
+
+def reserve_big_ws(dev: torch.device, enable: bool = None) -> None:
+    """gemm_big's split-tail workspace on ``dev`` (csrc/kernels/gemm_big.hip:
+    256 fp32 partial tiles + tickets, zeroed once): without it the kernel runs
+    a partial last wave of whole tiles.  ``enable=False`` unregisters it (A/B)."""
+    dev = torch.device(dev)
+    if dev.type != "cuda":
+        return
+    on = _big_tail if enable is None else enable
+    with torch.cuda.device(dev):
+        if not on:
+            check(lib().k8s_gemm_big_set_ws(None), "gemm_big_set_ws")
+            return
+        t = _big_ws.get(dev)
+        if t is None:
+            t = _big_ws[dev] = torch.zeros(lib().k8s_gemm_big_ws_bytes(), dtype=torch.uint8, device=dev)
+        check(lib().k8s_gemm_big_set_ws(ptr(t)), "gemm_big_set_ws")
 
 
 # ------------------------------------------------ hipBLASLt solution tuning
@@ -363,15 +389,15 @@ def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
     return out
 
 
-BIG_PIPE = int(os.environ.get("K8SRCA_BIG_PIPE", "2"))
+BIG_PIPE = int(os.environ.get("K8SRCA_BIG_VAR", "1"))  # schedule variant (gemm_big.hip: 1 = ping-pong)
 # Prefill-size dispatch between gemm_big and hipBLASLt: per (N, K) the M ranges
-# where the hand-written kernel measured faster (data/gemm_big_<model>.json,
-# tools/big_gemm_ab.py --emit), separately for the SwiGLU-fused gate_up form
-# (against hipBLASLt + silu_mul).  K8SRCA_BIG_GEMM=0 disables it;
-# K8SRCA_BIG_GEMM=all uses gemm_big for every shape it accepts above
-# DISPATCH_MAX_M (A/B runs).
+# where the hand-written kernel measured faster, each with its K split count
+# (data/gemm_big_<model>.json, tools/big_gemm_ab.py --emit), separately for the
+# SwiGLU-fused gate_up form (against hipBLASLt + silu_mul).
+# K8SRCA_BIG_GEMM=0 disables it; K8SRCA_BIG_GEMM=all uses gemm_big (no K split)
+# for every shape it accepts above DISPATCH_MAX_M (A/B runs).
 _big_mode = os.environ.get("K8SRCA_BIG_GEMM", "1")
-_big_ranges: Dict[Tuple, List[Tuple[int, int]]] = {}
+_big_ranges: Dict[Tuple, List[Tuple[int, int, int]]] = {}
 
 
 def big_path(model: str, tp: int = 1) -> str:
@@ -389,9 +415,23 @@ def load_big(path: str) -> int:
     for tag, silu in (("ranges", False), ("silu", True)):
         for key, rows in d.get(tag, {}).items():
             N, K = (int(v) for v in key.split(","))
-            _big_ranges[("silu", N, K) if silu else (N, K)] = [(int(lo), int(hi)) for lo, hi in rows]
+            _big_ranges[("silu", N, K) if silu else (N, K)] = [
+                (int(r[0]), int(r[1]), int(r[2]) if len(r) > 2 else 1) for r in rows]
             n += len(rows)
     return n
+
+
+def big_scratch_elems() -> int:
+    """fp32 elements of split-K partials the loaded gemm_big ranges can need
+    (the gemm_mid scratch, reserved before any capture)."""
+    need = 0
+    for key, rows in _big_ranges.items():
+        if key[0] == "silu":
+            continue
+        for lo, hi, splits in rows:
+            if splits > 1:
+                need = max(need, min(hi, 8192) * key[0] * splits)
+    return need
 
 
 def set_big(mode: str) -> None:
@@ -399,19 +439,19 @@ def set_big(mode: str) -> None:
     _big_mode = mode
 
 
-def _big_pick(M: int, N: int, K: int, silu: bool = False) -> bool:
-    """gemm_big for this (M, N, K)?  ``N`` is the weight's row count (2I for
-    the SwiGLU form)."""
+def _big_pick(M: int, N: int, K: int, silu: bool = False) -> int:
+    """K splits of gemm_big for this (M, N, K), 0 = not gemm_big.  ``N`` is
+    the weight's row count (2I for the SwiGLU form)."""
     if _big_mode == "0" or M <= DISPATCH_MAX_M:
-        return False
+        return 0
     if not big_shape_ok(M, N // 2 if silu else N, K, silu):
-        return False
+        return 0
     if _big_mode == "all":
-        return True
-    for lo, hi in _big_ranges.get(("silu", N, K) if silu else (N, K), ()):
-        if lo <= M <= hi:
-            return True
-    return False
+        return 1
+    for lo, hi, splits in _big_ranges.get(("silu", N, K) if silu else (N, K), ()):
+        if lo <= M <= hi and big_shape_ok(M, N // 2 if silu else N, K, silu, splits):
+            return splits
+    return 0
 
 
 # SwiGLU epilogue on the decode stream kernel: where the dispatch table picks
@@ -460,29 +500,43 @@ def swiglu_gemm(y: torch.Tensor, w_gu: torch.Tensor):
     return gemm_stream_silu(y, w_gu, ch[1])
 
 
-def big_shape_ok(M: int, N: int, K: int, silu: bool = False) -> bool:
+def big_shape_ok(M: int, N: int, K: int, silu: bool = False, splits: int = 1) -> bool:
     """What csrc/kernels/gemm_big.hip accepts: 256-column tiles (128 act
-    columns for the SwiGLU form), 32-deep chunks."""
-    return M > 0 and K % 32 == 0 and N % (128 if silu else 256) == 0
+    columns for the SwiGLU form), K in pairs of 64-deep tiles per K split
+    (split-K only for the plain form)."""
+    return (M > 0 and splits >= 1 and K % (128 * splits) == 0 and N % (128 if silu else 256) == 0
+            and not (silu and splits > 1))
 
 
 def gemm_big(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, silu: bool = False,
-             pipe: int = None) -> torch.Tensor:
+             pipe: int = None, splits: int = 1) -> torch.Tensor:
     """``x @ w.T`` on the prefill-size MFMA kernel (csrc/kernels/gemm_big.hip:
-    256 x 256 tiles, LDS-DMA ring).  ``silu=True``: ``w`` is the gate_up weight
+    256 x 256 x 64 tiles, eight-phase ping-pong schedule, LDS-DMA staging;
+    ``pipe`` = schedule variant, 3 the default).  ``silu=True``: ``w`` is the gate_up weight
     [2I, K] and the result is ``silu(x @ Wg.T) * (x @ Wu.T)`` [M, I] -- the
-    SwiGLU epilogue, with the unfused path's bf16 rounding of gate and up."""
+    SwiGLU epilogue, with the unfused path's bf16 rounding of gate and up.
+    ``splits`` > 1: K split over that many workgroups per tile (fp32 partials
+    in the gemm_mid scratch, then a reduce launch)."""
     M, K = x.shape
     N = w.shape[0] // 2 if silu else w.shape[0]
     if not (x.dtype == torch.bfloat16 and w.dtype == torch.bfloat16 and x.stride(1) == 1 and x.stride(0) % 8 == 0
-            and w.is_contiguous() and w.shape[1] == K and big_shape_ok(M, N, K, silu)):
-        raise ValueError(f"gemm_big: unsupported operands x {tuple(x.shape)} w {tuple(w.shape)} silu={silu}")
+            and w.is_contiguous() and w.shape[1] == K and big_shape_ok(M, N, K, silu, splits)):
+        raise ValueError(f"gemm_big: unsupported operands x {tuple(x.shape)} w {tuple(w.shape)} silu={silu} "
+                         f"splits={splits}")
     if out is None:
         out = torch.empty((M, N), dtype=x.dtype, device=x.device)
     if M == 0:
         return out
-    check(lib().k8s_gemm_big(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, int(silu),
-                             BIG_PIPE if pipe is None else pipe, stream_ptr(x)), "gemm_big")
+    var = BIG_PIPE if pipe is None else pipe
+    if x.device not in _big_ws and _big_tail:
+        reserve_big_ws(x.device)
+    if splits > 1:
+        part = _scratch(x.device, splits * M * N)
+        check(lib().k8s_gemm_big_split(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, var, splits,
+                                       ptr(part), stream_ptr(x)), "gemm_big_split")
+        return out
+    check(lib().k8s_gemm_big(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, int(silu), var,
+                             stream_ptr(x)), "gemm_big")
     return out
 
 
@@ -572,6 +626,7 @@ def reserve_dispatch_scratch(dev: torch.device) -> None:
                 need_mid = max(need_mid, m * n * splits)
             elif kind == "grp" and splits > 1:
                 need_grp = max(need_grp, m * n * splits)
+    need_mid = max(need_mid, big_scratch_elems())
     if need_mid:
         _scratch(dev, need_mid)
     if need_grp:

@@ -46,17 +46,24 @@ def _on_xgmi(pc, nbytes: int) -> bool:
     return car is not None and pc.ep_group is pc.tp_group and car.a2a_fits(nbytes)
 
 
-def _a2a(pc, send: torch.Tensor, recv: torch.Tensor, sim_replicate: bool = True) -> torch.Tensor:
+def _a2a(pc, send: torch.Tensor, recv: torch.Tensor, sim_fill: str = "own") -> torch.Tensor:
     """Equal-split all-to-all over the EP group: ``send`` / ``recv`` [ep, ...].
     Under tp-sim (rank 0 alone, parallel/tpsim.py) the loopback kernel moves
-    the bytes and every "peer" region then carries this rank's own region --
-    the same routing statistics from every rank, so the local expert sees the
-    row count it would on a real EP group."""
+    the bytes, and the "peer" regions -- never written by any rank -- are then
+    filled: ``"own"`` with this rank's own region (dispatch: the same routing
+    statistics from every rank, so the local expert sees the row count it
+    would on a real EP group; row all-gather: finite activations), ``"zero"``
+    with zeros (combine: the peers' expert outputs for this rank's slots are
+    not computed here -- rank 0's own block in their place would hand back
+    the never-computed null-expert rows past its slot count)."""
     car = pc.custom_ar
     if send.is_cuda and send.dtype == torch.bfloat16 and _on_xgmi(pc, send.numel() * 2):
         car.all_to_all(send, recv)
-        if getattr(pc, "sim", False) and sim_replicate:
-            recv[1:] = recv[0:1]
+        if getattr(pc, "sim", False):
+            if sim_fill == "own":
+                recv[1:] = recv[0:1]
+            else:
+                recv[1:].zero_()
         return recv
     dist.all_to_all_single(recv, send, group=pc.ep_group)
     return recv
@@ -92,14 +99,19 @@ def ep_moe_forward_fixed(moe, li: int, y: torch.Tensor, topk_w: torch.Tensor, to
     # rows past offs2[El] are never computed; the grouped kernels read the offsets on the device
     ys = moe.experts(li, xs, offs2[: El + 1].contiguous(), device_offsets=True)
     out_recv = ys.index_select(0, inv2.long()).contiguous()
-    back = _a2a(pc, out_recv.view(ep, C * H), torch.empty(ep, C * H, dtype=y.dtype, device=dev)).view(ep * C, H)
+    back = _a2a(pc, out_recv.view(ep, C * H), torch.empty(ep, C * H, dtype=y.dtype, device=dev),
+                sim_fill="zero").view(ep * C, H)
     own = y.new_zeros((per, H))
     if n_own:
         y_slots = back.index_select(0, flat)                         # (token, k) slot order
         own[:n_own] = M.combine(y_slots.contiguous(), slots.to(torch.int32), topk_w[lo:hi].contiguous(), n_own, k)
-    # all-gather of the owned rows as an all-to-all of `ep` copies (one static-size collective)
+    # all-gather of the owned rows as an all-to-all of `ep` copies (one static-size collective).
+    # Under tp-sim the "peer" blocks of the loopback buffer were never written:
+    # they carry this rank's block instead (finite activations, like every other
+    # stand-in), never the stale slots -- with those the hidden states of 7/8 of
+    # the rows were garbage and the simulated runs sampled ~2 tokens each.
     gathered = _a2a(pc, own.unsqueeze(0).expand(ep, per, H).contiguous().view(ep, per * H),
-                    torch.empty(ep, per * H, dtype=y.dtype, device=dev), sim_replicate=False)
+                    torch.empty(ep, per * H, dtype=y.dtype, device=dev))
     return gathered.view(ep * per, H)[:T]
 
 

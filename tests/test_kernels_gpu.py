@@ -842,12 +842,14 @@ def test_sampling_top_p_and_tie_candidates_deterministic():
     assert bool((ids >= 16032).all()) and bool((ids[:, 1:] > ids[:, :-1]).all())  # valid, (v desc, id asc)
 
 
-@pytest.mark.parametrize("pipe", [0, 1, 2])
-@pytest.mark.parametrize("M,N,K", [(1, 256, 32), (100, 512, 96), (256, 1024, 4096), (300, 768, 256),
-                                   (1000, 6144, 512), (2085, 4096, 1024), (4096, 256, 14336)])
+@pytest.mark.parametrize("pipe", [3, 0, 1, 2])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 128), (100, 512, 128), (256, 1024, 4096), (300, 768, 384),
+                                   (1000, 6144, 512), (1300, 768, 256), (2085, 4096, 1024), (4096, 256, 14336)])
 def test_gemm_big_vs_fp32(M, N, K, pipe):
-    """Prefill-size GEMM (csrc/kernels/gemm_big.hip: 256 x 256 tiles, LDS-DMA
-    ring, XCD-grouped tile order) vs fp32, M tails, K of 1..448 chunks, plus an
+    """Prefill-size GEMM (csrc/kernels/gemm_big.hip: 256 x 256 x 64 eight-phase
+    schedule, LDS-DMA staging, XCD-grouped tile order, permuted W rows for the
+    16-byte epilogue stores) vs fp32 for every schedule variant: M tails, tile
+    groups cut short (1300 rows = 6 M tiles), K of 2..224 tiles, plus an
     asymmetric exact check (one-hot rows pick weight columns)."""
     _need_gpu()
     from k8s_llm_rca_amd.ops import linear as LIN
@@ -870,8 +872,61 @@ def test_gemm_big_vs_fp32(M, N, K, pipe):
     assert torch.count_nonzero(yb[:, N:]) == 0
 
 
-@pytest.mark.parametrize("pipe", [0, 1, 2])
-@pytest.mark.parametrize("M,I,K", [(5, 128, 64), (300, 384, 512), (1500, 1024, 4096)])
+@pytest.mark.parametrize("splits", [2, 4])
+@pytest.mark.parametrize("M,N,K", [(1, 256, 512), (1000, 512, 1024), (300, 768, 2048), (2085, 256, 14336)])
+def test_gemm_big_split_k_vs_fp32(M, N, K, splits):
+    """gemm_big with K split over workgroups (fp32 partials [splits][M][N] +
+    the slice-order reduce): fp32 reference, and the partials themselves sum
+    to the reduced output."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops._lib import check, lib, ptr, stream_ptr
+    torch.manual_seed(M + N + K + splits)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    y = LIN.gemm_big(x, w, splits=splits)
+    torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+    part = torch.full((splits, M, N), float("nan"), device=dev)
+    check(lib().k8s_gemm_big_part(ptr(x), x.stride(0), ptr(w), None, N, M, N, K, LIN.BIG_PIPE, splits, ptr(part),
+                                  stream_ptr(x)), "gemm_big_part")
+    acc = part[0].clone()
+    for s_ in range(1, splits):
+        acc += part[s_]
+    assert torch.equal(acc.bfloat16(), y)
+
+
+@pytest.mark.parametrize("M,N,K,silu", [(6144, 4096, 1024, False), (3072, 6144, 2048, False),
+                                        (1300, 4352, 512, False), (2085, 1024, 1024, True)])
+def test_gemm_big_split_tail(M, N, K, silu):
+    """Split tail (the partial last wave's tiles as K slices, the last arriver
+    sums the fp32 partials in slice order): fp32 reference, run-to-run
+    identical, and within bf16 rounding of the whole-tile path.  Tile counts:
+    384 (128 tail tiles x 2), 288 (32 x 4), 102 (no full wave: 102 x 2),
+    SwiGLU 72 (72 x 2)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    torch.manual_seed(M + N)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(2 * N if silu else N, K, device=dev) * 0.03).bfloat16()
+    try:
+        LIN.reserve_big_ws(dev, enable=True)
+        y1 = LIN.gemm_big(x, w, silu=silu)
+        y2 = LIN.gemm_big(x, w, silu=silu)
+        LIN.reserve_big_ws(dev, enable=False)
+        y0 = LIN.gemm_big(x, w, silu=silu)
+    finally:
+        LIN.reserve_big_ws(dev)
+    assert torch.equal(y1, y2)
+    ref = x.float() @ w.float().t()
+    if silu:
+        g, u = ref.split(N, dim=1)
+        ref = torch.nn.functional.silu(g) * u
+    torch.testing.assert_close(y1.float(), ref, atol=3e-2, rtol=3e-2)
+    torch.testing.assert_close(y1.float(), y0.float(), atol=2e-2, rtol=2e-2)
+
+
+@pytest.mark.parametrize("pipe", [3, 1])
+@pytest.mark.parametrize("M,I,K", [(5, 128, 128), (300, 384, 512), (1500, 1024, 4096), (4100, 14336, 256)])
 def test_gemm_big_silu_epilogue(M, I, K, pipe):
     """SwiGLU epilogue of gemm_big (gate_up never written) == the unfused
     gemm_big + silu_mul bit for bit, and fp32 silu(x Wg^T) * (x Wu^T)."""

@@ -110,7 +110,8 @@ def test_mixtral_engine_graphs_match_eager():
 
 
 @pytest.mark.parametrize("graphs,splitk", [(False, False), (True, False), (False, True), (True, True),
-                                           (False, "stream"), (True, "stream"), (False, "big"), (True, "big")])
+                                           (False, "stream"), (True, "stream"), (False, "big"), (True, "big"),
+                                           (False, "bigsplit")])
 def test_layer_executor_bit_identical(graphs, splitk):
     """The native layer executor (one C call per forward) issues the same
     kernels in the same order as the Python layer loop: every step's logits
@@ -120,7 +121,10 @@ def test_layer_executor_bit_identical(graphs, splitk):
     inside the following residual add + RMSNorm instead of a reduce kernel.
     ``"big"``: every projection above 256 rows on gemm_big (gate_up with its
     SwiGLU epilogue) and the decode-size gate_up on the stream kernel's
-    SwiGLU epilogue."""
+    SwiGLU epilogue.  ``"bigsplit"``: gemm_big with K split over 2 / 4
+    workgroups for qkv / o / down above 256 rows: the executor leaves the fp32
+    partials to the RoPE / KV write and the residual add + RMSNorm, the Python
+    path reduces them with gemm_big's reduce kernel -- same sums, same order."""
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
@@ -142,6 +146,12 @@ def test_layer_executor_bit_identical(graphs, splitk):
                 assert LIN.swiglu_choice(300, 2048, 512)[0] == LIN.KIND_BIG
                 assert LIN.swiglu_choice(5, 2048, 512) == (LIN.KIND_STREAM, 4, 1)
                 assert LIN.select_gemm(300, 512, 1024)[0] == LIN.KIND_BIG
+            elif splitk == "bigsplit":
+                LIN.set_big("1")
+                LIN._big_ranges[(512, 1024)] = [(257, 1 << 20, 4)]   # o and down
+                LIN._big_ranges[(1536, 512)] = [(257, 1 << 20, 2)]   # qkv
+                assert LIN.select_gemm(300, 512, 1024) == (LIN.KIND_BIG, LIN.BIG_PIPE, 4)
+                assert LIN.select_gemm(300, 1536, 512) == (LIN.KIND_BIG, LIN.BIG_PIPE, 2)
             elif splitk:  # after the engine's own (absent) dispatch table was loaded
                 LIN._dispatch[(512, 1024)] = split_rows
                 if splitk == "stream":
@@ -172,6 +182,8 @@ def test_layer_executor_bit_identical(graphs, splitk):
         LX.set_enabled(True)
         LIN._dispatch.pop((512, 1024), None)
         LIN._dispatch.pop((2048, 512), None)
+        LIN._big_ranges.pop((512, 1024), None)
+        LIN._big_ranges.pop((1536, 512), None)
         LIN.set_big(os.environ.get("K8SRCA_BIG_GEMM", "1"))
     (r0, l0), (r1, l1) = runs
     assert r0 == r1

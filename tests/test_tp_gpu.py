@@ -263,6 +263,48 @@ def test_tp_sim_rank0_runs_real_kernels_with_standin_collectives():
     pc.custom_ar.close()
 
 
+def test_tp_sim_moe_ep_runs_full_length():
+    """bench --tp-sim on a MoE model (VERDICT r3 missing #2): rank 0 of a
+    TP=4 / EP=4 tiny-mixtral -- attention shards, E/4 local experts, the
+    fixed-capacity dispatch / combine / row all-gather over the loopback xGMI
+    all-to-all -- produces finite logits and full-length runs (the r3 run
+    sampled ~2 tokens per run: the row all-gather handed back never-written
+    loopback slots), decode steps replay HIP graphs, and the projection prices
+    the MoE collectives."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.parallel.tpsim import project, sim_context
+    pc = sim_context(4, ep=4)
+    eng = LLMEngine(EngineConfig(model="tiny-mixtral", device="cuda:0", num_blocks=128, block_size=64,
+                                 max_batch_tokens=1024, temperature=0.8), pc)
+    assert eng.model.moe is not None and eng.model.moe.E_local * 4 == eng.model.moe.E
+    finite = []
+    fwd = eng.model.forward
+
+    def rec(*a, **k):
+        out = fwd(*a, **k)
+        if not torch.cuda.is_current_stream_capturing():
+            finite.append(bool(torch.isfinite(out.float()).all()))
+        return out
+    eng.model.forward = rec
+    outs = {}
+    for i in range(6):
+        sid = eng.new_sequence()
+        toks = eng.tok.system_prefix("sys") + eng.tok.message("user", "moe %d " % i * (40 + 60 * i)) \
+            + eng.tok.header("assistant")
+        eng.submit(sid, toks, None, 24, seed=2, on_done=lambda g, st, i=i: outs.__setitem__(i, g))
+    eng.run_until_idle()
+    assert finite and all(finite)
+    lens = {i: (None if g is None else len(g)) for i, g in outs.items()}
+    assert len(outs) == 6 and all(v == 24 for v in lens.values()), (lens, eng.stats)
+    assert eng.stats["graph_steps"] > 0
+    pr = project(eng.sim_rows, pc, eng.mc.hidden, eng.mc.n_layers, "cuda:0", moe_k=eng.model.moe.k)
+    assert pr["standin_s"] > 0 and pr["modelled_s"] > 0
+    assert pc.custom_ar.status() == 0
+    pc.custom_ar.close()
+
+
 def _overlap_worker(rank, world, port, out_dir):
     import ctypes
 

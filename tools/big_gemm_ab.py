@@ -6,7 +6,13 @@ engine's per-layer weights), Llama-3-8B projection shapes.  Prints per (shape, M
 the median us and TFLOP/s of each arm, and for gate_up the SwiGLU-fused arm vs
 hipBLASLt + silu_mul.
 
-usage: python tools/big_gemm_ab.py [--ms 512,1024,...] [--rounds 5] [--layers 4]
+usage: python tools/big_gemm_ab.py [--ms 512,1024,...] [--rounds 5] [--layers 4] [--splits 2,4]
+                                   [--emit data/gemm_big_llama3-8b.json]
+
+``--emit`` writes the dispatch ranges the engine loads (ops/linear.py
+load_big): per (N, K) the M ranges where the best gemm_big arm (any K split)
+beat hipBLASLt by >= 1 %, and for gate_up the SwiGLU arm vs hipBLASLt +
+silu_mul; a range reaches halfway to the next measured M (the last one is open).
 """
 import argparse
 import json
@@ -39,8 +45,11 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--layers", type=int, default=4)
-    ap.add_argument("--pipes", default="0,1")
+    ap.add_argument("--pipes", default="3,1")
     ap.add_argument("--out", default="")
+    ap.add_argument("--splits", default="2,4", help="K splits tried for the plain form ('' = none)")
+    ap.add_argument("--emit", default="")
+    ap.add_argument("--margin", type=float, default=0.01)
     a = ap.parse_args()
     dev = torch.device("cuda")
     H, I = 4096, 14336
@@ -56,6 +65,11 @@ def main():
             arms = {"blaslt": lambda i: LIN.lib_gemm(x, ws[i % a.layers], y)}
             for p in pipes:
                 arms[f"big{p}"] = lambda i, p=p: LIN.gemm_big(x, ws[i % a.layers], y, pipe=p)
+            for sp in (int(v) for v in a.splits.split(",") if v):
+                tiles = -(-M // 256) * (N // 256)
+                if LIN.big_shape_ok(M, N, K, splits=sp) and tiles < 256:
+                    arms[f"big{pipes[0]}s{sp}"] = lambda i, sp=sp: LIN.gemm_big(x, ws[i % a.layers], y, pipe=pipes[0],
+                                                                                splits=sp)
             if name == "gu":
                 act = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
                 arms["blaslt+silu"] = lambda i: NRM.silu_mul(LIN.lib_gemm(x, ws[i % a.layers], y), out=act)
@@ -82,6 +96,47 @@ def main():
         with open(a.out, "w") as f:
             for r in rows:
                 f.write(json.dumps(r) + "\n")
+    if a.emit:
+        emit(rows, a.emit, a.margin)
+
+
+def emit(rows, path, margin):
+    """Dispatch ranges from the measured rows (module docstring)."""
+    out = {"source": "tools/big_gemm_ab.py", "ranges": {}, "silu": {}}
+    by = {}
+    for r in rows:
+        by.setdefault(r["shape"], []).append(r)
+    for shape, rs in by.items():
+        rs.sort(key=lambda r: r["M"])
+        key = f'{rs[0]["N"]},{rs[0]["K"]}'
+        for tag, base, pref in (("ranges", "blaslt", "big"), ("silu", "blaslt+silu", "big")):
+            if tag == "silu" and shape != "gu":
+                continue
+            picks = []
+            for r in rs:
+                arms = [k for k in r if k.startswith(pref) and not k.endswith("_tf")
+                        and (k.endswith("_silu") if tag == "silu" else not k.endswith("_silu"))]
+                if not arms or base not in r:
+                    picks.append(None)
+                    continue
+                best = min(arms, key=lambda k: r[k])
+                sp = int(best.split("s")[-1]) if "s" in best[3:] and tag != "silu" else 1
+                picks.append(sp if r[best] <= r[base] * (1 - margin) else None)
+            ranges = []
+            for i, (r, sp) in enumerate(zip(rs, picks)):
+                if sp is None:
+                    continue
+                lo = 257 if i == 0 else (rs[i - 1]["M"] + r["M"]) // 2 + 1
+                hi = (r["M"] + rs[i + 1]["M"]) // 2 if i + 1 < len(rs) else 1 << 20
+                if ranges and ranges[-1][2] == sp and ranges[-1][1] + 1 == lo:
+                    ranges[-1][1] = hi
+                else:
+                    ranges.append([lo, hi, sp])
+            if ranges:
+                out[tag][key] = ranges
+    with open(path, "w") as f:
+        json.dump(out, f, indent=1)
+    print("emitted", path, json.dumps(out))
 
 
 if __name__ == "__main__":

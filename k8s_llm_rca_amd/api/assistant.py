@@ -88,7 +88,8 @@ class GenericAssistant:
         run = self.service.wait_run(self.run.id, timeout)
         if run.status == "completed":
             return self.get_last_k_message(num)
-        log.warning("run %s %s", run.id, run.status)
+        if not self.service.closed:  # runs cut short by a shutdown are summarised by close()
+            log.warning("run %s %s", run.id, run.status)
         return None
 
     def get_token_usage(self, tmin: float, tmax: float, limit: int = 20) -> Dict[str, int]:

@@ -20,11 +20,14 @@ Result objects mirror the OpenAI SDK shapes the reference reads:
 from __future__ import annotations
 
 import itertools
+import logging
 import threading
 import time
 import uuid
 from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
+
+log = logging.getLogger(__name__)
 
 TERMINAL = ("completed", "failed", "cancelled", "expired")
 
@@ -152,6 +155,8 @@ class AssistantService:
             active = [r for r in self.runs.values() if not r.done.is_set()]
         for rs in active:
             self.cancel_run(rs.run.id)
+        if active:  # one line for the shutdown, not one warning per cut-short run
+            log.info("service closed: %d active run(s) cancelled", len(active))
 
     # ------------------------------------------------------------ assistants
     def create_assistant(self, instructions: str, name: str, model: str) -> Assistant:

@@ -103,6 +103,15 @@ def _allreduce_max(x: float, world: int, device) -> float:
     return float(t.item())
 
 
+def _allgather_objects(x: Any, world: int) -> List[Any]:
+    if world == 1:
+        return [x]
+    import torch.distributed as dist
+    out: List[Any] = [None] * world
+    dist.all_gather_object(out, x)
+    return out
+
+
 def _allgather_list(xs: List[float], world: int, device) -> List[float]:
     if world == 1:
         return xs
@@ -114,6 +123,11 @@ def _allgather_list(xs: List[float], world: int, device) -> List[float]:
 
 def run(args) -> Optional[Dict[str, Any]]:
     logging.basicConfig(level=logging.WARNING)
+    # bind this rank to its GPU's NUMA-local CPU slice before anything starts a
+    # thread or touches the GPU (utils/placement.py; every later thread inherits it)
+    from ..utils.placement import bind_rank
+    placement = bind_rank(int(os.environ.get("LOCAL_RANK", "0")),
+                          int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
     world, rank = _dist_init()
     if args.gpus is not None and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (bench.py spawns the ranks itself)")
@@ -315,6 +329,7 @@ def run(args) -> Optional[Dict[str, Any]]:
         f"RCA analyses/sec + p50 end-to-end latency, {model_name} backend, {args.graph_nodes}-node graph")
     if args.tp_sim > 1:
         metric = f"PROJECTION (rank 0 of TP={args.tp_sim} simulated on one GPU): " + metric
+    placements = [placement] if tp_mode else _allgather_objects(placement, world)
     res = {
         "metric": metric,
         "value": round(value, 4),
@@ -394,6 +409,8 @@ def run(args) -> Optional[Dict[str, Any]]:
         # CPU seconds per thread group over the timed window (GIL competition with the engine thread)
         "host_cpu_s": {k: round(v - cpu0.get(k, 0.0), 2) for k, v in cpu1.items()},
         "native_threads": {"n": len(native_top), "top_cpu_s": native_top[:4]},
+        # every rank's CPU binding (disjoint NUMA-local slices; null = unbound)
+        "cpu_affinity": placements,
         "setup_s": round(setup_s, 1),
         "wall_s": round(time.perf_counter() - t_start, 1),
         "clean_shutdown": clean,

@@ -26,8 +26,6 @@
 // cached prefix): workgroup = (tile of 64/G tokens, kv head); each wave owns 16
 // rows and walks the keys its rows can see.
 #include <cstdlib>
-#include <map>
-#include <mutex>
 #include <utility>
 
 #include "common.h"
@@ -74,9 +72,6 @@ struct AttnArgs {
   const int4* items;
   int n_items;
   const int* d_n_items;   // device {item count, part_size} (HIP graphs: the grid stays fixed), or null
-  // in-kernel split-KV merge (K8SRCA_DECODE_MERGE=1): arrival counter per (lead row, kv head),
-  // zero between launches (the last arriver resets its own); null: attn_reduce_kernel merges
-  int* merge_cnt;
   int pf_rows;            // rows per prefill partial slot (128: pg64 kernel, 256: w8 kernel)
 };
 
@@ -376,9 +371,6 @@ __global__ void __launch_bounds__(64, 2) attn_decode_kernel(AttnArgs a, int S) {
 // most of its waves on nothing when context lengths vary 1k..6k).
 // MFMA row rho = qi * G + g: token qi of the item (decode row seq + qi, q row
 // qrow + qi), q head g of the kv group.
-// SC1: partials stored write-through at agent scope (the in-kernel merge's
-// hand-off needs no release fence then: cdna_hip_programming.md Guideline 16 R1)
-template <bool SC1 = false>
 __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnArgs& a, int seq, int part, int qrow,
                                                 int kvh, bool whole, int nt, int lane) {
   const int r = lane & 15, h = lane >> 4;
@@ -404,101 +396,21 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
     } else {
       const size_t base = ((size_t)(seq + qi) * a.nq + qh) * a.n_parts + part;
       float* po = a.part_o + base * D;
-      if constexpr (SC1) {
 #pragma unroll
-        for (int dt = 0; dt < 8; ++dt)
-          __hip_atomic_store(po + 16 * dt + r, st.o[dt][i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        if (r == 0) {
-          __hip_atomic_store(a.part_ml + base * 2 + 0, mr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_store(a.part_ml + base * 2 + 1, lr[i], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-      } else {
-#pragma unroll
-        for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
-        if (r == 0) {
-          a.part_ml[base * 2 + 0] = mr[i];
-          a.part_ml[base * 2 + 1] = lr[i];
-        }
+      for (int dt = 0; dt < 8; ++dt) po[16 * dt + r] = st.o[dt][i];
+      if (r == 0) {
+        a.part_ml[base * 2 + 0] = mr[i];
+        a.part_ml[base * 2 + 1] = lr[i];
       }
     }
   }
 }
 
-// Split-KV merge by the LAST wave to finish a (row group, kv head): rows
-// seq .. seq + nt - 1, q heads kvh * G .. + G - 1.  Same arithmetic in the same
-// order as attn_reduce_kernel (exact max, then sequential sums over the
-// partitions), so the rows are bit-identical to the separate launch.
-// Hand-off (cdna_hip_programming.md Guideline 16, R1 counter form): every
-// partial-writing wave stores its partials write-through (agent-scope atomic
-// stores), drains them and takes a ticket; the wave that draws the last one
-// reads every partial with agent-scope loads (no release or acquire fence: a
-// per-wave release -- an L2 write-back -- made the first form 36 % slower,
-// profiles/r2_decode_merge/); it resets the counter for the next launch.  Four (row, head) pairs per pass, 16 lanes x 8
-// dims each.
-// agent-scope load that bypasses this CU's L1 (reads what other XCDs' write-through stores left)
-__device__ __forceinline__ float ld_sc1(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-// Publish this wave's partials and take a ticket: true for the last arriver
-// of the (row group, kv head), which then owes its merge.
-__device__ __forceinline__ bool decode_merge_ticket(const AttnArgs& a, int seq, int kvh, int nt, int part_size,
-                                                    int lane) {
-  const int np_grp = (a.ctx_lens[seq + nt - 1] + part_size - 1) / part_size;
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this wave's write-through partials have landed
-  int ticket = 0;
-  if (lane == 0)
-    ticket = __hip_atomic_fetch_add(a.merge_cnt + seq * a.nkv + kvh, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  return __shfl(ticket, 0, 64) == np_grp - 1;
-}
-
-// the owed merge (after the acquire); resets the group's counter
-__device__ __forceinline__ void decode_merge_rows(const AttnArgs& a, int seq, int kvh, int qrow, int nt,
-                                                  int part_size, int lane) {
-  int* cnt = a.merge_cnt + seq * a.nkv + kvh;
-  const int sub = lane & 15, grp = lane >> 4, d0 = 8 * sub;
-  const int pairs = nt * a.G;
-  for (int pb = 0; pb < pairs; pb += 4) {
-    const int pr = pb + grp;
-    const bool live = pr < pairs;
-    const int qi = live ? pr / a.G : 0, g = live ? pr % a.G : 0;
-    const int row = seq + qi, qh = kvh * a.G + g;
-    const int np = live ? min(a.n_parts, (a.ctx_lens[row] + part_size - 1) / part_size) : 0;
-    const size_t base = ((size_t)row * a.nq + qh) * a.n_parts;
-    // exact max over the partitions: lane sub covers p = sub, sub + 16, ...
-    float M = -INFINITY;
-    for (int p = sub; p < np; p += 16) M = fmaxf(M, ld_sc1(a.part_ml + (base + p) * 2));
-#pragma unroll
-    for (int o = 1; o < 16; o <<= 1) M = fmaxf(M, __shfl_xor(M, o, 64));
-    float L = 0.f, acc[8];
-#pragma unroll
-    for (int i = 0; i < 8; ++i) acc[i] = 0.f;
-    for (int p = 0; p < np; ++p) {
-      const float m = ld_sc1(a.part_ml + (base + p) * 2);
-      const float f = (m == -INFINITY) ? 0.f : exp2f(m - M);
-      // l * f rounded on its own, then added: attn_reduce_kernel stages l * f
-      // through LDS before summing (a contracted fma here would round once less)
-      L += __fmul_rn(ld_sc1(a.part_ml + (base + p) * 2 + 1), f);
-      const float* po = a.part_o + (base + p) * D + d0;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) acc[i] += ld_sc1(po + i) * f;
-    }
-    if (live) {
-      u16x8 ov;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) ov[i] = f2bf(L > 0.f ? acc[i] / L : 0.f);
-      *reinterpret_cast<u16x8*>(a.out + (size_t)(qrow + qi) * a.out_stride + qh * D + d0) = ov;
-    }
-  }
-  if (lane == 0) __hip_atomic_store(cnt, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <bool MERGE>
+// (Round 2-3 also had an in-kernel split-KV merge by the last-arriving wave of
+// each (row group, kv head), K8SRCA_DECODE_MERGE=1: its per-item ticket cost
+// what the separate reduce launch saves -- profiles/r2_decode_merge/ -- and it
+// was retired in round 4; attn_reduce_kernel merges.)
 __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
-  // MERGE: merges this wave owes (it drew a group's last ticket), done after its work list
-  // so the merge code does not share the streaming loop's registers: {seq, kvh | nt << 8, qrow}
-  __shared__ int owed[3 * 64];
-  int n_owed = 0;
   const int lane = threadIdx.x;
   const int r = lane & 15;
   // graphs: {item count, keys per partition} are read on the device, so one
@@ -529,29 +441,7 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
     RowState st;
     init_state(st, a, qrow + (valid ? qi : 0), kvh * a.G + (valid ? r - qi * a.G : 0), valid, lane);
     decode_stream64(st, a, blkv, kvh, k0, k1, kmin, lim, lane);
-    decode_epilogue<MERGE>(st, a, seq, part, qrow, kvh, whole, nt, lane);
-    if (MERGE && !whole && decode_merge_ticket(a, seq, kvh, nt, part_size, lane)) {
-      if (n_owed < 64) {
-        if (lane == 0) {
-          owed[3 * n_owed] = seq;
-          owed[3 * n_owed + 1] = kvh | (nt << 8);
-          owed[3 * n_owed + 2] = qrow;
-        }
-        ++n_owed;
-      } else {  // (never at decode batch sizes) merge at once
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        decode_merge_rows(a, seq, kvh, qrow, nt, part_size, lane);
-      }
-    }
-  }
-  if (!MERGE || n_owed == 0) return;
-  // every load of a handed-off partial is an agent-scope (sc1) load: no acquire
-  // fence, only a compiler barrier (Guideline 16, "Valid forms")
-  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  for (int i = 0; i < n_owed; ++i) {
-    const int e1 = owed[3 * i + 1];
-    decode_merge_rows(a, owed[3 * i], e1 & 0xFF, owed[3 * i + 2], e1 >> 8, part_size, lane);
+    decode_epilogue(st, a, seq, part, qrow, kvh, whole, nt, lane);
   }
 }
 
@@ -1194,34 +1084,6 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
 
 using namespace k8s;
 
-// Arrival counters of the in-kernel split-KV merge (K8SRCA_DECODE_MERGE=1, read
-// per call): one zeroed device buffer per GPU, allocated outside any stream
-// capture (the first eager decode step; until then, and for batches beyond its
-// capacity, the separate reduce kernel merges).
-// One buffer per (device, stream): launches on different streams (two engines on
-// one GPU) never share the self-resetting counters; the map is guarded, so
-// concurrent first calls from several host threads allocate once per key.
-static int* merge_counters(int need, hipStream_t stream) {
-  constexpr int kCap = 1 << 16;
-  static std::mutex mu;
-  static std::map<std::pair<int, hipStream_t>, int*> bufs;
-  const char* v = std::getenv("K8SRCA_DECODE_MERGE");
-  if (!(v && v[0] == '1') || need > kCap) return nullptr;
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return nullptr;
-  std::lock_guard<std::mutex> g(mu);
-  int*& slot = bufs[{dev, stream}];
-  if (!slot) {
-    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
-    if (hipStreamIsCapturing(stream, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) return nullptr;
-    int* p = nullptr;
-    if (hipMalloc(&p, kCap * sizeof(int)) != hipSuccess) return nullptr;
-    if (hipMemset(p, 0, kCap * sizeof(int)) != hipSuccess) return nullptr;
-    slot = p;
-  }
-  return slot;
-}
-
 K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,
                             int bt_stride, const int* ctx_lens, const int* q_start, int S, int nq, int nkv, int BS,
                             float scale, void* out, int out_stride, float* part_o, float* part_ml, int n_parts,
@@ -1253,16 +1115,12 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
     a.items = reinterpret_cast<const int4*>(items);
     a.n_items = n_items;
     a.d_n_items = d_n_items;
-    if (n_parts > 1) a.merge_cnt = merge_counters(S * nkv, stream);
-    if (a.merge_cnt)
-      hipLaunchKernelGGL(attn_decode_items_kernel<true>, dim3(grid_waves), dim3(64), 0, stream, a);
-    else
-      hipLaunchKernelGGL(attn_decode_items_kernel<false>, dim3(grid_waves), dim3(64), 0, stream, a);
+    hipLaunchKernelGGL(attn_decode_items_kernel, dim3(grid_waves), dim3(64), 0, stream, a);
   } else {
     const long nw = (long)S * nkv * n_parts;
     hipLaunchKernelGGL(attn_decode_kernel, dim3((unsigned)nw), dim3(64), 0, stream, a, S);
   }
-  if (n_parts > 1 && !a.merge_cnt) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
+  if (n_parts > 1) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
   return (int)hipGetLastError();
 }
 

@@ -72,6 +72,9 @@ int k8s_gemm_big_split(const void* x, int ldx, const void* w, void* y, int ldy, 
                        void* part, hipStream_t s);
 int k8s_gemm_big_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int var, int splits,
                       void* part, hipStream_t s);
+int k8s_gemm_big_rope(const void* x, int ldx, const void* w, void* qkv, int ldq, int M, int N, int K, const int* pos,
+                      const float* cos_sin, const int* slots, void* kc, void* vc, int nq, int nkv, int BS, int var,
+                      hipStream_t s);
 int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          hipStream_t s);
 }
@@ -81,7 +84,8 @@ int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy
 // fuse: 1 -- a split-K o / down projection may leave its partials to the next norm;
 // 2 (gate_up, kinds 4 / 5 with one K split) -- the SwiGLU-epilogue form, which
 // writes act directly (gu is never written, no silu_mul launch);
-// 3 (qkv, kind 1) -- the skinny kernel's RoPE / KV-write epilogue (no rope_kv launch)
+// 3 (qkv, kind 1) -- the skinny kernel's RoPE / KV-write epilogue (no rope_kv launch);
+// 4 (qkv, kind 5) -- gemm_big's RoPE / KV-write epilogue (prefill sizes)
 struct K8sGemmSel {
   int kind, cfg, splits, fuse;
 };
@@ -140,15 +144,6 @@ struct K8sLlamaStep {
   // ar_fuse: the all-reduce + residual add + RMSNorm of each row-parallel output in
   // one launch (k8s_ar_addnorm_bf16) instead of all-reduce, then rmsnorm
   int ar_id, ar_mode, ar_fuse;
-  // TP overlap of the row-parallel all-reduces with their GEMMs (eager steps,
-  // fused all-reduce + add + RMSNorm, hipBLASLt o / down only): the o and down
-  // GEMMs run in ar_chunks row blocks on the step stream and each block's
-  // k8s_ar_addnorm_bf16 (mode ar_mode_c) on a side stream as soon as the block's
-  // GEMM is done, so block c's all-reduce overlaps block c+1's GEMM.  Rows are
-  // independent in both ops (the norm is per row), so any row split is exact.
-  // ar_chunks <= 1: off.  ar_overlap_serial: the same chunked issue on the step
-  // stream alone (A/B and the bit-identity test).
-  int ar_chunks, ar_mode_c, ar_overlap_serial;
 };
 
 namespace {
@@ -190,70 +185,6 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
   }
 }
 
-// Mixed steps (decode rows + prefill chunks): the prefill attention (MFMA-heavy)
-// may run on a side stream concurrently with the decode attention (HBM-bound),
-// both after the layer's RoPE / KV write and before its o projection; the
-// decode kernel then gets at most `overlap_grid` waves (one per SIMD at 1024)
-// so prefill waves can be resident beside it.  K8SRCA_ATTN_OVERLAP=1 enables it
-// (tools/overlap_probe.py measures the pair both ways).  Same kernels, same
-// work items, disjoint outputs: results are bit-identical either way.
-struct Overlap {
-  bool on = false;
-  int grid = 1024;
-  int dev = -1;
-  hipStream_t side = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-};
-
-// side stream + per-chunk events of the TP all-reduce overlap (calling thread's device)
-struct TpOverlap {
-  static constexpr int kMax = 8;
-  int dev = -1;
-  hipStream_t side = nullptr;
-  hipEvent_t done[kMax] = {}, join = nullptr;
-};
-
-bool tp_overlap_ready(TpOverlap& o) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (o.dev == dev && o.side) return true;
-  if (hipStreamCreateWithFlags(&o.side, hipStreamNonBlocking) != hipSuccess) return false;
-  for (int i = 0; i < TpOverlap::kMax; ++i)
-    if (hipEventCreateWithFlags(&o.done[i], hipEventDisableTiming) != hipSuccess) return false;
-  if (hipEventCreateWithFlags(&o.join, hipEventDisableTiming) != hipSuccess) return false;
-  o.dev = dev;
-  return true;
-}
-
-TpOverlap& tp_overlap_state() {
-  static thread_local TpOverlap o;
-  return o;
-}
-
-Overlap& overlap_state() {
-  static thread_local Overlap o;
-  const char* v = std::getenv("K8SRCA_ATTN_OVERLAP");  // read per step: A/B-able in one process
-  o.on = v && v[0] == '1';
-  const char* g = std::getenv("K8SRCA_ATTN_OVERLAP_GRID");
-  o.grid = g && std::atoi(g) > 0 ? std::atoi(g) : 1024;
-  return o;
-}
-
-// side stream + fork/join events of the calling thread's current device
-bool overlap_ready(Overlap& o) {
-  int dev = 0;
-  if (hipGetDevice(&dev) != hipSuccess) return false;
-  if (o.dev == dev && o.side) return true;
-  if (hipStreamCreateWithFlags(&o.side, hipStreamNonBlocking) != hipSuccess ||
-      hipEventCreateWithFlags(&o.fork, hipEventDisableTiming) != hipSuccess ||
-      hipEventCreateWithFlags(&o.join, hipEventDisableTiming) != hipSuccess) {
-    o.side = nullptr;
-    return false;
-  }
-  o.dev = dev;
-  return true;
-}
-
 }  // namespace
 
 #define K8S_TRY(call)          \
@@ -261,36 +192,6 @@ bool overlap_ready(Overlap& o) {
     const int rc_ = (call);    \
     if (rc_) return rc_;       \
   } while (0)
-
-// Row-parallel projection out = x . w^T (hipBLASLt) + all-reduce + residual
-// add + RMSNorm (k8s_ar_addnorm_bf16 into y), in s.ar_chunks row blocks with
-// each block's all-reduce on the side stream behind its GEMM (see K8sLlamaStep).
-static long g_tp_chunked_calls = 0;  // chunked projections issued (tests check the path ran)
-
-static int tp_chunked_ar_norm(const K8sLlamaStep& s, TpOverlap& ov, const uint16_t* x, int ldx, const void* w, int K,
-                              uint16_t* out, const void* norm_w, hipStream_t st) {
-  const int T = s.T, H = s.H, nc = s.ar_chunks;
-  const bool par = !s.ar_overlap_serial;
-  hipStream_t side = par ? ov.side : st;
-  for (int c = 0; c < nc; ++c) {
-    const int r0 = (int)((long)T * c / nc), r1 = (int)((long)T * (c + 1) / nc);
-    if (r1 <= r0) continue;
-    const int rc = k8s_blaslt_gemm(x + (size_t)r0 * ldx, ldx, w, out + (size_t)r0 * H, H, r1 - r0, H, K, s.blaslt_ws,
-                                   s.blaslt_ws_bytes, st);
-    if (rc) return rc;
-    if (par) {
-      if (hipEventRecord(ov.done[c], st) != hipSuccess || hipStreamWaitEvent(side, ov.done[c], 0) != hipSuccess)
-        return (int)hipErrorUnknown;
-    }
-    const int ra = k8s_ar_addnorm_bf16(s.ar_id, out + (size_t)r0 * H, (uint16_t*)s.residual + (size_t)r0 * H, norm_w,
-                                       (uint16_t*)s.y + (size_t)r0 * H, r1 - r0, H, s.eps, s.ar_mode_c, side);
-    if (ra) return ra;
-  }
-  ++g_tp_chunked_calls;
-  if (par && (hipEventRecord(ov.join, side) != hipSuccess || hipStreamWaitEvent(st, ov.join, 0) != hipSuccess))
-    return (int)hipErrorUnknown;
-  return 0;
-}
 
 // Layers [0, L): on return `y` holds nothing useful and `prev` + `residual`
 // are the inputs of the final norm (exactly as after the Python loop).
@@ -309,16 +210,6 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   const bool tp = s.ar_id >= 0;  // row-parallel outputs are partial sums: all-reduce, never defer split-K
   const bool fuse_an = tp && s.ar_fuse;  // the previous layer's down all-reduce already produced y
   const long n_out = (long)T * H;
-  Overlap& ov = overlap_state();
-  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-  const bool capturing = !(hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone);
-  // never inside a graph capture (decode-only steps are the captured ones anyway)
-  const bool ov_ok = ov.on && nd > 0 && nd < T && !capturing && overlap_ready(ov);
-  TpOverlap& tov = tp_overlap_state();
-  // chunked TP all-reduce overlap: eager steps, fused epilogue, library GEMMs for o and down
-  const bool tp_chunk = fuse_an && s.ar_chunks > 1 && s.ar_chunks <= TpOverlap::kMax && !capturing &&
-                        (s.ar_overlap_serial || tp_overlap_ready(tov));
-  const bool chunk_o = tp_chunk && s.sel[1].kind == 0, chunk_d = tp_chunk && s.sel[3].kind == 0;
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
       K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
@@ -335,6 +226,9 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st, true));
       K8S_TRY(k8s_splitk_rope_kv(part_of(s, s.sel[0]), s.sel[0].splits, qkv, ld_qkv, s.pos, s.cos_sin, s.slots,
                                  s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
+    } else if (s.sel[0].kind == 5 && s.sel[0].fuse == 4) {  // prefill-size qkv, RoPE / KV write in the epilogue
+      K8S_TRY(k8s_gemm_big_rope(s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, s.pos, s.cos_sin, s.slots, s.kc[l],
+                                s.vc[l], s.nq, s.nkv, s.BS, s.sel[0].cfg, st));
     } else if (s.sel[0].kind == 1 && s.sel[0].fuse == 3) {  // skinny qkv with the RoPE / KV-write epilogue
       K8S_TRY(k8s_gemm_skinny_rope(s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, s.pos, s.cos_sin, s.slots, s.kc[l],
                                    s.vc[l], s.nq, s.nkv, s.BS, st));
@@ -343,31 +237,17 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(k8s_rope_kv(qkv, ld_qkv, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
     }
     const bool dec = nd > 0 && s.d_bt, pre = nd < T && s.p_bt;
-    const bool conc = dec && pre && ov.on && ov_ok;
-    if (conc) {  // prefill attention on the side stream, joined before the o projection
-      K8S_TRY((int)hipEventRecord(ov.fork, st));
-      K8S_TRY((int)hipStreamWaitEvent(ov.side, ov.fork, 0));
-    }
     if (pre)
       K8S_TRY(k8s_attn_prefill(qkv + (size_t)nd * ld_qkv, ld_qkv, s.kc[l], s.vc[l], s.p_bt, s.p_bt_stride, s.p_ctx,
                                s.p_qs, s.tile[0], s.tile[1], s.tile[2], s.tile[3], s.tile[4], s.tile[5], s.n_tiles,
                                s.merge[0], s.merge[1], s.merge[2], s.merge[3], s.n_merge, s.pf_o, s.pf_ml, s.nq,
-                               s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, conc ? ov.side : st));
-    if (conc) K8S_TRY((int)hipEventRecord(ov.join, ov.side));
+                               s.nkv, s.BS, s.scale, attn + (size_t)nd * qd, qd, st));
     if (dec)
       K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
                               s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,
-                              s.d_items, s.d_n_items, s.d_n_items_dev,
-                              conc ? (s.d_grid < ov.grid ? s.d_grid : ov.grid) : s.d_grid, st));
-    if (conc) K8S_TRY((int)hipStreamWaitEvent(st, ov.join, 0));
-    if (chunk_o) {
-      K8S_TRY(tp_chunked_ar_norm(s, tov, attn, qd, s.wo[l], qd, (uint16_t*)s.obuf, s.post_norm[l], st));
-    } else {
-      K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
-    }
-    if (chunk_o) {
-      // all-reduce + residual add + post-attention norm done above, per row block
-    } else if (fuse_an)
+                              s.d_items, s.d_n_items, s.d_n_items_dev, s.d_grid, st));
+    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
+    if (fuse_an)
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.obuf, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode, st));
     else if (tp)
       K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
@@ -388,11 +268,6 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     }
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
-    if (chunk_d && l + 1 < s.L) {  // the next layer's input norm rides on the chunked all-reduces
-      K8S_TRY(tp_chunked_ar_norm(s, tov, (const uint16_t*)s.act, s.I, s.wdown[l], s.I, (uint16_t*)s.prev,
-                                 s.in_norm[l + 1], st));
-      continue;
-    }
     K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));
     if (fuse_an && l + 1 < s.L)  // the next layer's input norm rides on this all-reduce
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.prev, s.residual, s.in_norm[l + 1], s.y, T, H, s.eps, s.ar_mode, st));
@@ -403,5 +278,3 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
 }
 
 K8S_API int k8s_llama_step_size() { return (int)sizeof(K8sLlamaStep); }
-
-K8S_API long k8s_llama_tp_chunked_calls() { return g_tp_chunked_calls; }

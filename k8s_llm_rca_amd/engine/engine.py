@@ -99,12 +99,6 @@ class EngineConfig:
     kv_mem_fraction: float = 0.85
     kv_max_gb: Optional[float] = None
     max_batch_tokens: int = 8192
-    # time hipBLASLt's top solutions per projection at a ladder of prefill M
-    # at init (ops/linear.py tune_lib_gemms).  Off: measured 6.34 -> 6.10
-    # analyses/s on the headline config -- a solution tuned at a ladder M is
-    # slower than the heuristic's own pick at the M between ladder points
-    # (profiles/r1_blaslt_tune_8b.txt)
-    tune_lib_gemms: bool = field(default_factory=lambda: os.environ.get("K8SRCA_BLASLT_TUNE", "0") == "1")
     max_decode_seqs: int = 256
     # prompt prefill batching: while decode rows are running, a new run's prompt
     # waits (at most prefill_max_defer_s after its submit) until the waiting
@@ -223,11 +217,6 @@ class LLMEngine:
             gemm_tuning.load(self.mc.name, self.pc.tp_size)
             LIN.reserve_lib_workspace(self.device)
             self.lib_algos = LIN.load_lib_algos(LIN.lib_algos_path(self.mc.name, self.pc.tp_size))
-            if cfg.tune_lib_gemms:  # measured hipBLASLt solutions for prefill-sized M
-                t_tune = time.perf_counter()
-                self.gemm_tuning = LIN.tune_lib_gemms(self.device, LIN.projection_shapes(self.mc, self.pc.tp_size),
-                                                      max_m=cfg.max_batch_tokens)
-                self.t_gemm_tune = time.perf_counter() - t_tune
             self.gemm_dispatch = LIN.load_dispatch(LIN.dispatch_path(self.mc.name, self.pc.tp_size))
             # prefill-size M ranges where the hand-written gemm_big beats hipBLASLt
             self.big_gemm_ranges = LIN.load_big(LIN.big_path(self.mc.name, self.pc.tp_size))

@@ -70,7 +70,7 @@ class MoELayerSet:
         out_perm = self.experts(li, x_perm, offsets)
         return M.combine(out_perm, inv, topk_w, T, self.k)
 
-    GROUPED_MAX_ROWS = 2048  # above: per-expert hipBLASLt (433 vs ~1100 TF at 8k rows, MI355X)
+    GROUPED_MAX_ROWS = 2048  # above: the grouped 8-phase GEMM (gemm_big.hip) -- SwiGLU fused, no host sync
     # split-K of the grouped down projection (tools/bench_kernels.py --what
     # moe_split, Mixtral shapes): 237 -> 161-185 us (5.8 TB/s) at <= 512 rows,
     # 264 -> 305 / 485 -> 442 us at 1024 / 2048 rows with 2 slices
@@ -82,6 +82,7 @@ class MoELayerSet:
     # split-K grouped kernel and stays there; at 512 rows the grouped kernel wins
     # (tools/bench_kernels.py --what moe_glds, profiles/r2_moe_glds.txt)
     GLDS_MAX_ROWS = int(os.environ.get("K8S_MOE_GLDS_MAX_ROWS", "384"))  # 0 disables (A/B)
+    BIG_PREFILL = os.environ.get("K8SRCA_MOE_BIG", "1") == "1"  # 0: per-expert hipBLASLt (A/B)
     GLDS_UP = (13, 1)
 
     def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor,
@@ -93,7 +94,20 @@ class MoELayerSet:
         for the offsets but run near the MFMA roof.  ``device_offsets``: the
         grouped kernels whatever the row count (the EP dispatch buffer holds
         ``ep``-fold capacity rows, most of them the never-computed null
-        expert: a host read of the offsets would stall every prefill layer)."""
+        expert: a host read of the offsets would stall every prefill layer).
+
+        Prefill-sized batches run the grouped form of the 8-phase prefill GEMM
+        (``ops/moe.py grouped_big``): gate_up with its SwiGLU epilogue, then
+        down, two launches over every expert with the offsets read on the
+        device -- no ``offsets.tolist()`` host sync per layer, no
+        silu_mul launch.  The per-expert hipBLASLt loop remains only for shapes
+        that kernel does not take."""
+        H = x_perm.shape[1]
+        I = self.w2[li].shape[2]
+        if (x_perm.is_cuda and x_perm.shape[0] > self.GROUPED_MAX_ROWS and self.BIG_PREFILL
+                and M.grouped_big_ok(x_perm.shape[0], I, H, True) and M.grouped_big_ok(x_perm.shape[0], H, I, False)):
+            act = M.grouped_big(x_perm, self.w13[li], offsets, silu=True)
+            return M.grouped_big(act, self.w2[li], offsets)
         if x_perm.is_cuda and x_perm.shape[0] > self.GROUPED_MAX_ROWS and not device_offsets:
             offs = offsets.tolist()
             out = torch.empty_like(x_perm)

@@ -41,6 +41,8 @@ _SIGS = {
     "k8s_gemm_big": [P, I, P, P, I, I, I, I, I, I, P],
     "k8s_gemm_big_split": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_gemm_big_part": [P, I, P, P, I, I, I, I, I, I, P, P],
+    "k8s_gemm_big_grouped": [P, I, P, P, I, P, I, I, I, I, I, I, P],
+    "k8s_gemm_big_rope": [P, I, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_gemm_big_ws_bytes": [],
     "k8s_gemm_big_set_ws": [P],
     "k8s_gemm_stream_silu": [P, I, P, P, I, I, I, I, I, P],

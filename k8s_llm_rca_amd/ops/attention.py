@@ -116,10 +116,14 @@ def linear_rope_kv(y: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, co
                                              ptr(cos_sin), ptr(slots), ptr(k_cache), ptr(v_cache), nq, nkv, BS,
                                              stream_ptr(y)), "gemm_skinny_rope")
             return qkv
-        if kind in (LIN.KIND_STREAM, LIN.KIND_MID) and splits > 1:
+        if layout and N == (nq + 2 * nkv) * HEAD_DIM and LIN.rope_choice(M, N, K):
+            # the prefill-size qkv GEMM with RoPE + the paged KV write in its epilogue
+            return LIN.gemm_big_rope(y, w, positions, cos_sin, slots, k_cache, v_cache, nq, nkv)
+        if kind in (LIN.KIND_STREAM, LIN.KIND_MID, LIN.KIND_BIG) and splits > 1:
             qkv = torch.empty((M, N), dtype=y.dtype, device=y.device)
             part = LIN._scratch(y.device, splits * M * N)
-            fn = lib().k8s_gemm_stream_part if kind == LIN.KIND_STREAM else lib().k8s_gemm_mid_part
+            fn = {LIN.KIND_STREAM: lib().k8s_gemm_stream_part, LIN.KIND_MID: lib().k8s_gemm_mid_part,
+                  LIN.KIND_BIG: lib().k8s_gemm_big_part}[kind]
             check(fn(ptr(y), y.stride(0), ptr(w), ptr(qkv), N, M, N, K, cfg, splits, ptr(part), stream_ptr(y)),
                   "qkv gemm (split-K partials)")
             BS = k_cache.shape[2]

@@ -43,7 +43,6 @@ class LlamaStep(ctypes.Structure):
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
         ("ar_id", I), ("ar_mode", I), ("ar_fuse", I),
-        ("ar_chunks", I), ("ar_mode_c", I), ("ar_overlap_serial", I),
     ]
 
 
@@ -52,23 +51,10 @@ _enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
 _fuse_ar_norm = os.environ.get("K8SRCA_TP_FUSED_NORM", "1") == "1"
 # split-K o / down projections reduced inside the following residual add + RMSNorm
 _fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
-# TP: eager steps of >= TP_OVERLAP_MIN_ROWS rows run the o / down GEMMs in
-# TP_OVERLAP_CHUNKS row blocks, each block's fused all-reduce + add + RMSNorm on
-# a side stream behind its GEMM (overlapping the next block's GEMM).
-# K8SRCA_TP_OVERLAP: 1 on, 0 off (default), "serial" the same chunks on one stream.
-# Off by default: rank 0 of a 70B TP=8 engine on one MI355X (bench.py --tp-sim 8,
-# the xGMI kernels on a loopback communicator) ran 3.68 analyses/s with it vs
-# 4.09 without (profiles/r3/ab/tp_overlap_*_tpsim70b.json): half-M hipBLASLt
-# calls lose more than the side-stream all-reduce hides, and the all-reduce
-# kernel's waves compete with the GEMM for the same CUs.
-_tp_overlap = os.environ.get("K8SRCA_TP_OVERLAP", "0")
-TP_OVERLAP_CHUNKS = int(os.environ.get("K8SRCA_TP_OVERLAP_CHUNKS", "2"))
-TP_OVERLAP_MIN_ROWS = int(os.environ.get("K8SRCA_TP_OVERLAP_MIN_ROWS", "512"))
-
-
-def set_tp_overlap(mode: str) -> None:
-    global _tp_overlap
-    _tp_overlap = mode
+# (Round 3 also carried a row-chunked o / down GEMM with each chunk's
+# all-reduce on a side stream, and the prefill attention on a side stream beside
+# the decode attention: both measured as losses -- profiles/r3/ab/tp_overlap_*,
+# profiles/r3/overlap/ -- and were retired from the executor in round 4.)
 _checked = False
 
 
@@ -171,10 +157,6 @@ class LlamaExecutor:
             st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
             # the two-shot epilogue splits each row's 16-B chunks evenly over the ranks
             st.ar_fuse = int(_fuse_ar_norm and (st.ar_mode == 1 or (H // 8) % self._car.world == 0))
-            nc = TP_OVERLAP_CHUNKS if _tp_overlap != "0" and T >= TP_OVERLAP_MIN_ROWS else 1
-            st.ar_chunks = nc
-            st.ar_mode_c = 1 if (T + nc - 1) // nc * H * 2 <= ONE_SHOT_MAX else 2
-            st.ar_overlap_serial = int(_tp_overlap == "serial")
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)
@@ -213,6 +195,9 @@ class LlamaExecutor:
             st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
             if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):
                 st.sel[i].fuse = 3  # RoPE + KV write in the qkv GEMM's epilogue
+            elif i == 0 and N == (m.nq + 2 * m.nkv) * m.D and LIN.rope_choice(T, N, K):
+                st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = LIN.KIND_BIG, LIN.BIG_PIPE, 1
+                st.sel[i].fuse = 4  # gemm_big's RoPE + KV-write epilogue
             if kind in (LIN.KIND_MID, LIN.KIND_STREAM, LIN.KIND_BIG) and splits > 1:
                 need_mid = max(need_mid, splits * T * N)
             elif kind == LIN.KIND_GRP:

@@ -159,17 +159,10 @@ def reserve_big_ws(dev: torch.device, enable: bool = None) -> None:
         check(lib().k8s_gemm_big_set_ws(ptr(t)), "gemm_big_set_ws")
 
 
-# ------------------------------------------------ hipBLASLt solution tuning
-# Prefill-sized projections (M >= 256) always run on hipBLASLt (the hand-written
-# kernels lose there: profiles/r1_prefill_gemm_sweep.txt).  The heuristic's
-# first solution is not always the fastest it lists at these M, so at engine
-# init each projection (N, K) is timed at a ladder of M over the heuristic's top
-# candidates and the fastest is kept natively (csrc/kernels/blaslt.hip); any
-# later M uses the solution tuned at the largest ladder M <= M.  Off by default
-# (EngineConfig.tune_lib_gemms): end to end it lost 4 % on the headline config.
-TUNE_LADDER = (256, 384, 512, 768, 1024, 1536, 2048, 3072, 4096, 6144, 8192)
-_tuned_report: List[tuple] = []
-_tuned_done: set = set()
+# ------------------------------------------------ hipBLASLt solution tables
+# (Engine-init tuning of hipBLASLt solutions over an M ladder lost 4 % end to
+# end -- profiles/r1_blaslt_tune_8b.txt -- and was retired in round 4; the
+# bucketed table below, verified per bucket, stays.)
 
 
 def projection_shapes(mc, tp: int = 1) -> List[Tuple[int, int]]:
@@ -179,43 +172,6 @@ def projection_shapes(mc, tp: int = 1) -> List[Tuple[int, int]]:
     out = [(qkv, H), (H, mc.n_heads * mc.head_dim // tp)]
     if not getattr(mc, "n_experts", 0):
         out += [(2 * I // tp, H), (H, I // tp)]
-    return out
-
-
-def tune_lib_gemms(dev: torch.device, shapes, max_m: int = 8192, max_algos: int = 24, iters: int = 5) -> List[tuple]:
-    """Time hipBLASLt's top ``max_algos`` solutions for every (N, K) in
-    ``shapes`` at each ladder M <= ``max_m`` and keep the fastest (native
-    table).  Call before any HIP-graph capture.  Returns
-    ``[(M, N, K, heuristic_us, tuned_us, rank)]``."""
-    import ctypes
-    if not (_native_lib_gemm and dev.type == "cuda"):
-        return []
-    reserve_lib_workspace(dev)
-    ws = _blaslt_ws[dev]
-    out = []
-    times = (ctypes.c_float * 2)()
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0)
-    for N, K in shapes:
-        w = torch.randn(N, K, device=dev, dtype=torch.bfloat16, generator=gen) * 0.02
-        for M in TUNE_LADDER:
-            if M > max_m:
-                break
-            if (dev, M, N, K) in _tuned_done:  # an earlier engine in this process
-                continue
-            _tuned_done.add((dev, M, N, K))
-            x = torch.randn(M, K, device=dev, dtype=torch.bfloat16, generator=gen)
-            y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-            torch.cuda.synchronize(dev)
-            rank = lib().k8s_blaslt_tune(ptr(x), K, ptr(w), ptr(y), N, M, N, K, ptr(ws), BLASLT_WS_BYTES, max_algos,
-                                         iters, stream_ptr(x), times)
-            if rank < 0:
-                raise RuntimeError(f"k8s_blaslt_tune({M}, {N}, {K}) failed: {rank}")
-            out.append((M, N, K, round(times[0], 2), round(times[1], 2), rank))
-            del x, y
-        del w
-    torch.cuda.synchronize(dev)
-    _tuned_report[:] = out
     return out
 
 
@@ -262,8 +218,6 @@ def load_lib_algos(path: str) -> int:
 
 def clear_lib_tuning() -> None:
     lib().k8s_blaslt_clear_tuning()
-    _tuned_report.clear()
-    _tuned_done.clear()
 
 
 # ------------------------------------------------------- measured dispatch
@@ -412,13 +366,49 @@ def load_big(path: str) -> int:
     with open(path) as f:
         d = json.load(f)
     n = 0
-    for tag, silu in (("ranges", False), ("silu", True)):
+    for tag in ("ranges", "silu", "rope"):
         for key, rows in d.get(tag, {}).items():
             N, K = (int(v) for v in key.split(","))
-            _big_ranges[("silu", N, K) if silu else (N, K)] = [
+            _big_ranges[(tag, N, K) if tag != "ranges" else (N, K)] = [
                 (int(r[0]), int(r[1]), int(r[2]) if len(r) > 2 else 1) for r in rows]
             n += len(rows)
     return n
+
+
+def rope_choice(M: int, N: int, K: int) -> bool:
+    """The qkv projection of M rows on gemm_big with its RoPE + paged KV-write
+    epilogue (data file table ``rope``: measured against hipBLASLt +
+    k8s_rope_kv)?  ``K8SRCA_BIG_GEMM=all`` takes it wherever the shape fits."""
+    if _big_mode == "0" or M <= DISPATCH_MAX_M or not big_shape_ok(M, N, K):
+        return False
+    if _big_mode == "all":
+        return True
+    return any(lo <= M <= hi for lo, hi, _ in _big_ranges.get(("rope", N, K), ()))
+
+
+def gemm_big_rope(x: torch.Tensor, w: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Tensor,
+                  slots: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, nq: int, nkv: int,
+                  out: torch.Tensor = None, pipe: int = None) -> torch.Tensor:
+    """``qkv = x @ w.T`` with q, k rotated and k, v written to their pages in
+    the GEMM's epilogue (csrc/kernels/gemm_big.hip MODE 2): bit-identical to
+    :func:`gemm_big` + ``ops.attention.rope_kv_write``, one launch and one
+    pass over qkv fewer."""
+    M, K = x.shape
+    N = w.shape[0]
+    assert N == (nq + 2 * nkv) * 128 and big_shape_ok(M, N, K) and x.stride(1) == 1 and w.is_contiguous()
+    assert positions.dtype == torch.int32 and cos_sin.dtype == torch.float32
+    assert slots is None or slots.dtype == torch.int32
+    if out is None:
+        out = torch.empty((M, N), dtype=x.dtype, device=x.device)
+    if M == 0:
+        return out
+    if x.device not in _big_ws and _big_tail:
+        reserve_big_ws(x.device)
+    BS = k_cache.shape[2]
+    check(lib().k8s_gemm_big_rope(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), M, N, K, ptr(positions),
+                                  ptr(cos_sin), ptr(slots), ptr(k_cache), ptr(v_cache), nq, nkv, BS,
+                                  BIG_PIPE if pipe is None else pipe, stream_ptr(x)), "gemm_big_rope")
+    return out
 
 
 def big_scratch_elems() -> int:

@@ -100,6 +100,33 @@ def grouped_gemm(a: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, fuse_s
     return out
 
 
+def grouped_big_ok(rows: int, N: int, K: int, silu: bool) -> bool:
+    """What the grouped form of csrc/kernels/gemm_big.hip accepts."""
+    return rows > 0 and K % 128 == 0 and N % (128 if silu else 256) == 0
+
+
+def grouped_big(x: torch.Tensor, w: torch.Tensor, offsets: torch.Tensor, silu: bool = False,
+                out: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """B13 at prefill sizes on the 8-phase MFMA GEMM (csrc/kernels/gemm_big.hip,
+    grouped form): rows offsets[e]..offsets[e+1] of ``x`` times ``w[e]^T`` in one
+    launch with the offsets read on the device (no host sync, capturable).
+    ``silu``: ``w`` [E, 2I, K] is the gate_up weight (gate rows first) and the
+    result is the SwiGLU activation [rows, I] -- gate_up is never written."""
+    from .linear import BIG_PIPE
+    E, Nw, K = w.shape
+    N = Nw // 2 if silu else Nw
+    rows = x.shape[0]
+    if out is None:
+        out = torch.empty(rows, N, dtype=x.dtype, device=x.device)
+    if rows == 0:
+        return out
+    assert x.dtype == torch.bfloat16 and w.is_contiguous() and x.stride(1) == 1 and x.shape[1] == K
+    assert offsets.dtype == torch.int32 and offsets.is_cuda and grouped_big_ok(rows, N, K, silu)
+    check(lib().k8s_gemm_big_grouped(ptr(x), x.stride(0), ptr(w), ptr(out), out.stride(0), ptr(offsets), E, rows, N,
+                                     K, int(silu), BIG_PIPE, stream_ptr(x)), "gemm_big_grouped")
+    return out
+
+
 _scratch = {}
 
 

@@ -247,59 +247,6 @@ def test_paged_decode_multi_token_items(nq, nkv):
     assert torch.equal(outs[0][0], outs[1][0])
 
 
-@pytest.mark.parametrize("nq,nkv", [(32, 8), (64, 8), (8, 1)])
-def test_decode_in_kernel_merge_matches_reduce(nq, nkv, monkeypatch):
-    """K8SRCA_DECODE_MERGE=1: the last wave of each (row group, kv head) merges
-    the split-KV partials inside the decode kernel instead of the reduce
-    launch -- the same rows to 1 bf16 ulp (single rows and multi-token
-    groups), over repeated launches (the arrival counters reset themselves)."""
-    _need_gpu()
-    torch.manual_seed(5)
-    BS = 64
-    runs = [(1000, 6), (254, 6), (60, 3), (5000, 4), (17, 1), (1535, 5), (4700, 1), (3100, 1)]
-    ctx, seq_of, chain = [], [], []
-    for i, (c0, q) in enumerate(runs):
-        for j in range(q):
-            ctx.append(c0 + j + 1)
-            seq_of.append(i)
-            chain.append(j > 0)
-    S = len(ctx)
-    NB = sum((c0 + q + BS - 1) // BS for c0, q in runs) + 4
-    kc, vc = _setup_cache(nkv, BS, NB, dev)
-    perm = torch.randperm(NB)
-    maxb = max((c + BS - 1) // BS for c in ctx)
-    bt_seq, used = [], 0
-    for c0, q in runs:
-        nb = (c0 + q + BS - 1) // BS
-        row = torch.zeros(maxb, dtype=torch.int32)
-        row[:nb] = perm[used:used + nb].int()
-        used += nb
-        bt_seq.append(row)
-    bt = torch.stack([bt_seq[i] for i in seq_of])
-    q = torch.randn(S, (nq + 2 * nkv) * 128, device=dev).bfloat16()
-    scale = 1 / math.sqrt(128)
-    for ch, part in ((None, 256), (np.asarray(chain), 256), (None, None)):
-        meta = A.AttnMeta(block_tables=bt.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
-                          q_start=torch.arange(S + 1, dtype=torch.int32, device=dev), num_seqs=S, decode=True,
-                          ctx_lens_host=list(ctx), q_start_host=list(range(S + 1)))
-        A.attach_decode_plan(meta, ctx, nq, nkv, BS, dev, part=part, chain=ch)
-        assert meta.n_parts > 1
-        monkeypatch.setenv("K8SRCA_DECODE_MERGE", "0")
-        ref = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
-        monkeypatch.setenv("K8SRCA_DECODE_MERGE", "1")
-        for grid in (None, 64):  # 64 waves: many items (and tickets) per wave
-            meta.grid_waves = grid or 0
-            for _ in range(3):
-                got = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
-                torch.cuda.synchronize()
-                # same merge arithmetic in the same order; the partials come from a
-                # separately compiled instantiation of the decode kernel, whose
-                # softmax bookkeeping may round differently: allow 1 bf16 ulp
-                torch.testing.assert_close(got.float(), ref.float(), atol=1e-6, rtol=2.0 ** -7)
-                assert (got != ref).float().mean() < 0.01
-    monkeypatch.setenv("K8SRCA_DECODE_MERGE", "0")
-
-
 @pytest.mark.parametrize("BS", [64, 32])  # 64: paged-64 32x32x16 kernel; 32: generic kernel
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
 @pytest.mark.parametrize("ctx,qlen", [([7], [7]), ([300, 40], [300, 13]), ([1500, 90, 33], [64, 90, 1]),
@@ -647,27 +594,6 @@ def test_grouped_gemm_matches_per_expert(E, N, K, fuse, splits):
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
 
 
-def test_blaslt_tuned_solutions():
-    """Measured hipBLASLt solutions (k8s_blaslt_tune): the tuned table serves
-    M on and between ladder points, results match fp32, and below the ladder
-    (decode sizes) the heuristic's plan is used."""
-    _need_gpu()
-    from k8s_llm_rca_amd.ops import linear as LIN
-    torch.manual_seed(11)
-    N, K = 1536, 2048
-    rep = LIN.tune_lib_gemms(torch.device(dev), [(N, K)], max_m=512, max_algos=8, iters=2)
-    assert [r[0] for r in rep] == [256, 384, 512]
-    assert all(r[4] <= r[3] + 1e-3 and r[5] >= 0 for r in rep)
-    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
-    try:
-        for M in (64, 256, 300, 512, 777):
-            x = torch.randn(M, K, device=dev).bfloat16()
-            y = LIN.lib_gemm(x, w)
-            torch.testing.assert_close(y.float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
-    finally:
-        LIN.clear_lib_tuning()
-
-
 def test_blaslt_bucket_registration(monkeypatch):
     """A solution registered for M in [lo, hi] (k8s_blaslt_set_algo_range: the
     heuristic's own pick at another M) serves that range only; results inside
@@ -737,6 +663,40 @@ def test_grouped_glds_matches_per_expert(E, N, K, cfg, splits):
     got = MO.grouped_gemm(a.to(dev), w.to(dev), offs.to(dev), splits=splits, glds=cfg).float().cpu()
     ref = MO.grouped_gemm(a, w, offs).float()
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
+
+
+@pytest.mark.parametrize("E,N,K,silu", [(8, 512, 512, False), (8, 384, 1024, True), (2, 256, 2048, True),
+                                        (4, 1024, 256, False)])
+@pytest.mark.parametrize("pad", [0, 300])
+@pytest.mark.parametrize("var", [1, 5])
+def test_grouped_big_matches_per_expert(E, N, K, silu, pad, var, monkeypatch):
+    """The grouped form of the 8-phase prefill GEMM (gemm_big.hip): device
+    offsets, empty experts, experts of 1 row and of several 256-row tiles,
+    rows past offsets[E] (the EP capacity padding: never read or written),
+    plain and SwiGLU-epilogue forms == per-expert fp32."""
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops import moe as MO
+    _need_gpu()
+    monkeypatch.setattr(LIN, "BIG_PIPE", var)
+    torch.manual_seed(E * 7 + N + pad)
+    counts = torch.tensor([0, 700, 1, 260, 255, 0, 513, 90][:E])
+    offs = torch.zeros(E + 1, dtype=torch.int32)
+    offs[1:] = torch.cumsum(counts, 0)
+    rows = int(offs[-1]) + pad
+    a = (torch.randn(rows, K) * 0.5).bfloat16()
+    w = (torch.randn(E, 2 * N if silu else N, K) / K ** 0.5).bfloat16()
+    out = torch.full((rows, N), 7.0, device=dev).bfloat16()
+    got = MO.grouped_big(a.to(dev), w.to(dev), offs.to(dev), silu=silu, out=out).float().cpu()
+    ref = torch.empty(rows, N)
+    for e in range(E):
+        lo, hi = int(offs[e]), int(offs[e + 1])
+        y = a[lo:hi].float() @ w[e].float().t()
+        if silu:
+            y = torch.nn.functional.silu(y[:, :N]) * y[:, N:]
+        ref[lo:hi] = y
+    n = int(offs[-1])
+    torch.testing.assert_close(got[:n], ref[:n], atol=3e-2, rtol=3e-2)
+    assert bool((got[n:] == 7.0).all())  # padding rows untouched
 
 
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
@@ -842,7 +802,7 @@ def test_sampling_top_p_and_tie_candidates_deterministic():
     assert bool((ids >= 16032).all()) and bool((ids[:, 1:] > ids[:, :-1]).all())  # valid, (v desc, id asc)
 
 
-@pytest.mark.parametrize("pipe", [3, 0, 1, 2])
+@pytest.mark.parametrize("pipe", [1, 3, 5, 7])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 128), (100, 512, 128), (256, 1024, 4096), (300, 768, 384),
                                    (1000, 6144, 512), (1300, 768, 256), (2085, 4096, 1024), (4096, 256, 14336)])
 def test_gemm_big_vs_fp32(M, N, K, pipe):
@@ -872,15 +832,50 @@ def test_gemm_big_vs_fp32(M, N, K, pipe):
     assert torch.count_nonzero(yb[:, N:]) == 0
 
 
+@pytest.mark.parametrize("var", [1, 5])
+@pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 8)])
+@pytest.mark.parametrize("M", [5, 700, 4100])
+def test_gemm_big_rope_kv_epilogue_bit_identical(M, nq, nkv, var, monkeypatch):
+    """gemm_big's qkv form with RoPE + the paged KV write in the epilogue ==
+    gemm_big + k8s_rope_kv bit for bit: the qkv buffer (q, k rotated; v), the
+    K pages and the (transposed) V pages, incl. rows with no slot (-1); and
+    within bf16 rounding of the fp32 reference."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    monkeypatch.setattr(LIN, "BIG_PIPE", var)
+    torch.manual_seed(M + nq)
+    K, BS = 512, 64
+    N = (nq + 2 * nkv) * 128
+    NB = (M + BS - 1) // BS + 3
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.05).bfloat16()
+    cs = A.rope_cos_sin(8192, 500000.0, device=dev)
+    pos = torch.randint(0, 8000, (M,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=dev)[:M].int()
+    slots[:: 7] = -1
+    kc0 = torch.randn(NB, nkv, BS, 128, device=dev).bfloat16()
+    vc0 = torch.randn(NB, nkv, 128, BS, device=dev).bfloat16()
+    kc1, vc1, kc2, vc2 = kc0.clone(), vc0.clone(), kc0.clone(), vc0.clone()
+    q1 = LIN.gemm_big(x, w)
+    A.rope_kv_write(q1, pos, cs, slots, kc1, vc1, nq, nkv)
+    q2 = LIN.gemm_big_rope(x, w, pos, cs, slots, kc2, vc2, nq, nkv)
+    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    ref = (x.float() @ w.float().t()).bfloat16()  # v is not rotated: the GEMM's own output
+    torch.testing.assert_close(q2[:, (nq + nkv) * 128:].float(), ref[:, (nq + nkv) * 128:].float(), atol=3e-2,
+                               rtol=2e-2)
+
+
+@pytest.mark.parametrize("var", [1, 5])
 @pytest.mark.parametrize("splits", [2, 4])
 @pytest.mark.parametrize("M,N,K", [(1, 256, 512), (1000, 512, 1024), (300, 768, 2048), (2085, 256, 14336)])
-def test_gemm_big_split_k_vs_fp32(M, N, K, splits):
+def test_gemm_big_split_k_vs_fp32(M, N, K, splits, var, monkeypatch):
     """gemm_big with K split over workgroups (fp32 partials [splits][M][N] +
     the slice-order reduce): fp32 reference, and the partials themselves sum
     to the reduced output."""
     _need_gpu()
     from k8s_llm_rca_amd.ops import linear as LIN
     from k8s_llm_rca_amd.ops._lib import check, lib, ptr, stream_ptr
+    monkeypatch.setattr(LIN, "BIG_PIPE", var)
     torch.manual_seed(M + N + K + splits)
     x = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
@@ -895,9 +890,10 @@ def test_gemm_big_split_k_vs_fp32(M, N, K, splits):
     assert torch.equal(acc.bfloat16(), y)
 
 
+@pytest.mark.parametrize("var", [1, 5])
 @pytest.mark.parametrize("M,N,K,silu", [(6144, 4096, 1024, False), (3072, 6144, 2048, False),
                                         (1300, 4352, 512, False), (2085, 1024, 1024, True)])
-def test_gemm_big_split_tail(M, N, K, silu):
+def test_gemm_big_split_tail(M, N, K, silu, var, monkeypatch):
     """Split tail (the partial last wave's tiles as K slices, the last arriver
     sums the fp32 partials in slice order): fp32 reference, run-to-run
     identical, and within bf16 rounding of the whole-tile path.  Tile counts:
@@ -905,6 +901,7 @@ def test_gemm_big_split_tail(M, N, K, silu):
     SwiGLU 72 (72 x 2)."""
     _need_gpu()
     from k8s_llm_rca_amd.ops import linear as LIN
+    monkeypatch.setattr(LIN, "BIG_PIPE", var)
     torch.manual_seed(M + N)
     x = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(2 * N if silu else N, K, device=dev) * 0.03).bfloat16()
@@ -925,7 +922,7 @@ def test_gemm_big_split_tail(M, N, K, silu):
     torch.testing.assert_close(y1.float(), y0.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("pipe", [3, 1])
+@pytest.mark.parametrize("pipe", [1, 5])
 @pytest.mark.parametrize("M,I,K", [(5, 128, 128), (300, 384, 512), (1500, 1024, 4096), (4100, 14336, 256)])
 def test_gemm_big_silu_epilogue(M, I, K, pipe):
     """SwiGLU epilogue of gemm_big (gate_up never written) == the unfused

@@ -62,6 +62,37 @@ def test_forward_gpu_matches_cpu(name):
     assert torch.equal(out.argmax(-1), ref.argmax(-1))
 
 
+def test_moe_prefill_no_host_sync():
+    """a Mixtral prefill-sized MoE layer (tiny-mixtral, 1,100
+    tokens x top-2 = 2,200 routed rows > GROUPED_MAX_ROWS) runs routing,
+    permutation, the grouped SwiGLU gate_up + down (gemm_big.hip grouped form)
+    and the combine with no host sync (torch's sync checker in error mode), and
+    matches the per-expert hipBLASLt path it replaced."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    cfg = get_config("tiny-mixtral")
+    m = LlamaModel(cfg, "cuda", torch.bfloat16, None, seed=4)
+    moe = m.moe
+    y = (torch.randn(1100, cfg.hidden, device="cuda") * 0.5).bfloat16()
+    torch.cuda.synchronize()
+    assert 1100 * moe.k > moe.GROUPED_MAX_ROWS
+    torch.cuda.set_sync_debug_mode("error")
+    try:
+        out = moe.forward(0, y)
+    finally:
+        torch.cuda.set_sync_debug_mode(0)
+    torch.cuda.synchronize()
+    moe.BIG_PREFILL = False
+    try:
+        ref = moe.forward(0, y)
+    finally:
+        moe.BIG_PREFILL = True
+    assert torch.isfinite(out.float()).all()
+    torch.testing.assert_close(out.float(), ref.float(), atol=2e-2, rtol=2e-2)
+
+
 def test_engine_graph_vs_eager_decode():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
@@ -188,43 +219,6 @@ def test_layer_executor_bit_identical(graphs, splitk):
     (r0, l0), (r1, l1) = runs
     assert r0 == r1
     assert len(l0) == len(l1) and len(l0) > 2
-    for a, b in zip(l0, l1):
-        assert torch.equal(a, b)
-
-
-def test_attention_overlap_bit_identical(monkeypatch):
-    """K8SRCA_ATTN_OVERLAP=1: in mixed steps the native executor runs the
-    prefill attention on a side stream beside the decode attention (decode at
-    a capped grid).  Same kernels and work items, disjoint outputs: every
-    step's logits are bit-identical to the serial order."""
-    if not torch.cuda.is_available():
-        pytest.skip("no GPU")
-    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
-    runs = []
-    for on in ("0", "1"):
-        monkeypatch.setenv("K8SRCA_ATTN_OVERLAP", on)
-        monkeypatch.setenv("K8SRCA_ATTN_OVERLAP_GRID", "64")  # a small grid: many items per wave
-        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=512, use_graphs=False,
-                                     temperature=0.0, max_batch_tokens=256))
-        logs = []
-        fwd = eng.model.forward
-
-        def rec(*a, **k):
-            out = fwd(*a, **k)
-            logs.append(out.float().cpu())
-            return out
-        eng.model.forward = rec
-        res = {}
-        for i in range(6):
-            sid = eng.new_sequence()
-            p = eng.tok.system_prefix("s") + eng.tok.message("user", "w%d " % i * (20 + 40 * i)) + \
-                eng.tok.header("assistant")
-            eng.submit(sid, p, None, 12, temperature=0.0, on_done=lambda g, st, i=i: res.__setitem__(i, g))
-        eng.run_until_idle()
-        assert eng.model._exec is not None
-        runs.append((res, logs))
-    (r0, l0), (r1, l1) = runs
-    assert r0 == r1 and len(l0) == len(l1) and len(l0) > 2
     for a, b in zip(l0, l1):
         assert torch.equal(a, b)
 

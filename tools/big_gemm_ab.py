@@ -45,15 +45,20 @@ def main():
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--iters", type=int, default=8)
     ap.add_argument("--layers", type=int, default=4)
-    ap.add_argument("--pipes", default="3,1")
+    ap.add_argument("--pipes", default="1,5")
     ap.add_argument("--out", default="")
     ap.add_argument("--splits", default="2,4", help="K splits tried for the plain form ('' = none)")
     ap.add_argument("--emit", default="")
     ap.add_argument("--margin", type=float, default=0.01)
+    ap.add_argument("--model", default="llama3-8b", help="projection shapes of this preset (per TP rank)")
+    ap.add_argument("--tp", type=int, default=1)
     a = ap.parse_args()
     dev = torch.device("cuda")
-    H, I = 4096, 14336
-    shapes = {"qkv": (6144, H), "o": (H, H), "gu": (2 * I, H), "down": (H, I)}
+    from k8s_llm_rca_amd.models.config import get_config
+    mc = get_config(a.model)
+    H, I, tp = mc.hidden, mc.intermediate // a.tp, a.tp
+    nq, nkv = mc.n_heads // tp, max(1, mc.n_kv_heads // tp)
+    shapes = {"qkv": ((nq + 2 * nkv) * mc.head_dim, H), "o": (H, nq * mc.head_dim), "gu": (2 * I, H), "down": (H, I)}
     pipes = [int(p) for p in a.pipes.split(",")]
     rows = []
     for name in a.shapes.split(","):
@@ -70,6 +75,20 @@ def main():
                 if LIN.big_shape_ok(M, N, K, splits=sp) and tiles < 256:
                     arms[f"big{pipes[0]}s{sp}"] = lambda i, sp=sp: LIN.gemm_big(x, ws[i % a.layers], y, pipe=pipes[0],
                                                                                 splits=sp)
+            if name == "qkv":  # the RoPE + paged KV-write epilogue vs hipBLASLt + k8s_rope_kv
+                from k8s_llm_rca_amd.ops import attention as A
+                BS = 64
+                cs = A.rope_cos_sin(8192, 500000.0, device=dev)
+                pos = torch.arange(M, device=dev, dtype=torch.int32) % 8192
+                slots = torch.arange(M, device=dev, dtype=torch.int32)
+                nb = (M + BS - 1) // BS
+                kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16)
+                vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16)
+                arms["blaslt+rope"] = lambda i: A.rope_kv_write(LIN.lib_gemm(x, ws[i % a.layers], y), pos, cs, slots,
+                                                                 kc, vc, nq, nkv)
+                for p in pipes:
+                    arms[f"big{p}_rope"] = lambda i, p=p: LIN.gemm_big_rope(x, ws[i % a.layers], pos, cs, slots, kc,
+                                                                            vc, nq, nkv, out=y, pipe=p)
             if name == "gu":
                 act = torch.empty(M, I, device=dev, dtype=torch.bfloat16)
                 arms["blaslt+silu"] = lambda i: NRM.silu_mul(LIN.lib_gemm(x, ws[i % a.layers], y), out=act)
@@ -102,25 +121,27 @@ def main():
 
 def emit(rows, path, margin):
     """Dispatch ranges from the measured rows (module docstring)."""
-    out = {"source": "tools/big_gemm_ab.py", "ranges": {}, "silu": {}}
+    out = {"source": "tools/big_gemm_ab.py", "ranges": {}, "silu": {}, "rope": {}}
     by = {}
     for r in rows:
         by.setdefault(r["shape"], []).append(r)
     for shape, rs in by.items():
         rs.sort(key=lambda r: r["M"])
         key = f'{rs[0]["N"]},{rs[0]["K"]}'
-        for tag, base, pref in (("ranges", "blaslt", "big"), ("silu", "blaslt+silu", "big")):
-            if tag == "silu" and shape != "gu":
+        for tag, base, pref in (("ranges", "blaslt", "big"), ("silu", "blaslt+silu", "big"),
+                                ("rope", "blaslt+rope", "big")):
+            if (tag == "silu" and shape != "gu") or (tag == "rope" and shape != "qkv"):
                 continue
             picks = []
             for r in rs:
+                suf = {"silu": "_silu", "rope": "_rope"}.get(tag)
                 arms = [k for k in r if k.startswith(pref) and not k.endswith("_tf")
-                        and (k.endswith("_silu") if tag == "silu" else not k.endswith("_silu"))]
+                        and (k.endswith(suf) if suf else not (k.endswith("_silu") or k.endswith("_rope")))]
                 if not arms or base not in r:
                     picks.append(None)
                     continue
                 best = min(arms, key=lambda k: r[k])
-                sp = int(best.split("s")[-1]) if "s" in best[3:] and tag != "silu" else 1
+                sp = int(best.split("s")[-1]) if "s" in best[3:] and tag == "ranges" else 1
                 picks.append(sp if r[best] <= r[base] * (1 - margin) else None)
             ranges = []
             for i, (r, sp) in enumerate(zip(rs, picks)):

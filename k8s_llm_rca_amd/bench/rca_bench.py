@@ -33,15 +33,32 @@ METRIC = "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-nod
 REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
 
 
-def _native_cpu() -> Dict[int, float]:
-    """CPU seconds per native (non-Python) thread of this process, by thread id."""
+def _native_cpu() -> Dict[int, tuple]:
+    """(user, system) CPU seconds per native (non-Python) thread of this
+    process, by thread id."""
     import threading
     try:
         import psutil
         py = {t.native_id for t in threading.enumerate()}
-        return {t.id: t.user_time + t.system_time for t in psutil.Process().threads() if t.id not in py}
+        return {t.id: (t.user_time, t.system_time) for t in psutil.Process().threads() if t.id not in py}
     except Exception:
         return {}
+
+
+def _native_detail(tid: int) -> Dict[str, Any]:
+    """What a busy native thread is doing, from /proc (no GPU call, no
+    ptrace): its name, kernel wait channel and current system call -- a thread
+    spinning in user space shows wchan 0 and mostly user time; one blocked in
+    the driver shows an ioctl / futex / poll."""
+    out: Dict[str, Any] = {"tid": tid}
+    for key, fn in (("comm", "comm"), ("wchan", "wchan"), ("syscall", "syscall")):
+        try:
+            with open(f"/proc/self/task/{tid}/{fn}") as f:
+                v = f.read().strip()
+            out[key] = v.split()[0] if key == "syscall" and v else v
+        except OSError:
+            pass
+    return out
 
 
 def _thread_cpu() -> Dict[str, float]:
@@ -265,7 +282,11 @@ def run(args) -> Optional[Dict[str, Any]]:
     ctx1 = backend.thread_stats()
     # the busiest native threads over the window (HIP runtime / torch pools: one
     # polling thread vs many pool workers)
-    native_top = sorted((round(v - ncpu0.get(t, 0.0), 2) for t, v in ncpu1.items()), reverse=True)
+    ndelta = {t: (u - ncpu0.get(t, (0.0, 0.0))[0], sy - ncpu0.get(t, (0.0, 0.0))[1])
+              for t, (u, sy) in ncpu1.items()}
+    native_top = sorted((round(u + sy, 2) for u, sy in ndelta.values()), reverse=True)
+    busiest = sorted(ndelta.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:2]
+    native_busiest = [dict(_native_detail(t), user_s=round(u, 2), sys_s=round(sy, 2)) for t, (u, sy) in busiest]
     n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
@@ -408,7 +429,7 @@ def run(args) -> Optional[Dict[str, Any]]:
             "kv_peak_util": round(eng.kv.peak_used / max(1, eng.kv.num_blocks), 4)},
         # CPU seconds per thread group over the timed window (GIL competition with the engine thread)
         "host_cpu_s": {k: round(v - cpu0.get(k, 0.0), 2) for k, v in cpu1.items()},
-        "native_threads": {"n": len(native_top), "top_cpu_s": native_top[:4]},
+        "native_threads": {"n": len(native_top), "top_cpu_s": native_top[:4], "busiest": native_busiest},
         # every rank's CPU binding (disjoint NUMA-local slices; null = unbound)
         "cpu_affinity": placements,
         "setup_s": round(setup_s, 1),

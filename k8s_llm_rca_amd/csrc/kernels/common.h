@@ -45,6 +45,14 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return *reinterpret_cast<uint16_t*>(&h);
 }
 
+// RoPE of one (x[i], x[i + 64]) pair in a fixed operation order -- no choice
+// left to the compiler's contraction -- so every kernel that rotates (rope_kv,
+// the skinny and the prefill qkv GEMM epilogues) rounds identically.
+__device__ __forceinline__ void rope_pair(float a, float b, float co, float si, float& lo, float& hi) {
+  lo = fmaf(a, co, -__fmul_rn(b, si));
+  hi = fmaf(b, co, __fmul_rn(a, si));
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

@@ -485,8 +485,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __rest
           for (int c = 0; c < NA; ++c) {
             const float co = cs[d0 + c], si = cs[64 + d0 + c];
             const float a = bf2f(f2bf(v[c])), b = bf2f(f2bf(v[NA + c]));
-            lo[c] = a * co - b * si;
-            hi[c] = b * co + a * si;
+            rope_pair(a, b, co, si, lo[c], hi[c]);
           }
         } else {
 #pragma unroll

@@ -116,8 +116,10 @@ __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __
       if (hd < rp.nq + rp.nkv) {  // q / k head: rotate-half pair (d, d + 64)
         const float* cs = rp.cos_sin + (size_t)rp.pos[m] * 128;
         const float co = cs[d], si = cs[64 + d], fa = bf2f(a), fb = bf2f(b);
-        a = f2bf(fa * co - fb * si);
-        b = f2bf(fb * co + fa * si);
+        float ra, rb;
+        rope_pair(fa, fb, co, si, ra, rb);
+        a = f2bf(ra);
+        b = f2bf(rb);
       }
       uint16_t* yr = y + (size_t)m * ldy + hd * 128;
       yr[d] = a;

@@ -180,8 +180,10 @@ __global__ void __launch_bounds__(256) rope_kv_kernel(uint16_t* __restrict__ qkv
     for (int j = 0; j < 8; ++j) {
       const float co = cs[c + j], si = cs[64 + c + j];
       const float a = bf2f(lo[j]), b = bf2f(hi[j]);
-      olo[j] = f2bf(a * co - b * si);
-      ohi[j] = f2bf(b * co + a * si);
+      float ra, rb;
+      rope_pair(a, b, co, si, ra, rb);
+      olo[j] = f2bf(ra);
+      ohi[j] = f2bf(rb);
     }
     *reinterpret_cast<u16x8*>(xp + c) = olo;
     *reinterpret_cast<u16x8*>(xp + 64 + c) = ohi;

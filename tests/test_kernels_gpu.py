@@ -859,7 +859,9 @@ def test_gemm_big_rope_kv_epilogue_bit_identical(M, nq, nkv, var, monkeypatch):
     q1 = LIN.gemm_big(x, w)
     A.rope_kv_write(q1, pos, cs, slots, kc1, vc1, nq, nkv)
     q2 = LIN.gemm_big_rope(x, w, pos, cs, slots, kc2, vc2, nq, nkv)
-    assert torch.equal(q1, q2) and torch.equal(kc1, kc2) and torch.equal(vc1, vc2)
+    for name, u, v in (("qkv", q1, q2), ("k pages", kc1, kc2), ("v pages", vc1, vc2)):
+        bad = (u != v).nonzero()
+        assert bad.numel() == 0, (name, bad.shape[0], bad[:8].tolist(), u[tuple(bad[0])].item(), v[tuple(bad[0])].item())
     ref = (x.float() @ w.float().t()).bfloat16()  # v is not rotated: the GEMM's own output
     torch.testing.assert_close(q2[:, (nq + nkv) * 128:].float(), ref[:, (nq + nkv) * 128:].float(), atol=3e-2,
                                rtol=2e-2)

@@ -14,6 +14,7 @@ CATS = [
     ("attn_decode", r"attn_decode|attn_reduce"),
     ("attn_prefill", r"attn_prefill"),
     ("gemm_hipblaslt", r"^(Custom_)?Cijk"),
+    ("gemm_big", r"gemm_big|big_reduce"),  # hand-written 256x256 prefill GEMM (+ fused epilogues)
     ("gemm_skinny", r"gemm_skinny|gemm_mid"),
     ("gemm_grouped", r"grouped_gemm|grouped_reduce"),  # MoE experts, and split-K dense GEMMs (dispatch 'grp')
     ("moe", r"moe"),

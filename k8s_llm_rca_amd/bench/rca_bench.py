@@ -45,7 +45,7 @@ def _native_cpu() -> Dict[int, tuple]:
         return {}
 
 
-def _native_detail(tid: int) -> Dict[str, Any]:
+def _native_detail(tid: int, samples: int = 0) -> Dict[str, Any]:
     """What a busy native thread is doing, from /proc (no GPU call, no
     ptrace): its name, kernel wait channel and current system call -- a thread
     spinning in user space shows wchan 0 and mostly user time; one blocked in
@@ -57,6 +57,32 @@ def _native_detail(tid: int) -> Dict[str, Any]:
                 v = f.read().strip()
             out[key] = v.split()[0] if key == "syscall" and v else v
         except OSError:
+            pass
+    if samples:
+        # where it spends its time: the current system call sampled every 2 ms
+        # ("running" = in user space; a number = blocked / inside that syscall;
+        # for ioctl the request code follows, e.g. KFD's wait-events ioctl)
+        import time
+        hist: Dict[str, int] = {}
+        for _ in range(samples):
+            try:
+                with open(f"/proc/self/task/{tid}/syscall") as f:
+                    v = f.read().split()
+            except OSError:
+                break
+            k = v[0] if v else "?"
+            if k == "16" and len(v) > 2:  # ioctl: add the request code
+                k = f"16:{v[2]}"
+            hist[k] = hist.get(k, 0) + 1
+            time.sleep(0.002)
+        out["syscall_samples"] = dict(sorted(hist.items(), key=lambda kv: -kv[1])[:6])
+        try:  # creation order among this process's threads (start time, clock ticks)
+            starts = {}
+            for t in os.listdir("/proc/self/task"):
+                with open(f"/proc/self/task/{t}/stat") as f:
+                    starts[int(t)] = int(f.read().rsplit(")", 1)[1].split()[19])
+            out["start_rank"] = sorted(starts, key=lambda t: (starts[t], t)).index(tid)
+        except (OSError, ValueError, IndexError):
             pass
     return out
 
@@ -286,10 +312,12 @@ def run(args) -> Optional[Dict[str, Any]]:
               for t, (u, sy) in ncpu1.items()}
     native_top = sorted((round(u + sy, 2) for u, sy in ndelta.values()), reverse=True)
     busiest = sorted(ndelta.items(), key=lambda kv: -(kv[1][0] + kv[1][1]))[:2]
-    native_busiest = [dict(_native_detail(t), user_s=round(u, 2), sys_s=round(sy, 2)) for t, (u, sy) in busiest]
     n_done = min(stream.n_ok - base, n_steps * quantum)
     _barrier(sync_world, device)
     elapsed = time.perf_counter() - t0
+    # outside the timed window: the stream still runs, so the sample sees the same threads busy
+    native_busiest = [dict(_native_detail(t, 300 if j == 0 else 0), user_s=round(u, 2), sys_s=round(sy, 2))
+                      for j, (t, (u, sy)) in enumerate(busiest)]
     truncated = truncated or not done_all
     d = {k: eng.stats[k] - stats0.get(k, 0) for k in eng.stats}
     sim = None
@@ -310,6 +338,10 @@ def run(args) -> Optional[Dict[str, Any]]:
                "projected_value": round(n_done / wall_p, 4) if wall_p > 0 else 0.0,
                "projected_ms_per_step": round(1000.0 * wall_p / n_steps, 2),
                "collective_share_modelled": round(pr["modelled_s"] / wall_p, 4) if wall_p > 0 else 0.0,
+               # hop-latency sensitivity of the model (one fabric hand-off = 2.5 / 5 / 10 us)
+               "projected_value_by_hop_us": {
+                   str(h): round(n_done / w, 4) if (w := elapsed - pr["standin_s"] + m) > 0 else 0.0
+                   for h, m in pr["modelled_s_by_hop"].items()},
                "per_T": pr["per_T"]}
     gq = {k: 1e3 * v["total_s"] for k, v in tracing.snapshot().items()}
     bstats = [dict(b.stats) for b in batchers]

@@ -793,11 +793,15 @@ __device__ __forceinline__ void pf8_glds(const uint16_t* src, unsigned char* lds
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
-// VAR (A/B only, K8SRCA_PF_W8=2/3): 2 = no static priority; 3 = waves 4-7 run half a page
-// behind (P.V of page i-1 first, then QK^T of page i and its softmax), so a SIMD's
-// two waves are in complementary segments two thirds of the time instead of in
-// lockstep (MI355X_MICROARCH.md "Two waves per SIMD", item 9); the stage refilled
-// after iteration i's barrier is then page i-2's (page i-1's V is still read).
+// VAR (K8SRCA_PF_W8): 2 = the compiler's schedule of the page loop; 4 = the same
+// arithmetic with the page's 16 K fragments read up front (the compiler otherwise
+// serialises read -> wait -> MFMA for the first 32 keys: 8 exposed LDS latencies
+// per page), the two 32-key score tiles accumulated as interleaved chains, the
+// row max as two max3 chains joined across the half-waves by permlane32_swap
+// (a VALU exchange instead of a ds_bpermute round trip) and the row sum as four
+// partial sums instead of one 32-long dependent add chain.  The measured-loss
+// variants (static priority for the younger half: 651 vs 664 TFLOP/s; waves 4-7
+// half a page behind: 608) are retired.
 template <int VAR>
 __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   __shared__ __attribute__((aligned(16))) unsigned char lds[PF8_NB * PF8_STAGE + 4 * PF8_MAXP];
@@ -873,46 +877,114 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
 
   const int kreg = (r & 3) + 4 * (r >> 3), khi = (r >> 2) & 1;
   const int krow0 = pf_key(kreg, khi);
-  // the younger half of the workgroup loses VALU arbitration on every segment:
-  // one static priority bump for it (cdna_hip_programming.md T5, static form)
-  if (VAR != 2 && __builtin_amdgcn_readfirstlane(tid) >= 256) __builtin_amdgcn_s_setprio(1);
-  constexpr int AHEAD = VAR == 3 ? PF8_NB - 2 : PF8_NB - 1;  // pages in flight beyond the current one
-  const bool late = VAR == 3 && __builtin_amdgcn_readfirstlane(tid) >= 256;
-  bf16x8 pl[2][2];          // late waves: the previous page's P, its P.V still owed
-  bool owe = false;
-  int owe_stage = 0;
+  constexpr int AHEAD = PF8_NB - 1;  // pages in flight beyond the current one
 
   if (np > 0) {
 #pragma unroll
     for (int j = 0; j < AHEAD; ++j) issue(j, min(j, np - 1));
   }
-  for (int i = 0; i <= np; ++i) {
-    if (i == np) {  // late waves: the last owed P.V (nothing else runs in this trip)
-      if (late && owe) {
-        const unsigned char* vl = lds + owe_stage * PF8_STAGE + PF_KBYTES;
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int d = 32 * dt + r;
-          const unsigned char* vr = vl + d * 128;
-          const int sw = (d >> 1) & 7;
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
-              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl[kt][s], o[dt], 0, 0, 0);
-            }
-        }
-      }
-      break;
-    }
+  for (int i = 0; i < np; ++i) {
     // this wave's DMAs of page i are done when only the later pages' remain
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"((AHEAD - 1) * PF8_DMA) : "memory");
     __builtin_amdgcn_s_barrier();  // every wave's page i landed; every wave is done with the refilled stage
     issue((i + AHEAD) % PF8_NB, min(i + AHEAD, np - 1));  // refill (clamped at the end: an L2 hit)
     const int k0 = (p_begin + i) * PF_PAGE;
-    if (late && owe) {  // P.V of page i-1 first (its P was made at the current reference max)
-      const unsigned char* vl = lds + owe_stage * PF8_STAGE + PF_KBYTES;
+    if (wave_live && k0 < wave_hi) {
+      const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
+      const unsigned char* vl = kl + PF_KBYTES;
+      f32x16 sc[2];
+      if constexpr (VAR == 4) {
+        // key 32 kt + krow0 has the swizzle of krow0 (32 kt is a multiple of 16):
+        // the second tile's reads are the first's at +8 KB
+        const unsigned char* kr = kl + krow0 * 256;
+        bf16x8 kf[2][8];
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt)
+            kf[kt][s] = *reinterpret_cast<const bf16x8*>(kr + kt * 8192 + (((2 * s + hi) ^ (krow0 & 15)) << 4));
+        __builtin_amdgcn_sched_barrier(0);  // all 16 reads issue before the first MFMA (counted waits follow)
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sc[kt][e] = 0.f;
+#pragma unroll
+        for (int s = 0; s < 8; ++s)
+#pragma unroll
+          for (int kt = 0; kt < 2; ++kt) sc[kt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[kt][s], qf[s], sc[kt], 0, 0, 0);
+      } else {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt) {
+          const int key = 32 * kt + krow0;
+          const unsigned char* kr = kl + key * 256;
+          f32x16 acc;
+#pragma unroll
+          for (int e = 0; e < 16; ++e) acc[e] = 0.f;
+#pragma unroll
+          for (int s = 0; s < 8; ++s) {
+            const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s + hi) ^ (key & 15)) << 4));
+            acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
+          }
+          sc[kt] = acc;
+        }
+      }
+      if (k0 + PF_PAGE > wave_lo) {
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
+      }
+      float cmax;
+      if constexpr (VAR == 4) {
+        float c0 = -INFINITY, c1 = -INFINITY;
+#pragma unroll
+        for (int e = 0; e < 16; ++e) {
+          c0 = fmaxf(c0, sc[0][e]);
+          c1 = fmaxf(c1, sc[1][e]);
+        }
+        cmax = fmaxf(c0, c1);
+        // lanes 0-31 and 32-63 hold the two halves of a row's 64 keys: after the
+        // swap one operand has this lane's value and the other the partner's
+        const auto pr = __builtin_amdgcn_permlane32_swap(__float_as_uint(cmax), __float_as_uint(cmax), false, false);
+        cmax = fmaxf(__uint_as_float(pr[0]), __uint_as_float(pr[1]));
+      } else {
+        cmax = -INFINITY;
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
+        cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
+      }
+      const float mcand = cmax * a.scale_log2;
+      const bool upd = mcand > m + 8.f;
+      const float mnew = upd ? mcand : m;
+      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
+      const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
+      bf16x8 pf[2][2];
+      float ps[4] = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
+            if constexpr (VAR == 4)
+              ps[j & 3] += e;
+            else
+              ps[0] += e;
+            pf[kt][s][j] = (__bf16)e;
+          }
+      const float psum = VAR == 4 ? (ps[0] + ps[1]) + (ps[2] + ps[3]) : ps[0];
+      l = l * alpha + psum;
+      m = mnew;
+      if (__ballot(upd)) {
+#pragma unroll
+        for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
+      }
 #pragma unroll
       for (int dt = 0; dt < 4; ++dt) {
         const int d = 32 * dt + r;
@@ -923,94 +995,13 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
 #pragma unroll
           for (int s = 0; s < 2; ++s) {
             const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pl[kt][s], o[dt], 0, 0, 0);
+            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
           }
-      }
-      owe = false;
-    }
-    if (wave_live && k0 < wave_hi) {
-      const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
-      const unsigned char* vl = kl + PF_KBYTES;
-      f32x16 sc[2];
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt) {
-        const int key = 32 * kt + krow0;
-        const unsigned char* kr = kl + key * 256;
-        f32x16 acc;
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[e] = 0.f;
-#pragma unroll
-        for (int s = 0; s < 8; ++s) {
-          const bf16x8 kf = *reinterpret_cast<const bf16x8*>(kr + (((2 * s + hi) ^ (key & 15)) << 4));
-          acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf, qf[s], acc, 0, 0, 0);
-        }
-        sc[kt] = acc;
-      }
-      if (k0 + PF_PAGE > wave_lo) {
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e)
-            if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
-      }
-      float cmax = -INFINITY;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
-      cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
-      const float mcand = cmax * a.scale_log2;
-      const bool upd = mcand > m + 8.f;
-      const float mnew = upd ? mcand : m;
-      const float alpha = upd ? __builtin_amdgcn_exp2f(m - mnew) : 1.f;
-      const float nmsub = (mnew == -INFINITY) ? 0.f : -mnew;
-      bf16x8 pf[2][2];
-      float psum = 0.f;
-#pragma unroll
-      for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-        for (int s = 0; s < 2; ++s)
-#pragma unroll
-          for (int j = 0; j < 8; ++j) {
-            const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
-            psum += e;
-            pf[kt][s][j] = (__bf16)e;
-          }
-      l = l * alpha + psum;
-      m = mnew;
-      if (__ballot(upd)) {  // (late waves: page i-1's P.V is already in O)
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
-      }
-      if (late) {  // P.V of this page next trip, behind its barrier
-#pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-          for (int s = 0; s < 2; ++s) pl[kt][s] = pf[kt][s];
-        owe = true;
-        owe_stage = i % PF8_NB;
-      } else {
-#pragma unroll
-        for (int dt = 0; dt < 4; ++dt) {
-          const int d = 32 * dt + r;
-          const unsigned char* vr = vl + d * 128;
-          const int sw = (d >> 1) & 7;
-#pragma unroll
-          for (int kt = 0; kt < 2; ++kt)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-              const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
-              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
-            }
-        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
-  __builtin_amdgcn_s_setprio(0);
 
   if (!valid) return;
   l += __shfl_xor(l, 32, 64);
@@ -1124,16 +1115,17 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   return (int)hipGetLastError();
 }
 
-// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups (2, the default: no static
-// priority; 1: with it; 3: staggered late waves), 0 = the 128-row pg64 kernel.
-// Read per launch, like the planner reads it per plan.  Replayed steady-state
-// mix (tools/bench_kernels.py --what replay, profiles/r3/pf_replay*.txt): 2 =
-// 664 / 1 = 651 / 3 = 608 / 0 = 647 TFLOP/s; on the round-2 (young-thread)
+// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups -- unset / 1 / 4: the explicit
+// page-loop schedule (VAR 4), 2: the compiler's schedule (A/B arm) -- and 0: the
+// 128-row pg64 kernel.  Read per launch, like the planner reads it per plan.
+// Replayed steady-state mix (tools/bench_kernels.py --what replay,
+// profiles/r4/prefill_attn/): 4 = 669 / 2 = 648 TFLOP/s (r3: 2 = 664, static
+// priority 651, staggered late waves 608, pg64 647); on the round-2 (young-thread)
 // mix of short chunks pg64 is ahead (406 vs 378): per-step choice measured at
 // <= 3 % of prefill attention, not wired.
 static int prefill_w8() {
   const char* v = std::getenv("K8SRCA_PF_W8");
-  if (!v || !v[0]) return 2;
+  if (!v || !v[0] || v[0] == '1') return 4;
   return v[0] - '0';
 }
 
@@ -1181,12 +1173,10 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
     const int var = prefill_w8();
     const bool w8 = var > 0 && PF8_ROWS % a.G == 0;
     a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
-    if (w8 && var == 3)
-      hipLaunchKernelGGL(attn_prefill_w8_kernel<3>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
-    else if (w8 && var == 2)
-      hipLaunchKernelGGL(attn_prefill_w8_kernel<2>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    if (w8 && var == 4)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<4>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else if (w8)
-      hipLaunchKernelGGL(attn_prefill_w8_kernel<1>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<2>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else
       hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
     if (n_merge > 0)

@@ -37,10 +37,11 @@ from .xgmi import ONE_SHOT_MAX, _bind, _check
 
 XGMI_LINK_GBPS = 153.0   # one xGMI link, per direction (7 links per GPU)
 XGMI_HOP_US = 2.5        # one flag hand-off across the fabric (signal -> visible on the peer)
+HOP_SENSITIVITY_US = (2.5, 5.0, 10.0)  # the projection is also reported at these hop latencies
 RCCL_BUS_GBPS = 300.0    # assumed RCCL all-reduce bus bandwidth on an 8-GPU xGMI node (not measured here)
 
 
-def xgmi_model_us(nbytes: int, world: int, mode: int) -> float:
+def xgmi_model_us(nbytes: int, world: int, mode: int, hop_us: float = XGMI_HOP_US) -> float:
     """Modelled time of one bf16 all-reduce of ``nbytes`` over a full xGMI
     mesh: one-shot reads (N-1) peer slices in parallel over N-1 links (one
     hop), two-shot moves 2 (N-1)/N of the message in two hops, and RCCL
@@ -48,10 +49,10 @@ def xgmi_model_us(nbytes: int, world: int, mode: int) -> float:
     ``RCCL_BUS_GBPS`` with 2 (N-1) ring hops."""
     bw = XGMI_LINK_GBPS * 1e3  # bytes per us
     if mode == 1:
-        return XGMI_HOP_US + nbytes / bw
+        return hop_us + nbytes / bw
     if mode == 2:
-        return 2 * XGMI_HOP_US + 2 * nbytes / (world * bw)
-    return 2 * (world - 1) * XGMI_HOP_US + 2 * (world - 1) / world * nbytes / (RCCL_BUS_GBPS * 1e3)
+        return 2 * hop_us + 2 * nbytes / (world * bw)
+    return 2 * (world - 1) * hop_us + 2 * (world - 1) / world * nbytes / (RCCL_BUS_GBPS * 1e3)
 
 
 class LoopbackAR:
@@ -177,10 +178,10 @@ def sim_context(tp: int, max_bytes: int = 64 << 20, ep: int = 1) -> SimParallelC
     return pc
 
 
-def a2a_model_us(nbytes: int, world: int) -> float:
+def a2a_model_us(nbytes: int, world: int, hop_us: float = XGMI_HOP_US) -> float:
     """Modelled equal-split all-to-all of ``nbytes`` per rank over a full
     xGMI mesh: (N-1)/N of them leave over N-1 links at once, one hop."""
-    return XGMI_HOP_US + nbytes / (world * XGMI_LINK_GBPS * 1e3)
+    return hop_us + nbytes / (world * XGMI_LINK_GBPS * 1e3)
 
 
 def _time_us(fn, reps: int = 20) -> float:
@@ -203,8 +204,10 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
     MoE (``moe_k`` = top-k, EP = TP): one all-reduce (o_proj) and the three
     fixed-capacity all-to-alls of ``parallel/ep.py`` (dispatch, combine, row
     all-gather).  ``projected`` wall = measured wall - stand-in + modelled (the
-    collectives are serial in the step's stream)."""
+    collectives are serial in the step's stream).  ``modelled_s_by_hop``: the
+    same model at each hop latency of ``HOP_SENSITIVITY_US``."""
     standin_us = model_us = 0.0
+    by_hop = {h: 0.0 for h in HOP_SENSITIVITY_US}
     per_t = {}
     N = pc.tp_size
     for T, n in sorted(rows_hist.items()):
@@ -215,6 +218,7 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
         m_us = xgmi_model_us(T * hidden * 2, N, mode)
         n_ar = 1 if moe_k else 2
         s_tot, m_tot = n_ar * s_us, n_ar * m_us
+        h_tot = {h: n_ar * xgmi_model_us(T * hidden * 2, N, mode, h) for h in by_hop}
         if moe_k:
             per = (T + N - 1) // N
             for row_elems in ((per * moe_k) * (hidden + 8), (per * moe_k) * hidden, per * hidden):
@@ -224,9 +228,14 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
                     recv = torch.empty_like(send)
                     s_tot += _time_us(lambda: car.all_to_all(send, recv))
                 m_tot += a2a_model_us(nb, N)
+                for h in by_hop:
+                    h_tot[h] += a2a_model_us(nb, N, h)
         k = n_layers * n
+        for h in by_hop:
+            by_hop[h] += k * h_tot[h]
         standin_us += k * s_tot
         model_us += k * m_tot
         per_t[int(T)] = {"forwards": int(n), "mode": mode, "standin_us": round(s_tot, 2),
                          "model_us": round(m_tot, 2)}
-    return {"standin_s": standin_us / 1e6, "modelled_s": model_us / 1e6, "per_T": per_t}
+    return {"standin_s": standin_us / 1e6, "modelled_s": model_us / 1e6, "per_T": per_t,
+            "modelled_s_by_hop": {h: v / 1e6 for h, v in by_hop.items()}}

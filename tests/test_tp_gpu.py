@@ -259,6 +259,8 @@ def test_tp_sim_rank0_runs_real_kernels_with_standin_collectives():
     assert eng.model._exec is not None and eng.stats["graph_steps"] > 0 and sum(eng.sim_rows.values()) > 0
     pr = project(eng.sim_rows, pc, eng.mc.hidden, eng.mc.n_layers, "cuda:0")
     assert pr["standin_s"] > 0 and pr["modelled_s"] > 0
+    hops = pr["modelled_s_by_hop"]  # hop-latency sensitivity: monotone, the default hop reproduces modelled_s
+    assert hops[2.5] == pytest.approx(pr["modelled_s"]) and hops[2.5] < hops[5.0] < hops[10.0]
     assert pc.custom_ar.status() == 0
     pc.custom_ar.close()
 

@@ -61,7 +61,7 @@ def main():
     ap.add_argument("--pf-ab", type=int, default=1, help="replay: time the prefill with every kernel of --pf-kinds")
     ap.add_argument("--pf-steps-out", default="", help="replay: per-step prefill timings (JSON lines) to this file")
     ap.add_argument("--pf-targets", default="", help="replay: comma list of prefill split targets (workgroups) to A/B")
-    ap.add_argument("--pf-kinds", default="1,0", help="K8SRCA_PF_W8 values to A/B (1 w8, 2 w8 no prio, 3 w8 stagger, 0 pg64)")
+    ap.add_argument("--pf-kinds", default="1,0", help="K8SRCA_PF_W8 values to A/B (2 w8, 4 w8 explicit schedule, 0 pg64)")
     args = ap.parse_args()
     dev = "cuda"
     torch.manual_seed(0)

@@ -73,6 +73,7 @@ struct AttnArgs {
   int n_items;
   const int* d_n_items;   // device {item count, part_size} (HIP graphs: the grid stays fixed), or null
   int pf_rows;            // rows per prefill partial slot (128: pg64 kernel, 256: w8 kernel)
+  int pf_bf16;            // partials are bf16 O / l (w8 VAR 4) instead of fp32 unnormalised O
 };
 
 struct RowState {
@@ -893,7 +894,7 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
       const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
       const unsigned char* vl = kl + PF_KBYTES;
       f32x16 sc[2];
-      if constexpr (VAR == 4) {
+      if constexpr (VAR >= 4) {
         // key 32 kt + krow0 has the swizzle of krow0 (32 kt is a multiple of 16):
         // the second tile's reads are the first's at +8 KB
         const unsigned char* kr = kl + krow0 * 256;
@@ -936,7 +937,7 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
             if (k0 + 32 * kt + pf_key(e, hi) >= limit) sc[kt][e] = -INFINITY;
       }
       float cmax;
-      if constexpr (VAR == 4) {
+      if constexpr (VAR >= 4) {
         float c0 = -INFINITY, c1 = -INFINITY;
 #pragma unroll
         for (int e = 0; e < 16; ++e) {
@@ -970,13 +971,13 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
             const float e = __builtin_amdgcn_exp2f(fmaf(sc[kt][8 * s + j], a.scale_log2, nmsub));
-            if constexpr (VAR == 4)
+            if constexpr (VAR >= 4)
               ps[j & 3] += e;
             else
               ps[0] += e;
             pf[kt][s][j] = (__bf16)e;
           }
-      const float psum = VAR == 4 ? (ps[0] + ps[1]) + (ps[2] + ps[3]) : ps[0];
+      const float psum = VAR >= 4 ? (ps[0] + ps[1]) + (ps[2] + ps[3]) : ps[0];
       l = l * alpha + psum;
       m = mnew;
       if (__ballot(upd)) {
@@ -1003,6 +1004,51 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
 
+  if constexpr (VAR == 5) {
+    // Epilogue through LDS (the ring is free once every wave has left the loop):
+    // each wave stages its 32 rows x 128 dims as bf16 (O / l) in a private,
+    // 272-B-pitch image (conflict-free 8-B writes), then stores 16 B per lane
+    // with 16 lanes per row: full 256-B rows (a token's G heads are contiguous
+    // in `out`), 8 dwordx4 stores instead of 16 dwordx2 at a 512-B lane stride
+    // (cdna_hip_programming.md T21: the row-per-lane store tail is issue-bound).
+    // Split tiles store the same bf16 O / l rows plus (m, l): half the fp32
+    // partial's bytes, merged by attn_prefill_merge (pf_bf16).
+    constexpr int PITCH = 272;
+    __syncthreads();
+    l += __shfl_xor(l, 32, 64);
+    const float inv = l > 0.f ? 1.f / l : 0.f;
+    unsigned char* wl = lds + w * (32 * PITCH);
+#pragma unroll
+    for (int dt = 0; dt < 4; ++dt)
+#pragma unroll
+      for (int q4 = 0; q4 < 4; ++q4) {
+        u16x4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = f2bf(o[dt][4 * q4 + e] * inv);
+        *reinterpret_cast<u16x4*>(wl + r * PITCH + 2 * (32 * dt + 8 * q4 + 4 * hi)) = v;
+      }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c16 = lane & 15;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int rr = 4 * j + (lane >> 4);
+      const int gr = w * 32 + rr, tr = gr / a.G, gg = gr % a.G;
+      const u16x8 v = *reinterpret_cast<const u16x8*>(wl + rr * PITCH + 16 * c16);
+      if (tr < tlen) {
+        uint16_t* dst = slot >= 0
+            ? reinterpret_cast<uint16_t*>(a.pf_o) + (((size_t)slot * a.nkv + kvh) * PF8_ROWS + gr) * D + 8 * c16
+            : a.out + (size_t)(tok0 + tr) * a.out_stride + (kvh * a.G + gg) * D + 8 * c16;
+        *reinterpret_cast<u16x8*>(dst) = v;
+      }
+    }
+    if (slot >= 0 && valid && hi == 0) {
+      const size_t rbase = ((size_t)slot * a.nkv + kvh) * PF8_ROWS + grow;
+      a.pf_ml[rbase * 2] = m;
+      a.pf_ml[rbase * 2 + 1] = l;
+    }
+    return;
+  }
   if (!valid) return;
   l += __shfl_xor(l, 32, 64);
   if (slot >= 0) {  // split tile: unnormalised partial, merged by attn_prefill_merge
@@ -1057,12 +1103,19 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
   for (int p = 0; p < np; ++p) {
     const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * a.pf_rows + row;
     const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
-    const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
     // a part that saw no key of the row has m = -inf: weight 0
     const float f = (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
     L += ml.y * f;
-    o0 += v.x * f;
-    o1 += v.y * f;
+    if (a.pf_bf16) {  // O / l in bf16: the part's O is (O / l) * l
+      const uint32_t v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(a.pf_o) + rb * D + 2 * lane);
+      const float fl = f * ml.y;
+      o0 += bf2f((uint16_t)(v & 0xffffu)) * fl;
+      o1 += bf2f((uint16_t)(v >> 16)) * fl;
+    } else {
+      const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
+      o0 += v.x * f;
+      o1 += v.y * f;
+    }
   }
   const float inv = L > 0.f ? 1.f / L : 0.f;
   const int tt = row / a.G, g = row % a.G;
@@ -1115,17 +1168,18 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   return (int)hipGetLastError();
 }
 
-// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups -- unset / 1 / 4: the explicit
-// page-loop schedule (VAR 4), 2: the compiler's schedule (A/B arm) -- and 0: the
-// 128-row pg64 kernel.  Read per launch, like the planner reads it per plan.
-// Replayed steady-state mix (tools/bench_kernels.py --what replay,
-// profiles/r4/prefill_attn/): 4 = 669 / 2 = 648 TFLOP/s (r3: 2 = 664, static
-// priority 651, staggered late waves 608, pg64 647); on the round-2 (young-thread)
-// mix of short chunks pg64 is ahead (406 vs 378): per-step choice measured at
-// <= 3 % of prefill attention, not wired.
+// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups -- unset / 1 / 5: the explicit
+// page-loop schedule with the LDS-staged bf16 epilogue (VAR 5), 4: the same loop
+// with per-lane fp32 partial / dwordx2 row stores, 2: the compiler's schedule --
+// and 0: the 128-row pg64 kernel.  Read per launch, like the planner reads it per
+// plan.  Replayed steady-state mix (tools/bench_kernels.py --what replay,
+// profiles/r4/prefill_attn/, interleaved in one process): 5 = 649 / 4 = 624 /
+// 2 = 628 TFLOP/s (VAR 5 ahead on every step class: long extends -3 %, 200-700-
+// token extends -5 %, jump-forward chunks -5 % time); an earlier box: 4 = 669 /
+// 2 = 648, pg64 633 (r3: static priority 651, staggered late waves 608).
 static int prefill_w8() {
   const char* v = std::getenv("K8SRCA_PF_W8");
-  if (!v || !v[0] || v[0] == '1') return 4;
+  if (!v || !v[0] || v[0] == '1') return 5;
   return v[0] - '0';
 }
 
@@ -1173,7 +1227,10 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
     const int var = prefill_w8();
     const bool w8 = var > 0 && PF8_ROWS % a.G == 0;
     a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
-    if (w8 && var == 4)
+    a.pf_bf16 = w8 && var == 5;
+    if (w8 && var == 5)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<5>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    else if (w8 && var == 4)
       hipLaunchKernelGGL(attn_prefill_w8_kernel<4>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else if (w8)
       hipLaunchKernelGGL(attn_prefill_w8_kernel<2>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);

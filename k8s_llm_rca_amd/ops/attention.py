@@ -355,6 +355,12 @@ PF8_MAXP = 1024             # key pages per w8 work item (page ids staged in LDS
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
 # split long key ranges until a prefill launch has about this many workgroups
 PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
+# makespan planner (PF_OVERHEAD_PAGES > 0): pick the split length that minimises
+# the launch's estimated makespan on the CU slots, pricing every work item at its
+# pages + this many pages of fixed cost (Q load, first DMAs, epilogue, merge share);
+# 0 = the fixed-target rule above
+PF_OVERHEAD_PAGES = float(os.environ.get("K8S_PF_OVERHEAD_PAGES", "0"))
+PF_CU_SLOTS = 256           # concurrent prefill workgroups: one 8-wave w8 workgroup per CU
 _NO_END = 1 << 30
 
 
@@ -434,8 +440,12 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
         return plan
     pages = [(end + 63) // 64 for end, _, _, _ in tiles]
     total = sum(pages)
-    # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
-    part = max(pages) if pages and len(tiles) * nkv >= target_wgs // 2 else max(4, -(-total * nkv // target_wgs))
+    if PF_OVERHEAD_PAGES > 0 and pages:
+        part = _makespan_part(pages, nkv, PF_OVERHEAD_PAGES, max_part, max_slots,
+                              PF_CU_SLOTS if max_part is not None else 2 * PF_CU_SLOTS)
+    else:
+        # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
+        part = max(pages) if pages and len(tiles) * nkv >= target_wgs // 2 else max(4, -(-total * nkv // target_wgs))
     if max_part is not None:
         part = min(part, max_part)
     while sum(-(-p // part) for p in pages if p > part) > max_slots:
@@ -463,6 +473,38 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
         for lst, v in zip(plan.arrays()[:6], (s, t, n, k0, k1, sl)):
             lst.append(v)
     return plan
+
+
+_PART_CANDIDATES = (4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32, 40, 48, 56, 64, 80, 96, 128, 160, 192, 256, 384,
+                    512, 768, 1024)
+
+
+def _makespan_part(pages: List[int], nkv: int, overhead: float, max_part: Optional[int], max_slots: int,
+                   slots: int) -> int:
+    """Split length (pages per item) minimising the estimated makespan of a
+    prefill launch: items (every tile cut into ceil(p / part) near-equal
+    pieces, times nkv heads) sorted longest first run in rounds of ``slots``
+    workgroups, each round as long as its longest item plus ``overhead``
+    pages.  The no-split choice (part = the longest tile) is a candidate."""
+    import numpy as np
+    pg = np.asarray(pages, dtype=np.int64)
+    longest = int(pg.max())
+    best, best_t = longest, None
+    for part in [c for c in _PART_CANDIDATES if c < longest] + [longest]:
+        if max_part is not None and part > max_part:
+            continue
+        k = -(-pg // part)
+        if int(k[k > 1].sum()) > max_slots:
+            continue
+        # piece lengths of tile i: floor / ceil of p_i / k_i (the planner's bounds split)
+        lo = pg // k
+        n_hi = pg - lo * k
+        lens = np.concatenate([np.repeat(lo + 1, n_hi), np.repeat(lo, k - n_hi)])
+        lens = np.sort(np.repeat(lens, nkv))[::-1]
+        t = float(lens[::slots].sum()) + overhead * (-(-lens.size // slots))
+        if best_t is None or t < best_t:
+            best, best_t = part, t
+    return best
 
 
 def attach_plan(meta: "AttnMeta", plan: PrefillPlan, device, workspace: Optional[tuple] = None) -> "AttnMeta":

@@ -179,7 +179,9 @@ def main():
             T = sum(ql)
             for k in kinds:
                 os.environ["K8SRCA_PF_W8"] = k.split("@")[0]
-                A.PF_TARGET_WGS = int(k.split("@")[1]) if "@" in k else targets[0]
+                arm = k.split("@")[1] if "@" in k else None
+                A.PF_OVERHEAD_PAGES = float(arm[1:]) if arm and arm.startswith("o") else 0.0
+                A.PF_TARGET_WGS = int(arm) if arm and not arm.startswith("o") else targets[0]
                 torch.manual_seed(i)
                 meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
                 if k == kinds[0]:
@@ -198,6 +200,7 @@ def main():
                                                                f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
         os.environ["K8SRCA_PF_W8"] = kinds0[0]
         A.PF_TARGET_WGS = targets[0]
+        A.PF_OVERHEAD_PAGES = 0.0
         if args.pf_steps_out:
             with open(args.pf_steps_out, "w") as f:
                 for v in per_step.values():

@@ -135,10 +135,47 @@ def main():
             x.add_(1.0)
             float(x[0].item())
 
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops import norm as NRM
+    xa = torch.randn(2048, 4096, device=dev).bfloat16()
+    wa = torch.randn(4096, 4096, device=dev).bfloat16()
+
+    def lib_gemm():  # the engine's prefill GEMMs (measured dispatch: hipBLASLt / gemm_big)
+        for _ in range(n // 40):
+            LIN.linear(xa, wa)
+
+    def torch_matmul():
+        for _ in range(n // 40):
+            torch.matmul(xa, wa.t())
+
+    def lib_norm():
+        wn = torch.ones(4096, device=dev).bfloat16()
+        xs = xa[:128]
+        for _ in range(n // 4):
+            NRM.rmsnorm(xs, wn, 1e-5)
+
+    def big_graph():  # a decode-step-sized graph: ~400 kernels
+        s2 = torch.cuda.Stream()
+        with torch.cuda.stream(s2):
+            x.add_(1.0)
+        torch.cuda.synchronize()
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for _ in range(400):
+                x.add_(1.0)
+        for _ in range(n // 400):
+            g.replay()
+
+    def memsets():
+        for _ in range(n // 4):
+            dsmall.zero_()
+
     for name, fn in (("idle_2s", idle), ("eager_kernels", kernels), ("graph_replays", graph), ("h2d_pinned", h2d),
                      ("d2h_pinned", d2h), ("event_query", ev_query), ("event_sync", ev_sync),
                      ("pin_churn", pin_churn), ("pageable_h2d", pageable_h2d), ("d2h_event_sync", d2h_event_sync),
-                     ("two_streams", two_streams), ("item_sync", item_sync)):
+                     ("two_streams", two_streams), ("item_sync", item_sync), ("lib_gemm", lib_gemm),
+                     ("torch_matmul", torch_matmul), ("lib_norm", lib_norm), ("big_graph", big_graph),
+                     ("memsets", memsets)):
         phase(name, fn, res)
     os.makedirs("gpurun_out", exist_ok=True)
     with open("gpurun_out/hip_thread_probe.json", "w") as f:

@@ -355,12 +355,16 @@ PF8_MAXP = 1024             # key pages per w8 work item (page ids staged in LDS
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
 # split long key ranges until a prefill launch has about this many workgroups
 PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
-# makespan planner (PF_OVERHEAD_PAGES > 0): pick the split length that minimises
+# makespan planner (PF_OVERHEAD_PAGES > 0): where the fixed-target rule would split
+# (too few tiles to fill the chip), pick instead the split length that minimises
 # the launch's estimated makespan on the CU slots, pricing every work item at its
-# pages + this many pages of fixed cost (Q load, first DMAs, epilogue, merge share);
-# 0 = the fixed-target rule above
-PF_OVERHEAD_PAGES = float(os.environ.get("K8S_PF_OVERHEAD_PAGES", "0"))
+# pages + this many pages of fixed cost (Q load, first DMAs, epilogue, merge share).
+# Replayed steady-state mix (profiles/r4/planner/): fixed target 635.5 -> 725.5
+# TFLOP/s at 8 pages (200-700-token extends -24 %, longer ones -7 %); applying it
+# to launches with enough tiles too (PF_MAKESPAN_ALL) 675-715; 0 = the fixed target.
+PF_OVERHEAD_PAGES = float(os.environ.get("K8S_PF_OVERHEAD_PAGES", "8"))
 PF_CU_SLOTS = 256           # concurrent prefill workgroups: one 8-wave w8 workgroup per CU
+PF_MAKESPAN_ALL = os.environ.get("K8S_PF_MAKESPAN_ALL", "0") == "1"
 _NO_END = 1 << 30
 
 
@@ -440,12 +444,13 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
         return plan
     pages = [(end + 63) // 64 for end, _, _, _ in tiles]
     total = sum(pages)
-    if PF_OVERHEAD_PAGES > 0 and pages:
+    enough = len(tiles) * nkv >= target_wgs // 2
+    if PF_OVERHEAD_PAGES > 0 and pages and (PF_MAKESPAN_ALL or not enough):
         part = _makespan_part(pages, nkv, PF_OVERHEAD_PAGES, max_part, max_slots,
                               PF_CU_SLOTS if max_part is not None else 2 * PF_CU_SLOTS)
     else:
         # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
-        part = max(pages) if pages and len(tiles) * nkv >= target_wgs // 2 else max(4, -(-total * nkv // target_wgs))
+        part = max(pages) if pages and enough else max(4, -(-total * nkv // target_wgs))
     if max_part is not None:
         part = min(part, max_part)
     while sum(-(-p // part) for p in pages if p > part) > max_slots:
@@ -499,9 +504,11 @@ def _makespan_part(pages: List[int], nkv: int, overhead: float, max_part: Option
         # piece lengths of tile i: floor / ceil of p_i / k_i (the planner's bounds split)
         lo = pg // k
         n_hi = pg - lo * k
-        lens = np.concatenate([np.repeat(lo + 1, n_hi), np.repeat(lo, k - n_hi)])
-        lens = np.sort(np.repeat(lens, nkv))[::-1]
-        t = float(lens[::slots].sum()) + overhead * (-(-lens.size // slots))
+        lens = np.sort(np.concatenate([np.repeat(lo + 1, n_hi), np.repeat(lo, k - n_hi)]))[::-1]
+        # every piece runs once per kv head: round r of the nkv-fold list starts at
+        # its element r * slots, i.e. element (r * slots) // nkv of the piece list
+        rounds = -(-lens.size * nkv // slots)
+        t = float(lens[(np.arange(rounds) * slots) // nkv].sum()) + overhead * rounds
         if best_t is None or t < best_t:
             best, best_t = part, t
     return best

@@ -79,3 +79,39 @@ def test_prefill_plan_caps_w8_items_at_lds_page_table(monkeypatch):
     monkeypatch.setenv("K8SRCA_PF_W8", "0")
     plan = A.plan_prefill([0, 66_000], 4, 64, None, nkv=8)
     assert plan.n_merge == 0
+
+
+def test_prefill_makespan_planner_covers_keys_and_balances(monkeypatch):
+    """The makespan split choice (K8S_PF_OVERHEAD_PAGES > 0): every tile's items
+    still tile its key range exactly once, the slot budget holds, and on a
+    200-700-token extend over a ~5k context (7 tiles x 8 heads of ~83 pages) it
+    picks a split whose round count is full rather than a few items over a
+    multiple of the CU slots."""
+    monkeypatch.setenv("K8SRCA_PF_W8", "1")
+    monkeypatch.setattr(A, "PF_OVERHEAD_PAGES", 3.0)
+    monkeypatch.setattr(A, "PF_MAKESPAN_ALL", True)
+    ctx, q = [5277], [437]
+    plan = A.plan_prefill([0, q[0]], 4, 64, ctx, nkv=8)
+    spans = {}
+    for t, k0, k1 in zip(plan.tok0, plan.kv0, plan.kv1):
+        spans.setdefault(t, []).append((k0, k1))
+    for t, sp in spans.items():
+        sp.sort()
+        assert sp[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
+        assert sp[-1][1] == -(-(ctx[0] - q[0] + t + min(64, q[0] - t)) // 64)
+    n_wg = plan.n_tiles * 8
+    rounds = -(-n_wg // A.PF_CU_SLOTS)
+    assert n_wg > (rounds - 1) * A.PF_CU_SLOTS + A.PF_CU_SLOTS // 2  # the last round is at least half full
+    assert sum(plan.m_np) <= A.PF_MAX_SLOTS
+    # a fresh 8k prompt: 32 causal tiles x 8 heads fill the CUs once, but the
+    # tiles run 1..128 pages -- the longest ones are split so the launch is not
+    # twice its average work (the fixed-target rule leaves them whole)
+    plan = A.plan_prefill([0, 8192], 4, 64, [8192], nkv=8)
+    longest = max(b - a for a, b in zip(plan.kv0, plan.kv1))
+    assert plan.n_merge > 0 and longest < 128
+    monkeypatch.setattr(A, "PF_OVERHEAD_PAGES", 0.0)
+    assert A.plan_prefill([0, 8192], 4, 64, [8192], nkv=8).n_merge == 0
+    # the default (makespan only where the fixed rule splits) leaves it whole too
+    monkeypatch.setattr(A, "PF_OVERHEAD_PAGES", 8.0)
+    monkeypatch.setattr(A, "PF_MAKESPAN_ALL", False)
+    assert A.plan_prefill([0, 8192], 4, 64, [8192], nkv=8).n_merge == 0

@@ -164,6 +164,7 @@ def main():
         # prefill: the 8-wave LDS-DMA kernel (K8SRCA_PF_W8=1) and the 4-wave pg64
         # kernel interleaved per recorded step (same process, same data)
         kinds0 = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        pf_ovh0, pf_all0 = A.PF_OVERHEAD_PAGES, A.PF_MAKESPAN_ALL  # the planner defaults (arms without "@")
         targets = [int(t) for t in args.pf_targets.split(",")] if args.pf_targets else [A.PF_TARGET_WGS]
         # arms: (kernel kind, planner split target in workgroups); the label keeps the old form for one target
         kinds = tuple(k if len(targets) == 1 else f"{k}@{t}" for t in targets for k in kinds0)
@@ -180,8 +181,11 @@ def main():
             for k in kinds:
                 os.environ["K8SRCA_PF_W8"] = k.split("@")[0]
                 arm = k.split("@")[1] if "@" in k else None
-                A.PF_OVERHEAD_PAGES = float(arm[1:]) if arm and arm.startswith("o") else 0.0
-                A.PF_TARGET_WGS = int(arm) if arm and not arm.startswith("o") else targets[0]
+                # "@o<pages>": makespan split choice everywhere; "@h<pages>": only where the
+                # fixed-target rule would split; "@<n>": fixed target of n workgroups
+                A.PF_OVERHEAD_PAGES = float(arm[1:]) if arm and arm[0] in "oh" else (0.0 if arm else pf_ovh0)
+                A.PF_MAKESPAN_ALL = bool(arm and arm[0] == "o") or (pf_all0 and not arm)
+                A.PF_TARGET_WGS = int(arm) if arm and arm[0] not in "oh" else targets[0]
                 torch.manual_seed(i)
                 meta, nb = make_meta(ctx, ql, nq, nkv, BS, dev, False)
                 if k == kinds[0]:
@@ -200,7 +204,7 @@ def main():
                                                                f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
         os.environ["K8SRCA_PF_W8"] = kinds0[0]
         A.PF_TARGET_WGS = targets[0]
-        A.PF_OVERHEAD_PAGES = 0.0
+        A.PF_OVERHEAD_PAGES, A.PF_MAKESPAN_ALL = pf_ovh0, pf_all0
         if args.pf_steps_out:
             with open(args.pf_steps_out, "w") as f:
                 for v in per_step.values():

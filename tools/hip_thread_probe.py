@@ -13,10 +13,13 @@ usage (GPU box): python tools/hip_thread_probe.py [--n 20000]
 import argparse
 import json
 import os
+import sys
 import threading
 import time
 
-import torch
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+import torch  # noqa: E402
 
 
 def native_cpu():
@@ -50,6 +53,7 @@ def phase(name, fn, res):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=20000)
+    ap.add_argument("--phases", default="", help="comma list of phase names (default: all)")
     a = ap.parse_args()
     dev = torch.device("cuda:0")
     x = torch.zeros(1024, device=dev)
@@ -176,9 +180,11 @@ def main():
                      ("two_streams", two_streams), ("item_sync", item_sync), ("lib_gemm", lib_gemm),
                      ("torch_matmul", torch_matmul), ("lib_norm", lib_norm), ("big_graph", big_graph),
                      ("memsets", memsets)):
+        if a.phases and name not in a.phases.split(","):
+            continue
         phase(name, fn, res)
     os.makedirs("gpurun_out", exist_ok=True)
-    with open("gpurun_out/hip_thread_probe.json", "w") as f:
+    with open(os.environ.get("PROBE_OUT", "gpurun_out/hip_thread_probe.json"), "w") as f:
         json.dump(res, f, indent=1)
 
 

@@ -170,19 +170,52 @@ def main():
         for _ in range(n // 400):
             g.replay()
 
+    idx = torch.randint(0, 1024, (4096,), device=dev)
+
+    def index_ops():  # torch kernels that carry a device-side assert (index bounds)
+        for _ in range(n // 4):
+            x.index_select(0, idx)
+
+    xb = torch.randn(4096, 4096, device=dev).bfloat16()
+    wb = torch.randn(28672, 4096, device=dev).bfloat16()
+
+    def big_gemm():  # long hand-written GEMM kernels, few launches (gemm_big: no library call)
+        for _ in range(max(1, n // 200)):
+            LIN.gemm_big(xb, wb)
+
+    def _queue_gemms(k):
+        for _ in range(k):
+            LIN.gemm_big(xb, wb)
+        e = torch.cuda.Event()
+        e.record()
+        return e
+
+    def wait_sync():  # a host thread blocked in a HIP wait while the GPU works
+        for _ in range(5):
+            _queue_gemms(max(1, n // 1000)).synchronize()
+
+    def wait_poll():  # the same work, the host polling the event with short sleeps
+        for _ in range(5):
+            e = _queue_gemms(max(1, n // 1000))
+            while not e.query():
+                time.sleep(0.0002)
+
+    def one_matmul():  # a single library GEMM: does it switch the thread on for later work?
+        torch.matmul(xa, wa.t())
+
     def memsets():
         for _ in range(n // 4):
             dsmall.zero_()
 
-    for name, fn in (("idle_2s", idle), ("eager_kernels", kernels), ("graph_replays", graph), ("h2d_pinned", h2d),
-                     ("d2h_pinned", d2h), ("event_query", ev_query), ("event_sync", ev_sync),
-                     ("pin_churn", pin_churn), ("pageable_h2d", pageable_h2d), ("d2h_event_sync", d2h_event_sync),
-                     ("two_streams", two_streams), ("item_sync", item_sync), ("lib_gemm", lib_gemm),
-                     ("torch_matmul", torch_matmul), ("lib_norm", lib_norm), ("big_graph", big_graph),
-                     ("memsets", memsets)):
-        if a.phases and name not in a.phases.split(","):
-            continue
-        phase(name, fn, res)
+    phases = {"idle_2s": idle, "eager_kernels": kernels, "graph_replays": graph, "h2d_pinned": h2d,
+              "d2h_pinned": d2h, "event_query": ev_query, "event_sync": ev_sync, "pin_churn": pin_churn,
+              "pageable_h2d": pageable_h2d, "d2h_event_sync": d2h_event_sync, "two_streams": two_streams,
+              "item_sync": item_sync, "lib_gemm": lib_gemm, "torch_matmul": torch_matmul, "lib_norm": lib_norm,
+              "big_graph": big_graph, "memsets": memsets, "index_ops": index_ops, "big_gemm": big_gemm,
+              "wait_sync": wait_sync, "wait_poll": wait_poll, "one_matmul": one_matmul}
+    # --phases runs the named phases in the given order; "name#k" repeats a phase
+    for label in (a.phases.split(",") if a.phases else list(phases)):
+        phase(label, phases[label.split("#")[0]], res)
     os.makedirs("gpurun_out", exist_ok=True)
     with open(os.environ.get("PROBE_OUT", "gpurun_out/hip_thread_probe.json"), "w") as f:
         json.dump(res, f, indent=1)

@@ -502,7 +502,8 @@ def gemm_big(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None, silu: b
              pipe: int = None, splits: int = 1) -> torch.Tensor:
     """``x @ w.T`` on the prefill-size MFMA kernel (csrc/kernels/gemm_big.hip:
     256 x 256 x 64 tiles, eight-phase ping-pong schedule, LDS-DMA staging;
-    ``pipe`` = schedule variant, 3 the default).  ``silu=True``: ``w`` is the gate_up weight
+    ``pipe`` = the VAR bits (1 = the ping-pong stagger, the default ``BIG_PIPE``;
+    +2 static priority, +4 the 32x32x16-MFMA form)).  ``silu=True``: ``w`` is the gate_up weight
     [2I, K] and the result is ``silu(x @ Wg.T) * (x @ Wu.T)`` [M, I] -- the
     SwiGLU epilogue, with the unfused path's bf16 rounding of gate and up.
     ``splits`` > 1: K split over that many workgroups per tile (fp32 partials

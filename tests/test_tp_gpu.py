@@ -37,13 +37,17 @@ def _worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
-    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=20.0)
+    # generous: inside a long GPU suite a rank's first step (lazy code-object and library
+    # initialisation) can lag its peer's by seconds; the stall tests below use 1 s on purpose
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=60.0)
     res = {}
     for graphs in (False, True):
         cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
                            temperature=0.0, use_graphs=graphs)
         model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")
         eng = LLMEngine(cfg, pc, model=model)
+        torch.cuda.synchronize()
+        dist.barrier()  # both engines built before rank 0's first collective starts its clock
         # pass 0 captures every decode bucket; pass 1 replays the same work and, on
         # the worker, runs under torch's sync checker: a worker step never waits
         # for its own GPU (its sampling winners travel over the xGMI all-to-all)

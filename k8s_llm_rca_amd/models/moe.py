@@ -89,9 +89,10 @@ class MoELayerSet:
                 device_offsets: bool = False) -> torch.Tensor:
         """Grouped SwiGLU over contiguous expert slices offsets[e]..offsets[e+1]
         (``offsets`` int32 [E_local+1], on the rows' device).  Decode-sized
-        batches use the grouped kernel (weight streaming, no host sync);
-        prefill-sized ones the per-expert library GEMMs, which pay one sync
-        for the offsets but run near the MFMA roof.  ``device_offsets``: the
+        batches use the grouped weight-streaming kernel, prefill-sized ones the
+        grouped form of gemm_big (below); neither syncs with the host.  The
+        per-expert library loop (one offsets sync) is the fallback for shapes
+        gemm_big does not take (K8SRCA_MOE_BIG=0 forces it for A/B).  ``device_offsets``: the
         grouped kernels whatever the row count (the EP dispatch buffer holds
         ``ep``-fold capacity rows, most of them the never-computed null
         expert: a host read of the offsets would stall every prefill layer).

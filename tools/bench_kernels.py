@@ -420,7 +420,9 @@ def main():
             res[f"silu_mul T{T}"] = f"{us:.1f}us {T * I * 2 * 3 / us / 1e6:.2f} TB/s"
     for k, v in res.items():
         print(f"{k:40s} {v}")
-    json.dump(res, open("gpurun_out/bench_kernels.json", "w"), indent=1)
+    out_dir = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(out_dir, exist_ok=True)
+    json.dump(res, open(os.path.join(out_dir, "bench_kernels.json"), "w"), indent=1)
 
 
 if __name__ == "__main__":

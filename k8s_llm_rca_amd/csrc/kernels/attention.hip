@@ -794,6 +794,27 @@ __device__ __forceinline__ void pf8_glds(const uint16_t* src, unsigned char* lds
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
+// VAR 6: hand-issued LDS fragment reads.  hipcc waits lgkmcnt(0) before every
+// MFMA of this loop (it does not count the reads behind the LDS-DMA traffic),
+// exposing one LDS latency per fragment pair; an asm read is invisible to its
+// waitcnt pass, so each consumer gets an explicit counted wait instead, which
+// "rewrites" the fragments it covers so the MFMA cannot be hoisted above it
+// (cdna_hip_programming.md §5.7: an asm statement's memory traffic is not modelled).
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_rd16(uint32_t addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+
 // VAR (K8SRCA_PF_W8): 2 = the compiler's schedule of the page loop; 4 = the same
 // arithmetic with the page's 16 K fragments read up front (the compiler otherwise
 // serialises read -> wait -> MFMA for the first 32 keys: 8 exposed LDS latencies
@@ -879,6 +900,7 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
   const int kreg = (r & 3) + 4 * (r >> 3), khi = (r >> 2) & 1;
   const int krow0 = pf_key(kreg, khi);
   constexpr int AHEAD = PF8_NB - 1;  // pages in flight beyond the current one
+  const uint32_t lds_base = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) unsigned char*)lds;
 
   if (np > 0) {
 #pragma unroll
@@ -894,7 +916,32 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
       const unsigned char* kl = lds + (i % PF8_NB) * PF8_STAGE;
       const unsigned char* vl = kl + PF_KBYTES;
       f32x16 sc[2];
-      if constexpr (VAR >= 4) {
+      bf16x8 vq[16];  // VAR 6: the page's V fragments, read during the softmax
+      if constexpr (VAR == 6) {
+        // K fragments: 16 reads (the second 32-key tile at +8 KB), then each MFMA
+        // pair waits only for its own two reads
+        const uint32_t ka = lds_base + (uint32_t)((i % PF8_NB) * PF8_STAGE + krow0 * 256);
+        bf16x8 kf[2][8];
+#define K8S_KRD(S)                                                               \
+  {                                                                              \
+    const uint32_t a_ = ka + (uint32_t)((((2 * (S) + hi) ^ (krow0 & 15)) << 4)); \
+    kf[0][S] = lds_rd16<0>(a_);                                                  \
+    kf[1][S] = lds_rd16<8192>(a_);                                               \
+  }
+        K8S_KRD(0) K8S_KRD(1) K8S_KRD(2) K8S_KRD(3) K8S_KRD(4) K8S_KRD(5) K8S_KRD(6) K8S_KRD(7)
+#undef K8S_KRD
+#pragma unroll
+        for (int kt = 0; kt < 2; ++kt)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) sc[kt][e] = 0.f;
+#define K8S_KMM(S)                                                                   \
+  lgkm_wait<14 - 2 * (S)>(kf[0][S], kf[1][S]);                                       \
+  sc[0] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[0][S], qf[S], sc[0], 0, 0, 0); \
+  sc[1] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[1][S], qf[S], sc[1], 0, 0, 0); \
+  __builtin_amdgcn_sched_barrier(0); /* the next wait stays behind these MFMAs */
+        K8S_KMM(0) K8S_KMM(1) K8S_KMM(2) K8S_KMM(3) K8S_KMM(4) K8S_KMM(5) K8S_KMM(6) K8S_KMM(7)
+#undef K8S_KMM
+      } else if constexpr (VAR >= 4) {
         // key 32 kt + krow0 has the swizzle of krow0 (32 kt is a multiple of 16):
         // the second tile's reads are the first's at +8 KB
         const unsigned char* kr = kl + krow0 * 256;
@@ -957,6 +1004,23 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
           for (int e = 0; e < 16; ++e) cmax = fmaxf(cmax, sc[kt][e]);
         cmax = fmaxf(cmax, __shfl_xor(cmax, 32, 64));
       }
+      if constexpr (VAR == 6) {
+        // V fragments of d-row 32 dt + r: the row's chunk swizzle (d >> 1) & 7 does
+        // not depend on dt (32 dt is a multiple of 16), so dt is the +4 KB immediate;
+        // issued now, they land while the exps below run
+        const uint32_t va = lds_base + (uint32_t)((i % PF8_NB) * PF8_STAGE + PF_KBYTES + r * 128);
+        const int sw = (r >> 1) & 7;
+#define K8S_VRD(KT, S)                                                            \
+  {                                                                               \
+    const uint32_t a_ = va + (uint32_t)((((4 * (KT) + 2 * (S) + hi) ^ sw) << 4)); \
+    vq[0 + 2 * (KT) + (S)] = lds_rd16<0>(a_);                                     \
+    vq[4 + 2 * (KT) + (S)] = lds_rd16<4096>(a_);                                  \
+    vq[8 + 2 * (KT) + (S)] = lds_rd16<8192>(a_);                                  \
+    vq[12 + 2 * (KT) + (S)] = lds_rd16<12288>(a_);                                \
+  }
+        K8S_VRD(0, 0) K8S_VRD(0, 1) K8S_VRD(1, 0) K8S_VRD(1, 1)
+#undef K8S_VRD
+      }
       const float mcand = cmax * a.scale_log2;
       const bool upd = mcand > m + 8.f;
       const float mnew = upd ? mcand : m;
@@ -986,25 +1050,38 @@ __global__ void __launch_bounds__(512, 1) attn_prefill_w8_kernel(AttnArgs a) {
 #pragma unroll
           for (int e = 0; e < 16; ++e) o[dt][e] *= alpha;
       }
+      if constexpr (VAR == 6) {
+        // issue order: (kt, s) outer, dt inner -> read q = 4 (2 kt + s) + dt
+#define K8S_VMM(KT, S, DT)                                                                                  \
+  lgkm_wait<15 - (4 * (2 * (KT) + (S)) + (DT))>(vq[4 * (DT) + 2 * (KT) + (S)]);                             \
+  o[DT] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vq[4 * (DT) + 2 * (KT) + (S)], pf[KT][S], o[DT], 0, 0, 0); \
+  __builtin_amdgcn_sched_barrier(0);
+        K8S_VMM(0, 0, 0) K8S_VMM(0, 0, 1) K8S_VMM(0, 0, 2) K8S_VMM(0, 0, 3)
+        K8S_VMM(0, 1, 0) K8S_VMM(0, 1, 1) K8S_VMM(0, 1, 2) K8S_VMM(0, 1, 3)
+        K8S_VMM(1, 0, 0) K8S_VMM(1, 0, 1) K8S_VMM(1, 0, 2) K8S_VMM(1, 0, 3)
+        K8S_VMM(1, 1, 0) K8S_VMM(1, 1, 1) K8S_VMM(1, 1, 2) K8S_VMM(1, 1, 3)
+#undef K8S_VMM
+      } else {
 #pragma unroll
-      for (int dt = 0; dt < 4; ++dt) {
-        const int d = 32 * dt + r;
-        const unsigned char* vr = vl + d * 128;
-        const int sw = (d >> 1) & 7;
+        for (int dt = 0; dt < 4; ++dt) {
+          const int d = 32 * dt + r;
+          const unsigned char* vr = vl + d * 128;
+          const int sw = (d >> 1) & 7;
 #pragma unroll
-        for (int kt = 0; kt < 2; ++kt)
+          for (int kt = 0; kt < 2; ++kt)
 #pragma unroll
-          for (int s = 0; s < 2; ++s) {
-            const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
-            o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
-          }
+            for (int s = 0; s < 2; ++s) {
+              const bf16x8 vf = *reinterpret_cast<const bf16x8*>(vr + (((4 * kt + 2 * s + hi) ^ sw) << 4));
+              o[dt] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf, pf[kt][s], o[dt], 0, 0, 0);
+            }
+        }
       }
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // no DMA may outlive the workgroup's LDS
 
-  if constexpr (VAR == 5) {
+  if constexpr (VAR >= 5) {
     // Epilogue through LDS (the ring is free once every wave has left the loop):
     // each wave stages its 32 rows x 128 dims as bf16 (O / l) in a private,
     // 272-B-pitch image (conflict-free 8-B writes), then stores 16 B per lane
@@ -1168,18 +1245,18 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
   return (int)hipGetLastError();
 }
 
-// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups -- unset / 1 / 5: the explicit
-// page-loop schedule with the LDS-staged bf16 epilogue (VAR 5), 4: the same loop
-// with per-lane fp32 partial / dwordx2 row stores, 2: the compiler's schedule --
-// and 0: the 128-row pg64 kernel.  Read per launch, like the planner reads it per
-// plan.  Replayed steady-state mix (tools/bench_kernels.py --what replay,
-// profiles/r4/prefill_attn/, interleaved in one process): 5 = 649 / 4 = 624 /
-// 2 = 628 TFLOP/s (VAR 5 ahead on every step class: long extends -3 %, 200-700-
-// token extends -5 %, jump-forward chunks -5 % time); an earlier box: 4 = 669 /
-// 2 = 648, pg64 633 (r3: static priority 651, staggered late waves 608).
+// K8SRCA_PF_W8: 256-row LDS-DMA prefill workgroups -- unset / 1 / 6: the explicit
+// page loop with hand-issued LDS reads (counted waits, V fragments read during the
+// softmax) and the LDS-staged bf16 epilogue (VAR 6); 5: the same with hipcc's own
+// LDS reads (a full lgkmcnt(0) before every MFMA pair); 4: + per-lane fp32 partial /
+// dwordx2 row stores; 2: the compiler's schedule -- and 0: the 128-row pg64 kernel.
+// Read per launch, like the planner reads it per plan.  Replayed steady-state mix
+// (tools/bench_kernels.py --what replay, profiles/r4/prefill_attn/, interleaved in
+// one process): 6 = 711 / 5 = 684 TFLOP/s; earlier pairs 5 = 649 / 4 = 624 / 2 = 628
+// and 4 = 669 / 2 = 648, pg64 633 (r3: static priority 651, staggered late waves 608).
 static int prefill_w8() {
   const char* v = std::getenv("K8SRCA_PF_W8");
-  if (!v || !v[0] || v[0] == '1') return 5;
+  if (!v || !v[0] || v[0] == '1') return 6;
   return v[0] - '0';
 }
 
@@ -1227,8 +1304,10 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
     const int var = prefill_w8();
     const bool w8 = var > 0 && PF8_ROWS % a.G == 0;
     a.pf_rows = w8 ? PF8_ROWS : PF_ROWS;
-    a.pf_bf16 = w8 && var == 5;
-    if (w8 && var == 5)
+    a.pf_bf16 = w8 && var >= 5;
+    if (w8 && var == 6)
+      hipLaunchKernelGGL(attn_prefill_w8_kernel<6>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
+    else if (w8 && var == 5)
       hipLaunchKernelGGL(attn_prefill_w8_kernel<5>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else if (w8 && var == 4)
       hipLaunchKernelGGL(attn_prefill_w8_kernel<4>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);

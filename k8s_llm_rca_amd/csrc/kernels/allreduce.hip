@@ -61,6 +61,7 @@ struct ARCtx {
   bool used;
   int sim;          // loopback stand-in (tp-sim): every "peer" buffer is local, waits are skipped
   void* own_alloc;  // loopback: the one allocation holding all `world` buffers
+  int max_blocks;   // grid cap of every collective (the same on every rank; k8s_ar_set_max_blocks)
 };
 
 static ARCtx g_ctx[16];
@@ -379,7 +380,7 @@ K8S_API int k8s_ar_alltoall_bf16(int id, const void* send, void* recv, long chun
   if (chunk <= 0) return 0;
   if (chunk % 8 || 2 * chunk * c.world > 2 * c.max_bytes || send == recv) return (int)hipErrorInvalidValue;
   long nb = (chunk + 4095) / 4096;
-  if (nb > AR_MAX_BLOCKS) nb = AR_MAX_BLOCKS;
+  if (nb > c.max_blocks) nb = c.max_blocks;
   long slice = (chunk + nb - 1) / nb;
   slice = (slice + 7) / 8 * 8;
   nb = (chunk + slice - 1) / slice;
@@ -428,6 +429,7 @@ K8S_API int k8s_ar_register(int world, int rank, void** bases, long max_bytes, d
     c.timeout_ticks = (uint64_t)(timeout_s * khz * 1000.0);
     c.sim = 0;
     c.own_alloc = nullptr;
+    c.max_blocks = AR_MAX_BLOCKS;
     c.used = true;
     return id;
   }
@@ -458,6 +460,18 @@ K8S_API int k8s_ar_register_loopback(int world, long max_bytes) {
   return id;
 }
 
+// Cap the grid of this communicator's collectives (1..AR_MAX_BLOCKS; every rank
+// must set the same cap: block b of each rank pairs with block b of the others).
+// Ranks that SHARE one GPU (the shared-GPU TP / EP tests) need it: a collective's
+// blocks spin until the peer's arrive, and a full-size grid of spinning blocks on
+// every CU can leave no room (registers, LDS) for the peer process's next kernel,
+// so the peer never reaches the collective.  One rank per GPU never needs it.
+K8S_API int k8s_ar_set_max_blocks(int id, int nb) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used || nb < 1 || nb > AR_MAX_BLOCKS) return (int)hipErrorInvalidValue;
+  g_ctx[id].max_blocks = nb;
+  return 0;
+}
+
 K8S_API int k8s_ar_unregister(int id) {
   if (id < 0 || id >= 16) return (int)hipErrorInvalidValue;
   if (g_ctx[id].own_alloc) (void)hipFree(g_ctx[id].own_alloc);
@@ -474,7 +488,7 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
   if (n % 8 || 2 * n > c.max_bytes) return (int)hipErrorInvalidValue;
   const long unit = 8L * (mode == 2 ? c.world : 1);
   long nb = (n + 4095) / 4096;  // >= 8 KB of bf16 per block
-  if (nb > AR_MAX_BLOCKS) nb = AR_MAX_BLOCKS;
+  if (nb > c.max_blocks) nb = c.max_blocks;
   long slice = (n + nb - 1) / nb;
   slice = (slice + unit - 1) / unit * unit;
   nb = (n + slice - 1) / slice;
@@ -498,7 +512,7 @@ K8S_API int k8s_ar_addnorm_bf16(int id, const void* in, void* res, const void* w
   const long need = (long)T * H * 2 + 4L * T;  // staged rows / (two-shot) slice sums + sums of squares
   if (H % 8 || H / 8 > AN_THREADS * AN_NC || need > c.max_bytes || (mode == 2 && (H / 8) % c.world))
     return (int)hipErrorInvalidValue;
-  const int nb = T < AR_MAX_BLOCKS ? T : AR_MAX_BLOCKS;
+  const int nb = T < c.max_blocks ? T : c.max_blocks;
   if (mode == 2)
     hipLaunchKernelGGL(ar_addnorm_kernel<true>, dim3(nb), dim3(AN_THREADS), 0, s, (const uint16_t*)in,
                        (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps, c.world, c.rank, c.peers,

@@ -794,27 +794,7 @@ __device__ __forceinline__ void pf8_glds(const uint16_t* src, unsigned char* lds
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds_dst, 16, 0, 0);
 }
 
-// VAR 6: hand-issued LDS fragment reads.  hipcc waits lgkmcnt(0) before every
-// MFMA of this loop (it does not count the reads behind the LDS-DMA traffic),
-// exposing one LDS latency per fragment pair; an asm read is invisible to its
-// waitcnt pass, so each consumer gets an explicit counted wait instead, which
-// "rewrites" the fragments it covers so the MFMA cannot be hoisted above it
-// (cdna_hip_programming.md §5.7: an asm statement's memory traffic is not modelled).
-template <int OFF>
-__device__ __forceinline__ bf16x8 lds_rd16(uint32_t addr) {
-  bf16x8 v;
-  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
-  return v;
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(bf16x8& a) {
-  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
-}
-template <int N>
-__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
-  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
-}
-
+// VAR 6's hand-issued LDS reads with counted waits: lds_rd16 / lgkm_wait (common.h).
 // VAR (K8SRCA_PF_W8): 2 = the compiler's schedule of the page loop; 4 = the same
 // arithmetic with the page's 16 K fragments read up front (the compiler otherwise
 // serialises read -> wait -> MFMA for the first 32 keys: 8 exposed LDS latencies

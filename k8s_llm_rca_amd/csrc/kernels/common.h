@@ -88,4 +88,26 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
   return r;
 }
 
+// Hand-issued LDS fragment reads.  In the LDS-DMA kernels hipcc waits lgkmcnt(0)
+// before every MFMA that consumes an LDS fragment (it does not count the reads
+// behind the DMA traffic), exposing one LDS latency per fragment group; an asm read is invisible to its
+// waitcnt pass, so each consumer gets an explicit counted wait instead, which
+// "rewrites" the fragments it covers so the MFMA cannot be hoisted above it
+// (cdna_hip_programming.md §5.7: an asm statement's memory traffic is not modelled).
+template <int OFF>
+__device__ __forceinline__ bf16x8 lds_rd16(uint32_t addr) {
+  bf16x8 v;
+  asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");
+  return v;
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a) {
+  asm volatile("s_waitcnt lgkmcnt(%1)" : "+v"(a) : "n"(N) : "memory");
+}
+template <int N>
+__device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
+  asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
+}
+
+
 }  // namespace k8s

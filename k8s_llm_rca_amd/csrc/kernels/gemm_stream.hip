@@ -23,6 +23,8 @@
 //   * split-K over gridDim.y: fp32 partials [split][M][N] reduced by a
 //     vectorised kernel, or left for a fused consumer (the next residual add +
 //     RMSNorm, k8s_splitk_addnorm) -- the same contract as gemm_mid.
+#include <cstdlib>
+
 #include "common.h"
 
 namespace k8s {
@@ -235,7 +237,26 @@ constexpr int glds_lds_elems() {
 // strip's first W row ([N][K] row-major, K-slice offset already applied);
 // nch: 64-deep chunks in the slice; sm: the kernel's one __shared__ array of
 // glds_lds_elems<MTW, NB>() elements.
-template <int MTW, int NB, int NF = 4>
+// HAND: the stage's MTW X and NF W fragments per 32-deep half are read by
+// hand-issued ds_read_b128 (common.h lds_rd16) and each fragment column's MFMAs
+// wait only for the reads they consume (hipcc's own schedule waits lgkmcnt(0)
+// before every group: one LDS latency per NF group; K8SRCA_GLDS_HAND=0 restores it).
+template <int MTW, int NF, int CF>
+__device__ __forceinline__ void glds_mm(f32x4 (&acc)[MTW][NF], bf16x8 (&xf)[MTW], bf16x8 (&wf)[NF]) {
+  if constexpr (CF < NF) {
+    if constexpr (CF == 0) {
+#pragma unroll
+      for (int mt = 0; mt < MTW; ++mt) lgkm_wait<NF - 1>(xf[mt]);
+    }
+    lgkm_wait<NF - 1 - CF>(wf[CF]);
+#pragma unroll
+    for (int mt = 0; mt < MTW; ++mt) acc[mt][CF] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(xf[mt], wf[CF], acc[mt][CF], 0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);  // the next column's wait stays behind these MFMAs
+    glds_mm<MTW, NF, CF + 1>(acc, xf, wf);
+  }
+}
+
+template <int MTW, int NB, int NF = 4, bool HAND = false>
 __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int ldx, int M,
                                            const uint16_t* __restrict__ wstrip, int K, int nch, uint16_t* sm,
                                            f32x4 (&acc)[MTW][NF], int silu_i = 0) {
@@ -268,9 +289,29 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
 #pragma unroll
     for (int i = 0; i < XPT; ++i) glds16(xsrc[i] + c * kSC, st + WST + (256 * i + 64 * wv) * 8);
   };
+  const uint32_t lds0 = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint16_t*)sm;
   auto compute = [&](int stage) {
     const uint16_t* ws = sm + stage * STG;
     const uint16_t* xs = ws + WST;
+    if constexpr (HAND) {
+      const uint32_t wb = lds0 + 2u * (uint32_t)(stage * STG), xb = wb + 2u * WST;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        bf16x8 xf[MTW], wf[NF];
+#pragma unroll
+        for (int mt = 0; mt < MTW; ++mt) {
+          const int m = m_base + 16 * mt + r;
+          xf[mt] = lds_rd16<0>(xb + 2u * (uint32_t)(m * kSC + 8 * ((4 * s + g) ^ (m & 7))));
+        }
+#pragma unroll
+        for (int cf = 0; cf < NF; ++cf) {
+          const int n = 16 * cf + r;
+          wf[cf] = lds_rd16<0>(wb + 2u * (uint32_t)(n * kSC + 8 * ((4 * s + g) ^ (n & 7))));
+        }
+        glds_mm<MTW, NF, 0>(acc, xf, wf);
+      }
+      return;
+    }
 #pragma unroll
     for (int s = 0; s < 2; ++s) {
       bf16x8 xf[MTW];
@@ -351,7 +392,7 @@ __device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][NF], int M, u
     }
 }
 
-template <int MTW, int NB, int NF>
+template <int MTW, int NB, int NF, bool HAND>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                         int ldy, float* __restrict__ part, int M, int N, int K,
@@ -364,7 +405,7 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
   for (int mt = 0; mt < MTW; ++mt)
 #pragma unroll
     for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
-  glds_strip<MTW, NB, NF>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
+  glds_strip<MTW, NB, NF, HAND>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
   if (silu_i)
     glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0, true);
   else if (gridDim.y == 1)
@@ -431,11 +472,24 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_kernel(const float* __
   *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + n) = o;
 }
 
+// the hand-issued LDS reads of glds_strip (default; K8SRCA_GLDS_HAND=0: hipcc's
+// own reads, A/B, read per launch).  Bit-identical; 0-5 % faster per projection
+// at M = 64-192 (tools/glds_hand_ab.py, profiles/r4/glds_hand/): the decode GEMMs
+// are bound by their DMA stream more than by the exposed LDS latency.
+static bool glds_hand() {
+  const char* e = std::getenv("K8SRCA_GLDS_HAND");
+  return !(e && e[0] == '0');
+}
+
 template <int MTW, int NB, int NF = 4>
 static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
                               int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
-  hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N, K,
-                     kslice, silu_i);
+  if (glds_hand())
+    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF, true>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N,
+                       K, kslice, silu_i);
+  else
+    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF, false>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N,
+                       K, kslice, silu_i);
   return hipGetLastError();
 }
 

@@ -46,6 +46,7 @@ def _bind(L) -> None:
         "k8s_ar_handle_size": ([], c_int),
         "k8s_ar_register": ([c_int, c_int, ctypes.POINTER(P), c_long, ctypes.c_double], c_int),
         "k8s_ar_unregister": ([c_int], c_int),
+        "k8s_ar_set_max_blocks": ([c_int, c_int], c_int),
         "k8s_ar_allreduce_bf16": ([c_int, P, P, c_long, c_int, P], c_int),
         "k8s_ar_alltoall_bf16": ([c_int, P, P, c_long, P], c_int),
         "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
@@ -68,7 +69,12 @@ class XgmiAllReduce:
     """In-place bf16 sum over a process group whose ranks share an xGMI mesh
     (one process per GPU, all in one node)."""
 
-    def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 10.0):
+    def __init__(self, group=None, max_bytes: int = 8 << 20, timeout_s: float = 10.0,
+                 max_blocks: Optional[int] = None):
+        """``max_blocks`` caps every collective's grid (the same on every rank):
+        needed only when ranks SHARE one GPU -- a full grid of blocks spinning
+        for their peers can starve the peer process of the CUs its next kernel
+        needs (csrc/kernels/allreduce.hip k8s_ar_set_max_blocks)."""
         L = lib()
         _bind(L)
         self.L = L
@@ -98,6 +104,8 @@ class XgmiAllReduce:
         self.id = L.k8s_ar_register(self.world, self.rank, self._bases, self.max_bytes, float(timeout_s))
         if self.id < 0:
             raise RuntimeError("k8s_ar_register failed")
+        if max_blocks is not None:
+            _check(L.k8s_ar_set_max_blocks(self.id, int(max_blocks)), "k8s_ar_set_max_blocks")
         torch.cuda.synchronize()
         dist.barrier(group=group)
 

@@ -16,6 +16,10 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
+# two ranks share cuda:0: cap the xGMI collectives' grids so a rank's blocks spinning
+# for its peer never hold every CU the peer's next kernel needs (XgmiAllReduce max_blocks)
+SHARED_GPU_AR_BLOCKS = 32
+
 
 def _free_port() -> int:
     s = socket.socket()
@@ -36,7 +40,7 @@ def _worker(rank, world, port, out_dir):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, ep_size=world, ep_rank=rank,
                          ep_group=dist.group.WORLD)
-    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=20.0)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=20.0, max_blocks=SHARED_GPU_AR_BLOCKS)
     cfg = get_config("tiny-mixtral", n_experts=8, init_std=0.05)
     moe = MoELayerSet(cfg, "cuda", torch.bfloat16, pc, torch.Generator(device="cuda").manual_seed(11), 0.02,
                       full_slice=True)

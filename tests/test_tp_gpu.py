@@ -17,6 +17,10 @@ import torch.multiprocessing as mp
 
 pytestmark = pytest.mark.gpu
 
+# two ranks share cuda:0: cap the xGMI collectives' grids so a rank's blocks spinning
+# for its peer never hold every CU the peer's next kernel needs (XgmiAllReduce max_blocks)
+SHARED_GPU_AR_BLOCKS = 32
+
 
 def _free_port() -> int:
     s = socket.socket()
@@ -39,7 +43,7 @@ def _worker(rank, world, port, out_dir):
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
     # generous: inside a long GPU suite a rank's first step (lazy code-object and library
     # initialisation) can lag its peer's by seconds; the stall tests below use 1 s on purpose
-    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=60.0)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=60.0, max_blocks=SHARED_GPU_AR_BLOCKS)
     res = {}
     for graphs in (False, True):
         cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
@@ -114,7 +118,7 @@ def _stall_worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
-    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0, max_blocks=SHARED_GPU_AR_BLOCKS)
     cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
                        temperature=0.0, use_graphs=True)
     model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")
@@ -186,7 +190,7 @@ def _host_stall_worker(rank, world, port, out_dir):
     torch.cuda.set_device(0)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
-    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0)
+    pc.custom_ar = XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=1.0, max_blocks=SHARED_GPU_AR_BLOCKS)
     cfg = EngineConfig(model="tiny-llama", device="cuda:0", num_blocks=64, block_size=64, max_batch_tokens=256,
                        temperature=0.0, use_graphs=True)
     model = LlamaModel(get_config("tiny-llama"), "cuda:0", torch.bfloat16, pc, seed=5, init_mode="full_slice")

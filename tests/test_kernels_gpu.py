@@ -644,6 +644,28 @@ def test_gemm_stream_vs_fp32(M, N, K, splits, cfg):
     assert torch.equal(ye, w[:, idx].t().contiguous())
 
 
+@pytest.mark.parametrize("M", [16, 64, 100, 128, 192])
+@pytest.mark.parametrize("cfg,splits", [(13, 1), (14, 4), (15, 2), (23, 4), (24, 8)])
+def test_glds_hand_reads_bit_identical(M, cfg, splits, monkeypatch):
+    """The LDS-DMA decode GEMM's hand-issued LDS reads with counted waits (the
+    default, K8SRCA_GLDS_HAND) compute exactly what hipcc's own reads compute:
+    the same MFMAs in the same order, only the waits differ."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    N, K = 1024, 2048
+    if not LIN.stream_shape_ok(M, N, K, cfg, splits):
+        pytest.skip("shape outside this configuration's launch contract")
+    torch.manual_seed(M + cfg)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
+    outs = {}
+    for h in ("0", "1"):
+        monkeypatch.setenv("K8SRCA_GLDS_HAND", h)
+        outs[h] = LIN.gemm_stream(x, w, cfg, splits)
+    assert torch.equal(outs["0"], outs["1"])
+    torch.testing.assert_close(outs["1"].float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
+
+
 @pytest.mark.parametrize("E,N,K", [(8, 256, 512), (4, 1024, 512), (8, 512, 1024)])
 @pytest.mark.parametrize("cfg", [13, 14, 16])
 @pytest.mark.parametrize("splits", [1, 2, 4])

@@ -2,5 +2,5 @@
 # contract run (the first pass also ran tools/rccl_same_gpu.py last: RCCL refuses two ranks on one GPU)
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp
-bash tools/gpu_check.sh r4final2 || exit 1
-bash tools/prof_driver.sh r4final2 || exit 1
+bash tools/gpu_check.sh r4final3 || exit 1
+bash tools/prof_driver.sh r4final3 || exit 1

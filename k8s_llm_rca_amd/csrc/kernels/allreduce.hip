@@ -47,7 +47,13 @@ constexpr size_t AR_FLAGS_A = 0;
 constexpr size_t AR_FLAGS_B = AR_FLAGS_A + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
 constexpr size_t AR_EPOCH = AR_FLAGS_B + 4 * AR_MAX_WORLD * AR_MAX_BLOCKS;
 constexpr size_t AR_STATUS = AR_EPOCH + 4 * AR_MAX_BLOCKS;  // AR_EPOCH: [0] epoch, [1] arrivals
+constexpr size_t AR_FLAGS_P = 20480;  // push epilogue: [source rank][strip] u32 (kPushMaxStrips per rank)
 constexpr size_t AR_DATA = 32768;
+static_assert(AR_STATUS + 4 <= AR_FLAGS_P && AR_FLAGS_P + 4 * AR_MAX_WORLD * kPushMaxStrips <= AR_DATA,
+              "header layout");
+// push slots follow DATA / RES / A2A: [parity][source rank][slot], 2 x max_bytes in all
+__host__ __device__ inline size_t push_region(long max_bytes) { return AR_DATA + 8 * (size_t)max_bytes; }
+static long push_slot(long max_bytes, int world) { return (max_bytes / world) / 16 * 16; }
 
 struct ARPeers {
   unsigned char* base[AR_MAX_WORLD];
@@ -113,15 +119,57 @@ __device__ __forceinline__ void ar_wait(unsigned char* own, size_t flags, int wo
   __syncthreads();
 }
 
-// sum of `world` bf16 vectors [i, i+8) at byte offset `off` of every rank's buffer
-__device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off) {
+// Push-epilogue consumer wait: the flags of strips [s0, s0 + ns) from every
+// source rank, spread over the block's threads (world * ns flags), each spin
+// bounded like ar_wait's; then a barrier, so every thread's reads follow every
+// thread's acquire.
+__device__ __forceinline__ void push_wait(unsigned char* own, int world, int s0, int ns, uint32_t e,
+                                          uint64_t timeout_ticks, int sim) {
+  if (!sim) {
+    uint32_t* status = reinterpret_cast<uint32_t*>(own + AR_STATUS);
+    for (int i = threadIdx.x; i < world * ns; i += blockDim.x) {
+      uint32_t* f = reinterpret_cast<uint32_t*>(own + AR_FLAGS_P) + (i / ns) * kPushMaxStrips + s0 + i % ns;
+      const uint64_t t0 = wall_clock64();
+      while ((int)(__hip_atomic_load(f, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_SYSTEM) - e) < 0) {
+        if (__hip_atomic_load(status, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM) != 0u) break;
+        if (wall_clock64() - t0 > timeout_ticks) {
+          __hip_atomic_store(status, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(2);
+      }
+    }
+  }
+  __syncthreads();
+}
+
+// Sum of `world` bf16 vectors in source-rank order (fp32, then one bf16
+// rounding).  WN > 0 (world == WN, the launchers' 2 / 4 / 8 instantiations):
+// the WN loads are unconditional and all issued before the first add, so a
+// chunk costs ONE memory latency -- an uncached local or xGMI peer read --
+// instead of `world` of them in a chain (the runtime-world loop, WN = 0,
+// waits for each load before the next: hipcc's waitcnt pass puts a vmcnt(0)
+// behind every conditional load; the fused epilogue measured 9-21 us for
+// 0.5-4 MiB that way).
+template <int WN, typename Addr>
+__device__ __forceinline__ u16x8 sum8_ranks(int world, Addr addr) {
   float acc[8];
 #pragma unroll
   for (int j = 0; j < 8; ++j) acc[j] = 0.f;
-  for (int p = 0; p < world; ++p) {
-    const u16x8 v = *reinterpret_cast<const u16x8*>(P.base[p] + off);
+  if constexpr (WN > 0) {
+    u16x8 v[WN];
 #pragma unroll
-    for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+    for (int p = 0; p < WN; ++p) v[p] = *reinterpret_cast<const u16x8*>(addr(p));
+#pragma unroll
+    for (int p = 0; p < WN; ++p)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[p][j]);
+  } else {
+    for (int p = 0; p < world; ++p) {
+      const u16x8 v = *reinterpret_cast<const u16x8*>(addr(p));
+#pragma unroll
+      for (int j = 0; j < 8; ++j) acc[j] += bf2f(v[j]);
+    }
   }
   u16x8 r;
 #pragma unroll
@@ -129,8 +177,21 @@ __device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off
   return r;
 }
 
+// sum of the `world` pushed bf16 vectors at byte offset `off` of slot 0 of THIS
+// rank's buffer (slots `slot` bytes apart)
+template <int WN>
+__device__ __forceinline__ u16x8 push_sum8(const unsigned char* own, long slot, int world, size_t off) {
+  return sum8_ranks<WN>(world, [&](int p) { return own + off + (size_t)p * slot; });
+}
+
+// sum of `world` bf16 vectors [i, i+8) at byte offset `off` of every rank's buffer
+template <int WN>
+__device__ __forceinline__ u16x8 ar_sum8(const ARPeers& P, int world, size_t off) {
+  return sum8_ranks<WN>(world, [&](int p) { return P.base[p] + off; });
+}
+
 // n % 8 == 0 (host-checked); slice = elements per block (multiple of 8 * world)
-template <bool TWO_SHOT>
+template <bool TWO_SHOT, int WN>
 __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restrict__ in, uint16_t* __restrict__ out,
                                                          long n, long slice, int world, int rank, ARPeers P,
                                                          long max_bytes, uint64_t timeout_ticks, int sim,
@@ -155,12 +216,12 @@ __global__ void __launch_bounds__(AR_THREADS) ar_kernel(const uint16_t* __restri
 
   if (!TWO_SHOT) {
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS)
-      *reinterpret_cast<u16x8*>(out + i) = ar_sum8(P, world, data + 2 * i);
+      *reinterpret_cast<u16x8*>(out + i) = ar_sum8<WN>(P, world, data + 2 * i);
   } else {
     const long part = slice / world;
     const long p0 = i0 + (long)rank * part, p1 = min(i1, p0 + part);
     for (long i = p0 + 8L * t; i < p1; i += 8L * AR_THREADS)
-      *reinterpret_cast<u16x8*>(own + res + 2 * i) = ar_sum8(P, world, data + 2 * i);
+      *reinterpret_cast<u16x8*>(own + res + 2 * i) = ar_sum8<WN>(P, world, data + 2 * i);
     ar_publish(P, AR_FLAGS_B, world, rank, b, e, fence_all);
     ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks, sim);
     for (long i = i0 + 8L * t; i < i1; i += 8L * AR_THREADS) {
@@ -207,13 +268,19 @@ __device__ __forceinline__ float an_block_sum(float v, float* scratch) {
   return r;
 }
 
-template <bool TWO_SHOT>
+//   PUSH     : the row-parallel GEMM already stored its partial in the slots
+//              (push epilogue, common.h K8sPush): no staging, no flag A; wait
+//              for the `S` strip flags (one-shot: every strip of every rank;
+//              two-shot: this rank's column slice), then the same arithmetic
+//              with the local slots as the sum's source (bit-identical).
+template <bool TWO_SHOT, bool PUSH, int WN>
 __global__ void __launch_bounds__(AN_THREADS) ar_addnorm_kernel(const uint16_t* __restrict__ in,
                                                                  uint16_t* __restrict__ res,
                                                                  const uint16_t* __restrict__ w,
                                                                  uint16_t* __restrict__ y, int T, int H, float eps,
                                                                  int world, int rank, ARPeers P, long max_bytes,
-                                                                 uint64_t timeout_ticks, int sim, int fence_all) {
+                                                                 uint64_t timeout_ticks, int sim, int fence_all,
+                                                                 int S = 0, long pslot = 0) {
   __shared__ float scratch[AN_THREADS / 64];
   __shared__ uint32_t s_e;
   const int b = blockIdx.x, t = threadIdx.x, nb = gridDim.x;
@@ -227,36 +294,53 @@ __global__ void __launch_bounds__(AN_THREADS) ar_addnorm_kernel(const uint16_t* 
   const size_t rbuf = AR_DATA + 2 * (size_t)max_bytes + (size_t)(e & 1u) * max_bytes;
   const size_t ssbuf = rbuf + (size_t)T * H * 2;  // [T] fp32 slice sums of squares (two-shot)
   const int nv = H >> 3;
+  // PUSH: this parity's slot 0 (slot p = source rank p's partial)
+  const size_t pbase = push_region(max_bytes) + (size_t)(e & 1u) * world * pslot;
+  const int pw = TWO_SHOT ? H / world : H;  // row length of a push slot
 
-  // 1) stage this rank's rows
-  for (int row = b; row < T; row += nb)
-    for (int i = t; i < nv; i += AN_THREADS)
-      *reinterpret_cast<u16x8*>(own + data + 2 * ((size_t)row * H + 8 * i)) =
-          *reinterpret_cast<const u16x8*>(in + (size_t)row * H + 8 * i);
-  ar_publish(P, AR_FLAGS_A, world, rank, b, e, fence_all);
-  ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
+  if constexpr (PUSH) {
+    if (TWO_SHOT)
+      push_wait(own, world, rank * (S / world), S / world, e, timeout_ticks, sim);
+    else
+      push_wait(own, world, 0, S, e, timeout_ticks, sim);
+  } else {
+    // 1) stage this rank's rows
+    for (int row = b; row < T; row += nb)
+      for (int i = t; i < nv; i += AN_THREADS)
+        *reinterpret_cast<u16x8*>(own + data + 2 * ((size_t)row * H + 8 * i)) =
+            *reinterpret_cast<const u16x8*>(in + (size_t)row * H + 8 * i);
+    ar_publish(P, AR_FLAGS_A, world, rank, b, e, fence_all);
+    ar_wait(own, AR_FLAGS_A, world, b, e, timeout_ticks, sim);
+  }
 
   if (!TWO_SHOT) {
     for (int row = b; row < T; row += nb) {
       u16x8 wv[AN_NC];
       float v[AN_NC][8];
       float ss = 0.f;
+      // every load of the row first (no store in between for them to wait behind)
+      // (unconditional: a chunk past the row re-reads the row's last one, never stored)
+      u16x8 a[AN_NC], r0[AN_NC];
+#pragma unroll
+      for (int c = 0; c < AN_NC; ++c) {
+        const int i = min(t + c * AN_THREADS, nv - 1);
+        wv[c] = *reinterpret_cast<const u16x8*>(w + 8 * i);
+        r0[c] = *reinterpret_cast<const u16x8*>(res + (size_t)row * H + 8 * i);
+        a[c] = PUSH ? push_sum8<WN>(own, pslot, world, pbase + 2 * ((size_t)row * pw + 8 * i))
+                    : ar_sum8<WN>(P, world, data + 2 * ((size_t)row * H + 8 * i));
+      }
 #pragma unroll
       for (int c = 0; c < AN_NC; ++c) {
         const int i = t + c * AN_THREADS;
         if (i < nv) {
-          wv[c] = *reinterpret_cast<const u16x8*>(w + 8 * i);
-          const u16x8 a = ar_sum8(P, world, data + 2 * ((size_t)row * H + 8 * i));
-          uint16_t* rr = res + (size_t)row * H + 8 * i;
-          const u16x8 r0 = *reinterpret_cast<const u16x8*>(rr);
           u16x8 sv;
 #pragma unroll
           for (int j = 0; j < 8; ++j) {
-            sv[j] = f2bf(bf2f(a[j]) + bf2f(r0[j]));
+            sv[j] = f2bf(bf2f(a[c][j]) + bf2f(r0[c][j]));
             v[c][j] = bf2f(sv[j]);
             ss += v[c][j] * v[c][j];
           }
-          *reinterpret_cast<u16x8*>(rr) = sv;
+          *reinterpret_cast<u16x8*>(res + (size_t)row * H + 8 * i) = sv;
         }
       }
       const float inv = rsqrtf(an_block_sum(ss, scratch) / (float)H + eps);
@@ -277,7 +361,8 @@ __global__ void __launch_bounds__(AN_THREADS) ar_addnorm_kernel(const uint16_t* 
     for (int row = b; row < T; row += nb) {
       float ss = 0.f;
       for (int i = c0 + t; i < c0 + sl; i += AN_THREADS) {
-        const u16x8 a = ar_sum8(P, world, data + 2 * ((size_t)row * H + 8 * i));
+        const u16x8 a = PUSH ? push_sum8<WN>(own, pslot, world, pbase + 2 * ((size_t)row * pw + 8 * (i - c0)))
+                             : ar_sum8<WN>(P, world, data + 2 * ((size_t)row * H + 8 * i));
         const u16x8 r0 = *reinterpret_cast<const u16x8*>(res + (size_t)row * H + 8 * i);
         u16x8 sv;
 #pragma unroll
@@ -294,18 +379,34 @@ __global__ void __launch_bounds__(AN_THREADS) ar_addnorm_kernel(const uint16_t* 
     ar_publish(P, AR_FLAGS_B, world, rank, b, e, fence_all);
     ar_wait(own, AR_FLAGS_B, world, b, e, timeout_ticks, sim);
     for (int row = b; row < T; row += nb) {
-      float tot = 0.f;
-      for (int p = 0; p < world; ++p) tot += *reinterpret_cast<const float*>(P.base[p] + ssbuf + 4 * (size_t)row);
-      const float inv = rsqrtf(tot / (float)H + eps);
-      for (int i = t; i < nv; i += AN_THREADS) {
-        const int owner = i / sl;
-        const u16x8 sv = *reinterpret_cast<const u16x8*>(P.base[owner] + rbuf + 2 * ((size_t)row * H + 8 * i));
-        const u16x8 wv = *reinterpret_cast<const u16x8*>(w + 8 * i);
-        *reinterpret_cast<u16x8*>(res + (size_t)row * H + 8 * i) = sv;
-        u16x8 o;
+      float tot = 0.f;  // the slices' sums of squares in rank order (loads first when WN > 0)
+      if constexpr (WN > 0) {
+        float sq[WN];
 #pragma unroll
-        for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(sv[j]) * inv * bf2f(wv[j]));
-        *reinterpret_cast<u16x8*>(y + (size_t)row * H + 8 * i) = o;
+        for (int p = 0; p < WN; ++p) sq[p] = *reinterpret_cast<const float*>(P.base[p] + ssbuf + 4 * (size_t)row);
+#pragma unroll
+        for (int p = 0; p < WN; ++p) tot += sq[p];
+      } else {
+        for (int p = 0; p < world; ++p) tot += *reinterpret_cast<const float*>(P.base[p] + ssbuf + 4 * (size_t)row);
+      }
+      const float inv = rsqrtf(tot / (float)H + eps);
+      u16x8 sv[AN_NC], wv[AN_NC];  // the row's peer reads all in flight at once (unconditional, clamped)
+#pragma unroll
+      for (int c = 0; c < AN_NC; ++c) {
+        const int i = min(t + c * AN_THREADS, nv - 1);
+        sv[c] = *reinterpret_cast<const u16x8*>(P.base[i / sl] + rbuf + 2 * ((size_t)row * H + 8 * i));
+        wv[c] = *reinterpret_cast<const u16x8*>(w + 8 * i);
+      }
+#pragma unroll
+      for (int c = 0; c < AN_NC; ++c) {
+        const int i = t + c * AN_THREADS;
+        if (i < nv) {
+          *reinterpret_cast<u16x8*>(res + (size_t)row * H + 8 * i) = sv[c];
+          u16x8 o;
+#pragma unroll
+          for (int j = 0; j < 8; ++j) o[j] = f2bf(bf2f(sv[c][j]) * inv * bf2f(wv[c][j]));
+          *reinterpret_cast<u16x8*>(y + (size_t)row * H + 8 * i) = o;
+        }
       }
     }
   }
@@ -368,6 +469,32 @@ __global__ void __launch_bounds__(AR_THREADS) a2a_kernel(const uint16_t* __restr
   }
 }
 
+// ar_addnorm_kernel for (two-shot?, push?) x the communicator's world (2 / 4 / 8:
+// unconditional peer loads; else the runtime-world loop)
+template <bool TS, bool PU>
+static void launch_addnorm_w(const ARCtx& c, int nb, const uint16_t* in, uint16_t* res, const uint16_t* w, uint16_t* y,
+                             int T, int H, float eps, int S, long pslot, hipStream_t s) {
+#define K8S_AN(WN)                                                                                              \
+  hipLaunchKernelGGL((ar_addnorm_kernel<TS, PU, WN>), dim3(nb), dim3(AN_THREADS), 0, s, in, res, w, y, T, H, eps, \
+                     c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all(), S, pslot)
+  switch (c.world) {
+    case 2: K8S_AN(2); break;
+    case 4: K8S_AN(4); break;
+    case 8: K8S_AN(8); break;
+    default: K8S_AN(0); break;
+  }
+#undef K8S_AN
+}
+
+static int launch_addnorm(const ARCtx& c, bool two_shot, bool push, int nb, const uint16_t* in, uint16_t* res,
+                          const uint16_t* w, uint16_t* y, int T, int H, float eps, int S, long pslot, hipStream_t s) {
+  if (two_shot && push) launch_addnorm_w<true, true>(c, nb, in, res, w, y, T, H, eps, S, pslot, s);
+  else if (two_shot) launch_addnorm_w<true, false>(c, nb, in, res, w, y, T, H, eps, S, pslot, s);
+  else if (push) launch_addnorm_w<false, true>(c, nb, in, res, w, y, T, H, eps, S, pslot, s);
+  else launch_addnorm_w<false, false>(c, nb, in, res, w, y, T, H, eps, S, pslot, s);
+  return (int)hipGetLastError();
+}
+
 }  // namespace k8s
 
 using namespace k8s;
@@ -389,7 +516,8 @@ K8S_API int k8s_ar_alltoall_bf16(int id, const void* send, void* recv, long chun
   return (int)hipGetLastError();
 }
 
-K8S_API long k8s_ar_buffer_bytes(long max_bytes) { return (long)AR_DATA + 8 * max_bytes; }
+// header + DATA / RES (2 x 2 x max) + A2A (2 x 2 x max) + push slots (2 x max)
+K8S_API long k8s_ar_buffer_bytes(long max_bytes) { return (long)AR_DATA + 10 * max_bytes; }
 
 K8S_API int k8s_ar_alloc(long bytes, void** out) {
   hipError_t e = hipExtMallocWithFlags(out, (size_t)bytes, hipDeviceMallocUncached);
@@ -444,7 +572,7 @@ K8S_API int k8s_ar_register(int world, int rank, void** bases, long max_bytes, d
 // (bench --tp-sim), never a collective.
 K8S_API int k8s_ar_register_loopback(int world, long max_bytes) {
   if (world < 1 || world > AR_MAX_WORLD || max_bytes % 16) return -1;
-  const size_t per = (size_t)AR_DATA + 8 * (size_t)max_bytes;
+  const size_t per = (size_t)k8s_ar_buffer_bytes(max_bytes);
   void* base = nullptr;  // uncached, like the IPC buffers of a real communicator (k8s_ar_alloc)
   if (hipExtMallocWithFlags(&base, per * world, hipDeviceMallocUncached) != hipSuccess) return -1;
   if (hipMemset(base, 0, per * world) != hipSuccess) return -1;
@@ -492,12 +620,24 @@ K8S_API int k8s_ar_allreduce_bf16(int id, const void* in, void* out, long n, int
   long slice = (n + nb - 1) / nb;
   slice = (slice + unit - 1) / unit * unit;
   nb = (n + slice - 1) / slice;
-  if (mode == 2)
-    hipLaunchKernelGGL(ar_kernel<true>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
-  else
-    hipLaunchKernelGGL(ar_kernel<false>, dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim, fence_all());
+#define K8S_AR(TS, WN)                                                                                        \
+  hipLaunchKernelGGL((ar_kernel<TS, WN>), dim3((unsigned)nb), dim3(AR_THREADS), 0, s, (const uint16_t*)in,         \
+                     (uint16_t*)out, n, slice, c.world, c.rank, c.peers, c.max_bytes, c.timeout_ticks, c.sim,       \
+                     fence_all())
+#define K8S_AR_W(TS)             \
+  switch (c.world) {             \
+    case 2: K8S_AR(TS, 2); break; \
+    case 4: K8S_AR(TS, 4); break; \
+    case 8: K8S_AR(TS, 8); break; \
+    default: K8S_AR(TS, 0); break; \
+  }
+  if (mode == 2) {
+    K8S_AR_W(true)
+  } else {
+    K8S_AR_W(false)
+  }
+#undef K8S_AR_W
+#undef K8S_AR
   return (int)hipGetLastError();
 }
 
@@ -513,15 +653,70 @@ K8S_API int k8s_ar_addnorm_bf16(int id, const void* in, void* res, const void* w
   if (H % 8 || H / 8 > AN_THREADS * AN_NC || need > c.max_bytes || (mode == 2 && (H / 8) % c.world))
     return (int)hipErrorInvalidValue;
   const int nb = T < c.max_blocks ? T : c.max_blocks;
-  if (mode == 2)
-    hipLaunchKernelGGL(ar_addnorm_kernel<true>, dim3(nb), dim3(AN_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps, c.world, c.rank, c.peers,
-                       c.max_bytes, c.timeout_ticks, c.sim, fence_all());
-  else
-    hipLaunchKernelGGL(ar_addnorm_kernel<false>, dim3(nb), dim3(AN_THREADS), 0, s, (const uint16_t*)in,
-                       (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps, c.world, c.rank, c.peers,
-                       c.max_bytes, c.timeout_ticks, c.sim, fence_all());
-  return (int)hipGetLastError();
+  return launch_addnorm(c, mode == 2, false, nb, (const uint16_t*)in, (uint16_t*)res, (const uint16_t*)w,
+                        (uint16_t*)y, T, H, eps, 0, 0, s);
+}
+
+// ---------------------------------------------------------------- push epilogue
+// The TP row-parallel outputs at decode sizes (o / down projections on the
+// LDS-DMA stream GEMM, gemm_stream.hip k8s_gemm_stream_push) skip the staging
+// copy: the GEMM's epilogue stores each output strip straight into the slots
+// the fused all-reduce + add + RMSNorm reads, over xGMI, and raises one flag
+// per strip; the consumer (ar_addnorm_kernel<., PUSH>) waits on those flags
+// and sums its LOCAL slots.  Two-shot: each strip goes only to the rank that
+// owns its columns ((H / world) % strip width == 0), i.e. the push IS the
+// reduce-scatter's first leg; one-shot: the whole tile goes to every rank.
+// Same epoch sequence as every other collective of the communicator (the GEMM
+// reads the epoch, the consumer advances it): a push pair counts as one call.
+// Slot parity safety is the all-reduce's argument: a rank pushes call E's
+// tile only after its call E-1 waited for every peer's flags of E-1, i.e.
+// after every peer finished call E-2, the last reader of parity E & 1.
+static int push_check(const ARCtx& c, int N, int T, int mode) {
+  const long slot = push_slot(c.max_bytes, c.world);
+  if (N % 64 || N / 64 > kPushMaxStrips || T <= 0) return 0;
+  if (mode == 1) return (long)T * N * 2 <= slot;
+  if (mode != 2 || N % c.world) return 0;
+  const int w = N / c.world;
+  return w % 128 == 0 && (long)T * w * 2 <= slot;  // every 64- / 128-column strip inside one owner's slice
+}
+
+// 1 if a [T][N] row-parallel output of this communicator can take the push
+// epilogue in `mode` (1 one-shot, 2 two-shot), else 0.
+K8S_API int k8s_ar_push_ok(int id, int N, int T, int mode) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return 0;
+  return push_check(g_ctx[id], N, T, mode);
+}
+
+// The producer's descriptor (common.h K8sPush) for a [T][N] output in `mode`.
+K8S_API int k8s_ar_push_desc(int id, int N, int T, int mode, K8sPush* out) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used || !push_check(g_ctx[id], N, T, mode)) return (int)hipErrorInvalidValue;
+  const ARCtx& c = g_ctx[id];
+  for (int p = 0; p < AR_MAX_WORLD; ++p) out->base[p] = c.peers.base[p];
+  out->world = c.world;
+  out->rank = c.rank;
+  out->two_shot = mode == 2;
+  out->H = N;
+  out->slot = push_slot(c.max_bytes, c.world);
+  out->region = (long)push_region(c.max_bytes);
+  out->flags = (long)AR_FLAGS_P;
+  out->epoch = (long)AR_EPOCH;
+  return 0;
+}
+
+// The consumer: residual += sum of the pushed partials, y = rmsnorm(residual) * w
+// (res / y [T][H]); S = the producer's strip count (common.h k8s_push_strips).
+K8S_API int k8s_ar_push_addnorm_bf16(int id, void* res, const void* w, void* y, int T, int H, float eps, int mode,
+                                     int S, hipStream_t s) {
+  if (id < 0 || id >= 16 || !g_ctx[id].used) return (int)hipErrorInvalidValue;
+  const ARCtx& c = g_ctx[id];
+  if (T <= 0) return 0;
+  const long need = (long)T * H * 2 + 4L * T;  // two-shot: the reduced slices + sums of squares in RES
+  if (!push_check(c, H, T, mode) || H / 8 > AN_THREADS * AN_NC || need > c.max_bytes || S < 1 || S > H / 64 ||
+      H % S || (mode == 2 && S % c.world))
+    return (int)hipErrorInvalidValue;
+  const int nb = T < c.max_blocks ? T : c.max_blocks;
+  return launch_addnorm(c, mode == 2, true, nb, nullptr, (uint16_t*)res, (const uint16_t*)w, (uint16_t*)y, T, H, eps,
+                        S, push_slot(c.max_bytes, c.world), s);
 }
 
 // STATUS -> *host (pinned), stream-ordered after everything issued before it:

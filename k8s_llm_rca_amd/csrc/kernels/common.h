@@ -109,5 +109,69 @@ __device__ __forceinline__ void lgkm_wait(bf16x8& a, bf16x8& b) {
   asm volatile("s_waitcnt lgkmcnt(%2)" : "+v"(a), "+v"(b) : "n"(N) : "memory");
 }
 
+// TP push epilogue (allreduce.hip "push" section): where a row-parallel GEMM
+// (o / down projection at decode sizes) stores its bf16 output tile straight
+// into the peers' IPC staging slots instead of its own output buffer, then
+// raises one flag per output strip.  Filled on the host by k8s_ar_push_desc;
+// the parity half of the slots follows the communicator's device-side epoch,
+// read by the kernel itself (HIP-graph capturable).
+struct K8sPush {
+  unsigned char* base[8];  // every rank's mapped communicator buffer
+  int world, rank;
+  int two_shot;            // 0: the whole tile to every rank; 1: each strip to the owner of its columns
+  int H;                   // row length of the output (= N of the GEMM)
+  long slot;               // bytes per (source rank) slot
+  long region;             // byte offset of the parity-0 slots; parity 1 follows at + world * slot
+  long flags;              // byte offset of the per-(source rank, strip) flags
+  long epoch;              // byte offset of the epoch word
+};
+constexpr int kPushMaxStrips = 256;
+
+// Output strips of a push GEMM (the flag count the consumer waits for): the
+// LDS-DMA kernel's strip width (128 columns for cfg 23 / 24, else 64); the
+// split-K reduce pass always works on 64-column strips.
+__host__ __device__ inline int k8s_push_strips(int cfg, int splits, int N) {
+  return N / ((splits == 1 && cfg > 20) ? 128 : 64);
+}
+
+__device__ __forceinline__ uint32_t push_epoch(const K8sPush& P) {
+  return __hip_atomic_load(reinterpret_cast<uint32_t*>(P.base[P.rank] + P.epoch), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT) + 1u;
+}
+
+// Store 8 outputs (row m, columns n .. n + 7) of this rank's partial where the
+// consumer reads them: one-shot -> slot [rank] of every rank ([T][H] rows);
+// two-shot -> slot [rank] of the owner of column n only ([T][H / world] rows
+// of the owner's column slice).
+__device__ __forceinline__ void push_store8(const K8sPush& P, uint32_t e, int m, int n, const u16x8& v) {
+  const size_t par = P.region + (size_t)(e & 1u) * P.world * P.slot + (size_t)P.rank * P.slot;
+  if (P.two_shot) {
+    const int w = P.H / P.world, o = n / w;
+    *reinterpret_cast<u16x8*>(P.base[o] + par + 2 * ((size_t)m * w + (n - o * w))) = v;
+  } else {
+    for (int p = 0; p < P.world; ++p)
+      *reinterpret_cast<u16x8*>(P.base[p] + par + 2 * ((size_t)m * P.H + n)) = v;
+  }
+}
+
+// After every thread's push_store8 of strip `s` (columns n0 ..): drain the
+// stores, ONE system-scope release, then the strip's flag in every rank
+// (one-shot) or in the owner (two-shot) -- the all-reduce's ar_publish
+// (explicit vmcnt(0) behind the fence, lane-addressed vector stores).
+__device__ __forceinline__ void push_publish(const K8sPush& P, uint32_t e, int s, int n0) {
+  const int t = threadIdx.x;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (t < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // lane t signals rank t (lane-addressed: a vector store, as in ar_publish)
+    if (P.two_shot ? t == n0 / (P.H / P.world) : t < P.world) {
+      uint32_t* f = reinterpret_cast<uint32_t*>(P.base[t] + P.flags) + P.rank * kPushMaxStrips + s;
+      __hip_atomic_store(f, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+  }
+}
+
 
 }  // namespace k8s

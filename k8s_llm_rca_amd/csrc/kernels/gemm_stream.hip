@@ -392,11 +392,38 @@ __device__ __forceinline__ void glds_store(const f32x4 (&acc)[MTW][NF], int M, u
     }
 }
 
-template <int MTW, int NB, int NF, bool HAND>
+// Push epilogue (TP row-parallel output, common.h K8sPush): the tile goes
+// through LDS (bf16, 16-B padded rows) so each thread pushes whole 16-byte row
+// pieces -- full 128- / 256-byte row segments per strip over xGMI, not the
+// accumulator layout's 32-byte pieces -- then the strip's flag is raised.
+template <int MTW, int NF>
+__device__ __forceinline__ void glds_push_store(const f32x4 (&acc)[MTW][NF], int M, uint16_t* sm, const K8sPush& P,
+                                                int n0, int strip) {
+  constexpr int BN = 16 * NF, PITCH = BN + 8, CPR = BN / 8;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  const int m_base = wv * 16 * MTW;
+  __syncthreads();  // every wave is done reading the ring's last stage
+#pragma unroll
+  for (int mt = 0; mt < MTW; ++mt)
+#pragma unroll
+    for (int v = 0; v < 4; ++v)
+#pragma unroll
+      for (int cf = 0; cf < NF; ++cf) sm[(m_base + 16 * mt + 4 * g + v) * PITCH + 16 * cf + r] = f2bf(acc[mt][cf][v]);
+  __syncthreads();
+  const uint32_t e = push_epoch(P);
+  for (int i = threadIdx.x; i < M * CPR; i += 256) {
+    const int m = i / CPR, c = i % CPR;
+    push_store8(P, e, m, n0 + 8 * c, *reinterpret_cast<const u16x8*>(sm + m * PITCH + 8 * c));
+  }
+  push_publish(P, e, strip, n0);
+}
+
+template <int MTW, int NB, int NF, bool HAND, bool PUSH = false>
 __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restrict__ x, int ldx,
                                                         const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                         int ldy, float* __restrict__ part, int M, int N, int K,
-                                                        int kslice, int silu_i) {
+                                                        int kslice, int silu_i, K8sPush push) {
   __shared__ __attribute__((aligned(16))) uint16_t sm[glds_lds_elems<MTW, NB, NF>()];
   // strip: 16 NF W rows (plain: output columns n0 ..; SwiGLU: 8 NF act columns n0 ..)
   const int n0 = blockIdx.x * (silu_i ? 8 : 16) * NF, split = blockIdx.y, kbeg = split * kslice;
@@ -406,7 +433,10 @@ __global__ void __launch_bounds__(256) gemm_glds_kernel(const uint16_t* __restri
 #pragma unroll
     for (int cf = 0; cf < NF; ++cf) acc[mt][cf] = f32x4{0.f, 0.f, 0.f, 0.f};
   glds_strip<MTW, NB, NF, HAND>(x + kbeg, ldx, M, w + (size_t)n0 * K + kbeg, K, kslice / kSC, sm, acc, silu_i);
-  if (silu_i)
+  static_assert(64 * MTW * (16 * NF + 8) <= glds_lds_elems<MTW, NB, NF>(), "push tile must fit the ring's LDS");
+  if constexpr (PUSH)
+    glds_push_store<MTW, NF>(acc, M, sm, push, n0, blockIdx.x);
+  else if (silu_i)
     glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0, true);
   else if (gridDim.y == 1)
     glds_store<MTW, NF>(acc, M, y + n0, ldy, nullptr, 0);
@@ -472,6 +502,34 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_kernel(const float* __
   *reinterpret_cast<u16x8*>(y + (size_t)m * ldy + n) = o;
 }
 
+// The split-K form of the push epilogue: gemm_stream_reduce_kernel's sums (same
+// order: bit-identical) for one 64-column strip of all M rows per workgroup,
+// pushed into the peers' slots, then the strip's flag.
+__global__ void __launch_bounds__(256) gemm_stream_reduce_push_kernel(const float* __restrict__ part, int splits,
+                                                                      int M, int N, K8sPush P) {
+  const int strip = blockIdx.x, n0 = 64 * strip;
+  const size_t MN = (size_t)M * N;
+  const uint32_t e = push_epoch(P);
+  for (int i = threadIdx.x; i < M * 8; i += 256) {
+    const int m = i >> 3, n = n0 + 8 * (i & 7);
+    const size_t idx = (size_t)m * N + n;
+    f32x4 a0 = *reinterpret_cast<const f32x4*>(part + idx);
+    f32x4 a1 = *reinterpret_cast<const f32x4*>(part + idx + 4);
+    for (int s = 1; s < splits; ++s) {
+      a0 += *reinterpret_cast<const f32x4*>(part + s * MN + idx);
+      a1 += *reinterpret_cast<const f32x4*>(part + s * MN + idx + 4);
+    }
+    u16x8 o;
+#pragma unroll
+    for (int v = 0; v < 4; ++v) {
+      o[v] = f2bf(a0[v]);
+      o[v + 4] = f2bf(a1[v]);
+    }
+    push_store8(P, e, m, n, o);
+  }
+  push_publish(P, e, strip, n0);
+}
+
 // the hand-issued LDS reads of glds_strip (default; K8SRCA_GLDS_HAND=0: hipcc's
 // own reads, A/B, read per launch).  Bit-identical; 0-5 % faster per projection
 // at M = 64-192 (tools/glds_hand_ab.py, profiles/r4/glds_hand/): the decode GEMMs
@@ -481,15 +539,21 @@ static bool glds_hand() {
   return !(e && e[0] == '0');
 }
 
+// push != nullptr: the push-epilogue form (splits == 1, plain output; hand reads)
 template <int MTW, int NB, int NF = 4>
 static hipError_t launch_glds(dim3 grid, hipStream_t s, const uint16_t* x, int ldx, const uint16_t* w, uint16_t* y,
-                              int ldy, float* part, int M, int N, int K, int kslice, int silu_i) {
-  if (glds_hand())
+                              int ldy, float* part, int M, int N, int K, int kslice, int silu_i,
+                              const K8sPush* push = nullptr) {
+  const K8sPush none{};
+  if (push)
+    hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF, true, true>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M,
+                       N, K, kslice, 0, *push);
+  else if (glds_hand())
     hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF, true>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N,
-                       K, kslice, silu_i);
+                       K, kslice, silu_i, none);
   else
     hipLaunchKernelGGL((gemm_glds_kernel<MTW, NB, NF, false>), grid, dim3(256), 0, s, x, ldx, w, y, ldy, part, M, N,
-                       K, kslice, silu_i);
+                       K, kslice, silu_i, none);
   return hipGetLastError();
 }
 
@@ -512,7 +576,11 @@ using namespace k8s;
 // silu: w is the gate_up weight [2N][K] (gate rows first) and y[M][N] = silu(x Wg^T) * (x Wu^T)
 // (splits == 1 only: the nonlinearity needs the whole K sum).
 static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
-                         int splits, void* part, bool reduce, hipStream_t s, bool silu = false) {
+                         int splits, void* part, bool reduce, hipStream_t s, bool silu = false,
+                         const K8sPush* push = nullptr) {
+  // push (splits == 1): the LDS-DMA kernel's own epilogue pushes; splits > 1: the reduce pass does
+  const K8sPush* gpush = (push && splits == 1) ? push : nullptr;
+  if (push && (silu || !reduce || (splits == 1 && cfg < 13))) return (int)hipErrorInvalidValue;
   const int bn = (cfg > 20 ? 128 : kSBN) / (silu ? 2 : 1);  // output columns per strip
   if (M <= 0 || M > 256 || N % bn || splits < 1 || K % (splits * kSC) || (splits > 1 && part == nullptr) ||
       (cfg != 4 && cfg != 8 && (cfg < 13 || cfg > 16) && cfg != 23 && cfg != 24) || ldx % 8 ||
@@ -534,8 +602,8 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
   float* pp = (float*)part;
   hipError_t e;
 #define K8S_SL(MT, UU) e = launch_stream<MT, UU>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
-#define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
-#define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i)
+#define K8S_GL(MT, NB) e = launch_glds<MT, NB>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i, gpush)
+#define K8S_GW(MT, NB) e = launch_glds<MT, NB, 8>(grid, s, xx, ldx, ww, yy, ldy, pp, M, N, K, kslice, silu_i, gpush)
   if (cfg == 23) {
     switch (mtw) {
       case 1: K8S_GW(1, 3); break;
@@ -584,7 +652,10 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
 #undef K8S_GL
 #undef K8S_GW
   if (e != hipSuccess) return (int)e;
-  if (splits > 1 && reduce) {
+  if (splits > 1 && push) {
+    hipLaunchKernelGGL(gemm_stream_reduce_push_kernel, dim3(N / 64), dim3(256), 0, s, (const float*)part, splits, M, N,
+                       *push);
+  } else if (splits > 1 && reduce) {
     const int blocks = (M * N / 8 + 255) / 256;
     hipLaunchKernelGGL(gemm_stream_reduce_kernel, dim3(blocks), dim3(256), 0, s, (const float*)part, splits, yy, ldy,
                        M, N);
@@ -595,6 +666,23 @@ static int stream_launch(const void* x, int ldx, const void* w, void* y, int ldy
 K8S_API int k8s_gemm_stream(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                             int splits, void* part, hipStream_t s) {
   return stream_launch(x, ldx, w, y, ldy, M, N, K, cfg, splits, part, true, s);
+}
+
+extern "C" int k8s_ar_push_desc(int id, int N, int T, int mode, K8sPush* out);
+
+// A TP row-parallel projection with the push epilogue: x . w^T is stored into
+// the xGMI communicator `ar_id`'s slots (mode 1 one-shot / 2 two-shot layout)
+// instead of a y buffer, with one flag per output strip (k8s_push_strips(cfg,
+// splits, N) of them); k8s_ar_push_addnorm_bf16 consumes it.  cfg: the LDS-DMA
+// configurations (13-16, 23, 24), or any stream cfg with splits > 1 (the
+// split-K reduce pass pushes).
+K8S_API int k8s_gemm_stream_push(const void* x, int ldx, const void* w, int M, int N, int K, int cfg, int splits,
+                                 void* part, int ar_id, int mode, hipStream_t s) {
+  K8sPush P;
+  const int rc = k8s_ar_push_desc(ar_id, N, M, mode, &P);
+  if (rc) return rc;
+  if (k8s_push_strips(cfg, splits, N) > kPushMaxStrips) return (int)hipErrorInvalidValue;
+  return stream_launch(x, ldx, w, nullptr, N, M, N, K, cfg, splits, part, true, s, false, &P);
 }
 
 // y[M][N] = silu(x . w[0:N]^T) * (x . w[N:2N]^T): the gate_up projection with its

@@ -77,6 +77,10 @@ int k8s_gemm_big_rope(const void* x, int ldx, const void* w, void* qkv, int ldq,
                       hipStream_t s);
 int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,
                          hipStream_t s);
+int k8s_gemm_stream_push(const void* x, int ldx, const void* w, int M, int N, int K, int cfg, int splits, void* part,
+                         int ar_id, int mode, hipStream_t s);
+int k8s_ar_push_addnorm_bf16(int id, void* res, const void* w, void* y, int T, int H, float eps, int mode, int S,
+                             hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
@@ -144,6 +148,11 @@ struct K8sLlamaStep {
   // ar_fuse: the all-reduce + residual add + RMSNorm of each row-parallel output in
   // one launch (k8s_ar_addnorm_bf16) instead of all-reduce, then rmsnorm
   int ar_id, ar_mode, ar_fuse;
+  // ar_push (with ar_fuse): o / down projections whose choice is the stream GEMM
+  // (LDS-DMA cfg, or split-K) store their output straight into the peers'
+  // all-reduce slots (k8s_gemm_stream_push) and the fused epilogue waits on
+  // per-strip flags (k8s_ar_push_addnorm_bf16): no staging copy
+  int ar_push;
 };
 
 namespace {
@@ -185,6 +194,10 @@ int gemm(const K8sLlamaStep& s, const K8sGemmSel& g, const void* x, int ldx, con
   }
 }
 
+// the push epilogue exists on the stream GEMM's LDS-DMA configurations and on
+// its split-K reduce pass
+bool push_kind(const K8sGemmSel& g) { return g.kind == 4 && (g.cfg >= 13 || g.splits > 1); }
+
 }  // namespace
 
 #define K8S_TRY(call)          \
@@ -209,6 +222,8 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   bool pend = false;  // the previous layer's down projection is still split-K partials
   const bool tp = s.ar_id >= 0;  // row-parallel outputs are partial sums: all-reduce, never defer split-K
   const bool fuse_an = tp && s.ar_fuse;  // the previous layer's down all-reduce already produced y
+  const bool push_o = fuse_an && s.ar_push && push_kind(s.sel[1]);
+  const bool push_d = fuse_an && s.ar_push && push_kind(s.sel[3]);
   const long n_out = (long)T * H;
   for (int l = 0; l < s.L; ++l) {
     if (l == 0)
@@ -246,8 +261,17 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(k8s_attn_decode(qkv, ld_qkv, s.kc[l], s.vc[l], s.d_bt, s.d_bt_stride, s.d_ctx, s.d_qs, s.d_S, s.nq,
                               s.nkv, s.BS, s.scale, attn, qd, s.d_part_o, s.d_part_ml, s.d_n_parts, s.d_part_size,
                               s.d_items, s.d_n_items, s.d_n_items_dev, s.d_grid, st));
-    K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
-    if (fuse_an)
+    if (push_o) {
+      K8S_TRY(k8s_gemm_stream_push(attn, qd, s.wo[l], T, H, qd, s.sel[1].cfg, s.sel[1].splits, s.mid_part, s.ar_id,
+                                   s.ar_mode, st));
+      K8S_TRY(k8s_ar_push_addnorm_bf16(s.ar_id, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode,
+                                       k8s::k8s_push_strips(s.sel[1].cfg, s.sel[1].splits, H), st));
+    } else {
+      K8S_TRY(gemm(s, s.sel[1], attn, qd, s.wo[l], s.obuf, H, T, H, qd, st, !tp));
+    }
+    if (push_o) {
+      // all-reduce + residual add + post-attention norm done above
+    } else if (fuse_an)
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.obuf, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode, st));
     else if (tp)
       K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
@@ -268,6 +292,13 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     }
     // the last layer's down output is returned (`prev`) for the final norm
     pend = !tp && deferred(s.sel[3], l + 1 < s.L);
+    if (push_d && l + 1 < s.L) {  // the next layer's input norm rides on this all-reduce
+      K8S_TRY(k8s_gemm_stream_push(s.act, s.I, s.wdown[l], T, H, s.I, s.sel[3].cfg, s.sel[3].splits, s.mid_part,
+                                   s.ar_id, s.ar_mode, st));
+      K8S_TRY(k8s_ar_push_addnorm_bf16(s.ar_id, s.residual, s.in_norm[l + 1], s.y, T, H, s.eps, s.ar_mode,
+                                       k8s::k8s_push_strips(s.sel[3].cfg, s.sel[3].splits, H), st));
+      continue;
+    }
     K8S_TRY(gemm(s, s.sel[3], s.act, s.I, s.wdown[l], s.prev, H, T, H, s.I, st, !tp && l + 1 < s.L));
     if (fuse_an && l + 1 < s.L)  // the next layer's input norm rides on this all-reduce
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.prev, s.residual, s.in_norm[l + 1], s.y, T, H, s.eps, s.ar_mode, st));

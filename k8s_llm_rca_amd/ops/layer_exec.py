@@ -42,13 +42,23 @@ class LlamaStep(ctypes.Structure):
         ("p_bt_stride", I), ("p_S", I), ("n_tiles", I), ("n_merge", I),
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
-        ("ar_id", I), ("ar_mode", I), ("ar_fuse", I),
+        ("ar_id", I), ("ar_mode", I), ("ar_fuse", I), ("ar_push", I),
     ]
 
 
 _enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
 # TP: all-reduce + residual add + RMSNorm of every row-parallel output in one launch
 _fuse_ar_norm = os.environ.get("K8SRCA_TP_FUSED_NORM", "1") == "1"
+# TP: o / down projections on the stream GEMM store straight into the all-reduce's
+# slots (push epilogue, csrc/kernels/allreduce.hip "push epilogue").  Off by
+# default: on the tp-sim loopback the push GEMM's in-kernel publish (store acks +
+# release + flag per strip, +2.5-5.4 us) costs what the consumer saves (staging,
+# -2-2.5 us): 0.3-1.8 us slower per pair at 70B TP=8 decode shapes
+# (tools/push_ab.py, profiles/r4/push/).  1 = push wherever the shape allows.
+_tp_push = os.environ.get("K8SRCA_TP_PUSH", "0") == "1"
+# test hook: route o / down through the stream GEMM (LDS-DMA cfg 13; down split-K 2)
+# wherever its shape allows, so small test models exercise both push forms
+_tp_push_force = os.environ.get("K8SRCA_TP_PUSH_FORCE", "0") == "1"
 # split-K o / down projections reduced inside the following residual add + RMSNorm
 _fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
 # (Round 3 also carried a row-chunked o / down GEMM with each chunk's
@@ -110,6 +120,7 @@ class LlamaExecutor:
         st.ar_id = car.id if car is not None else -1
         st.ar_mode = 1
         st.ar_fuse = 0
+        st.ar_push = 0
 
     @staticmethod
     def eligible(model) -> bool:
@@ -157,6 +168,7 @@ class LlamaExecutor:
             st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
             # the two-shot epilogue splits each row's 16-B chunks evenly over the ranks
             st.ar_fuse = int(_fuse_ar_norm and (st.ar_mode == 1 or (H // 8) % self._car.world == 0))
+            st.ar_push = int(bool(st.ar_fuse) and _tp_push and self._car.push_ok(H, T, st.ar_mode))
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)
@@ -191,6 +203,10 @@ class LlamaExecutor:
             fused = LIN.swiglu_choice(T, N, K) if i == 2 else None  # the SwiGLU-epilogue gate_up (writes act)
             # otherwise the choice LIN.linear makes (models/llama.py's path)
             kind, cfg, splits = fused or LIN.select_gemm(T, N, K)
+            if _tp_push_force and self._car is not None and i in (1, 3):
+                fs = 1 if i == 1 else 2
+                if LIN.stream_shape_ok(T, N, K, 13, fs):
+                    kind, cfg, splits = LIN.KIND_STREAM, 13, fs
             st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
             st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
             if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):

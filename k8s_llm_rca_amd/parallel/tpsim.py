@@ -33,7 +33,7 @@ import torch
 
 from ..ops._lib import lib, stream_ptr
 from .groups import ParallelContext
-from .xgmi import ONE_SHOT_MAX, _bind, _check
+from .xgmi import ONE_SHOT_MAX, _bind, _check, linear_push_addnorm, push_ok
 
 XGMI_LINK_GBPS = 153.0   # one xGMI link, per direction (7 links per GPU)
 XGMI_HOP_US = 2.5        # one flag hand-off across the fabric (signal -> visible on the peer)
@@ -108,6 +108,21 @@ class LoopbackAR:
 
     def a2a_fits(self, nbytes: int) -> bool:
         return nbytes <= 2 * self.max_bytes and (nbytes // 2) % (8 * self.world) == 0
+
+    def push_ok(self, H: int, T: int, mode: int) -> bool:
+        return push_ok(self, H, T, mode)
+
+    def addnorm(self, x, residual, w, y, eps, mode=None):
+        T, H = x.shape
+        m = mode or (1 if T * H * 2 <= ONE_SHOT_MAX else 2)
+        _check(self.L.k8s_ar_addnorm_bf16(self.id, x.data_ptr(), residual.data_ptr(), w.data_ptr(), y.data_ptr(), T,
+                                          H, float(eps), m, stream_ptr(x)), "k8s_ar_addnorm_bf16 (loopback)")
+        return y
+
+    def linear_push_addnorm(self, x, w, residual, nw, y, eps, cfg, splits=1, mode=None):
+        """The push epilogue's stand-in: the GEMM stores into the loopback slots
+        (the bytes of the real push), the consumer's waits are skipped."""
+        return linear_push_addnorm(self, x, w, residual, nw, y, eps, cfg, splits, mode)
 
     def status_async(self, host: torch.Tensor) -> None:
         _check(self.L.k8s_ar_status_async(self.id, host.data_ptr(), stream_ptr()), "k8s_ar_status_async")

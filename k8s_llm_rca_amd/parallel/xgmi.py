@@ -52,6 +52,9 @@ def _bind(L) -> None:
         "k8s_ar_status": ([c_int, ctypes.POINTER(c_int)], c_int),
         "k8s_ar_status_async": ([c_int, P, P], c_int),
         "k8s_ar_addnorm_bf16": ([c_int, P, P, P, P, c_int, c_int, ctypes.c_float, c_int, P], c_int),
+        "k8s_ar_push_ok": ([c_int, c_int, c_int, c_int], c_int),
+        "k8s_ar_push_addnorm_bf16": ([c_int, P, P, P, c_int, c_int, ctypes.c_float, c_int, c_int, P], c_int),
+        "k8s_gemm_stream_push": ([P, c_int, P, c_int, c_int, c_int, c_int, c_int, P, c_int, c_int, P], c_int),
     }
     for name, (args, res) in sigs.items():
         fn = getattr(L, name)
@@ -137,6 +140,17 @@ class XgmiAllReduce:
                                           H, float(eps), m, stream_ptr(x)), "k8s_ar_addnorm_bf16")
         return y
 
+    def push_ok(self, H: int, T: int, mode: int) -> bool:
+        """A [T, H] row-parallel output can take the push epilogue in ``mode``."""
+        return push_ok(self, H, T, mode)
+
+    def linear_push_addnorm(self, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, nw: torch.Tensor,
+                            y: torch.Tensor, eps: float, cfg: int, splits: int = 1,
+                            mode: Optional[int] = None) -> torch.Tensor:
+        """``residual += all_reduce(x @ w.T)``, ``y = rmsnorm(residual) * nw`` with
+        the push epilogue: see :func:`linear_push_addnorm`."""
+        return linear_push_addnorm(self, x, w, residual, nw, y, eps, cfg, splits, mode)
+
     def all_to_all(self, send: torch.Tensor, recv: torch.Tensor) -> torch.Tensor:
         """Equal-split all-to-all: ``send`` [world, chunk...] bf16 -> ``recv`` (same
         shape), ``recv[r]`` = rank r's ``send[this rank]``.  Device-side epoch:
@@ -187,3 +201,32 @@ class XgmiAllReduce:
             self.L.k8s_ar_close_handle(q)
         self.L.k8s_ar_free(self._own)
         self.id = -1
+
+
+def push_ok(car, H: int, T: int, mode: int) -> bool:
+    return bool(car.L.k8s_ar_push_ok(car.id, int(H), int(T), int(mode)))
+
+
+def linear_push_addnorm(car, x: torch.Tensor, w: torch.Tensor, residual: torch.Tensor, nw: torch.Tensor,
+                        y: torch.Tensor, eps: float, cfg: int, splits: int = 1, mode: Optional[int] = None):
+    """The TP row-parallel projection + all-reduce + residual add + RMSNorm with
+    the push epilogue (csrc/kernels/allreduce.hip "push epilogue"): the stream
+    GEMM (``cfg``: LDS-DMA 13-16 / 23 / 24, or any cfg with ``splits`` > 1)
+    stores ``x @ w.T`` straight into the communicator's slots -- the whole tile
+    to every rank (one-shot) or each strip to the owner of its columns
+    (two-shot) -- with one flag per strip, and the fused epilogue sums the
+    local slots.  Bit-identical to ``linear`` + :meth:`XgmiAllReduce.addnorm`."""
+    from ..ops import linear as LIN
+    T, K = x.shape
+    H = w.shape[0]
+    m = mode or (1 if T * H * 2 <= ONE_SHOT_MAX else 2)
+    if not car.push_ok(H, T, m):
+        raise ValueError("output not eligible for the push epilogue")
+    part = LIN._scratch(x.device, splits * T * H).data_ptr() if splits > 1 else None
+    L = car.L
+    _check(L.k8s_gemm_stream_push(x.data_ptr(), x.stride(0), w.data_ptr(), T, H, K, int(cfg), int(splits), part,
+                                  car.id, m, stream_ptr(x)), "k8s_gemm_stream_push")
+    S = H // (128 if (splits == 1 and cfg > 20) else 64)  # common.h k8s_push_strips
+    _check(L.k8s_ar_push_addnorm_bf16(car.id, residual.data_ptr(), nw.data_ptr(), y.data_ptr(), T, H, float(eps), m,
+                                      S, stream_ptr(x)), "k8s_ar_push_addnorm_bf16")
+    return y

@@ -103,12 +103,17 @@ def test_tp2_graph_replay_matches_eager_processes_sharing_one_gpu():
     assert all(v is not None and len(v) == 24 for v in again["outs"].values())
 
 
-def _stall_worker(rank, world, port, out_dir):
+def _stall_worker(rank, world, port, out_dir, push=False):
     """Rank 1 stops arriving at the collectives after the first request: rank
     0's all-reduce waits time out, STATUS is set, and the engine fails the
-    runs in flight (and every later one) instead of returning wrong tokens."""
+    runs in flight (and every later one) instead of returning wrong tokens.
+    ``push``: o / down on the stream GEMM with the push epilogue, so the waits
+    that time out include the push consumer's per-strip flag waits."""
     import time
     import torch.distributed as dist
+    if push:
+        from k8s_llm_rca_amd.ops import layer_exec as LE
+        LE._tp_push = LE._tp_push_force = True
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
     from k8s_llm_rca_amd.models.config import get_config
     from k8s_llm_rca_amd.models.llama import LlamaModel
@@ -152,7 +157,8 @@ def _stall_worker(rank, world, port, out_dir):
         res = {"ok": [g is not None and len(g) == 16 for g, _ in ok.values()],
                "bad": [(g is None, st.get("error", "")) for g, st in bad.values()] if len(bad) == 3 else None,
                "late": [(g is None, st.get("error", "")) for g, st in late.values()],
-               "fault": isinstance(eng.error, CommFault), "status": pc.custom_ar.status()}
+               "fault": isinstance(eng.error, CommFault), "status": pc.custom_ar.status(),
+               "ar_push": int(model._exec.st.ar_push) if model._exec is not None else -1}
         torch.save(res, os.path.join(out_dir, "stall.pt"))
     torch.cuda.synchronize()
     dist.barrier()
@@ -160,13 +166,15 @@ def _stall_worker(rank, world, port, out_dir):
     dist.destroy_process_group()
 
 
-def test_tp2_stalled_peer_fails_runs():
+@pytest.mark.parametrize("push", [False, True], ids=["staged", "push"])
+def test_tp2_stalled_peer_fails_runs(push):
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     with tempfile.TemporaryDirectory() as d:
-        mp.spawn(_stall_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        mp.spawn(_stall_worker, args=(2, _free_port(), d, push), nprocs=2, join=True)
         res = torch.load(os.path.join(d, "stall.pt"), weights_only=True)
     assert res["ok"] == [True]
+    assert res["ar_push"] == int(push)
     assert res["fault"] and res["status"] == 1
     assert res["bad"] is not None and all(failed for failed, _ in res["bad"]), res["bad"]
     assert all(failed and "timed out" in err for failed, err in res["late"]), res["late"]

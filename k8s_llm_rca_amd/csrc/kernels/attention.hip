@@ -1162,12 +1162,12 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
     const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
     // a part that saw no key of the row has m = -inf: weight 0
     const float f = (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
-    L += ml.y * f;
+    L = fmaf(ml.y, f, L);  // explicit fmas: the merge16 form rounds identically
     if (a.pf_bf16) {  // O / l in bf16: the part's O is (O / l) * l
       const uint32_t v = *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(a.pf_o) + rb * D + 2 * lane);
       const float fl = f * ml.y;
-      o0 += bf2f((uint16_t)(v & 0xffffu)) * fl;
-      o1 += bf2f((uint16_t)(v >> 16)) * fl;
+      o0 = fmaf(bf2f((uint16_t)(v & 0xffffu)), fl, o0);
+      o1 = fmaf(bf2f((uint16_t)(v >> 16)), fl, o1);
     } else {
       const float2 v = *reinterpret_cast<const float2*>(a.pf_o + rb * D + 2 * lane);
       o0 += v.x * f;
@@ -1179,6 +1179,77 @@ __global__ void __launch_bounds__(256) attn_prefill_merge_kernel(AttnArgs a) {
   uint16_t* dst = a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D + 2 * lane;
   dst[0] = f2bf(o0 * inv);
   dst[1] = f2bf(o1 * inv);
+}
+
+// The bf16-partial merge (pf_bf16: VAR >= 5) at 16 rows per block: 16 lanes
+// per row, 8 dims (one 16-B load) per lane per part, so a block moves 4 KiB
+// per part instead of 1 KiB and the launch has a quarter of the waves (the
+// 2-dims-per-lane form above ran ~15 us per call on the steady-state replay:
+// tens of thousands of waves with 4-byte loads).  Same per-element arithmetic
+// in the same order: bit-identical.
+constexpr int kMergePre = 8;  // parts prefetched in one round (~97 % of the replay's merges; more: the two-pass loop)
+__global__ void __launch_bounds__(256) attn_prefill_merge16_kernel(AttnArgs a) {
+  const int kvh = blockIdx.x % a.nkv, mi = blockIdx.x / a.nkv;
+  const int c16 = threadIdx.x & 15, row = blockIdx.y * 16 + (threadIdx.x >> 4);
+  const int rows = a.m_len[mi] * a.G;
+  if (row >= rows) return;
+  const int tok0 = a.m_tok0[mi], slot0 = a.m_slot0[mi], np = a.m_np[mi];
+  float M = -INFINITY, L = 0.f, o[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) o[j] = 0.f;
+  if (np <= kMergePre) {
+    // every part's (m, l) and O piece in ONE round of loads (unconditional: parts past
+    // np re-read the last one and are never summed), then the two passes from registers
+    float2 ml[kMergePre];
+    u16x8 v[kMergePre];
+#pragma unroll
+    for (int p = 0; p < kMergePre; ++p) {
+      const size_t rb = ((size_t)(slot0 + min(p, np - 1)) * a.nkv + kvh) * a.pf_rows + row;
+      ml[p] = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
+      v[p] = *reinterpret_cast<const u16x8*>(reinterpret_cast<const uint16_t*>(a.pf_o) + rb * D + 8 * c16);
+    }
+#pragma unroll
+    for (int p = 0; p < kMergePre; ++p)
+      if (p < np) M = fmaxf(M, ml[p].x);
+#pragma unroll
+    for (int p = 0; p < kMergePre; ++p)
+      if (p < np) {
+        const float f = (ml[p].x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml[p].x - M);
+        L = fmaf(ml[p].y, f, L);
+        const float fl = f * ml[p].y;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) o[j] = fmaf(bf2f(v[p][j]), fl, o[j]);
+      }
+  } else {
+#pragma unroll 4
+  for (int p = 0; p < np; ++p) {
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * a.pf_rows + row;
+    M = fmaxf(M, a.pf_ml[rb * 2]);
+  }
+#pragma unroll 4
+  for (int p = 0; p < np; ++p) {
+    const size_t rb = ((size_t)(slot0 + p) * a.nkv + kvh) * a.pf_rows + row;
+    const float2 ml = *reinterpret_cast<const float2*>(a.pf_ml + rb * 2);
+    const float f = (ml.x == -INFINITY) ? 0.f : __builtin_amdgcn_exp2f(ml.x - M);
+    L = fmaf(ml.y, f, L);
+    const u16x8 v = *reinterpret_cast<const u16x8*>(reinterpret_cast<const uint16_t*>(a.pf_o) + rb * D + 8 * c16);
+    const float fl = f * ml.y;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) o[j] = fmaf(bf2f(v[j]), fl, o[j]);
+  }
+  }
+  const float inv = L > 0.f ? 1.f / L : 0.f;
+  const int tt = row / a.G, g = row % a.G;
+  u16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = f2bf(o[j] * inv);
+  *reinterpret_cast<u16x8*>(a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D + 8 * c16) = r;
+}
+
+// K8SRCA_PF_MERGE16=0: the 2-dims-per-lane merge for bf16 partials too (A/B, read per launch)
+static bool pf_merge16() {
+  const char* e = std::getenv("K8SRCA_PF_MERGE16");
+  return !(e && e[0] == '0');
 }
 
 }  // namespace k8s
@@ -1295,7 +1366,9 @@ K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const 
       hipLaunchKernelGGL(attn_prefill_w8_kernel<2>, dim3(n_tiles * nkv), dim3(512), 0, stream, a);
     else
       hipLaunchKernelGGL(attn_prefill_pg64_kernel, dim3(n_tiles * nkv), dim3(256), 0, stream, a);
-    if (n_merge > 0)
+    if (n_merge > 0 && a.pf_bf16 && pf_merge16())
+      hipLaunchKernelGGL(attn_prefill_merge16_kernel, dim3(n_merge * nkv, a.pf_rows / 16), dim3(256), 0, stream, a);
+    else if (n_merge > 0)
       hipLaunchKernelGGL(attn_prefill_merge_kernel, dim3(n_merge * nkv, a.pf_rows / 4), dim3(256), 0, stream, a);
   } else {
     if (n_merge > 0) return (int)hipErrorInvalidValue;  // the generic kernel does not split

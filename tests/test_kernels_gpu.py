@@ -738,9 +738,10 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     q = torch.randn(T, (nq + 2 * nkv) * 128, device=dev).bfloat16()
     scale = 1 / math.sqrt(128)
     outs = {}
-    for w8 in ("2", "4", "5", "6", "1", "0"):  # w8 compiler schedule, explicit schedule, + LDS epilogue (1 = default),
-        # + hand-issued LDS reads with counted waits, pg64
-        monkeypatch.setenv("K8SRCA_PF_W8", w8)
+    for w8 in ("2", "4", "5", "6", "6m", "1", "0"):  # w8 compiler schedule, explicit schedule, + LDS epilogue
+        # (1 = default), + hand-issued LDS reads with counted waits (6m: with the 2-dims-per-lane merge), pg64
+        monkeypatch.setenv("K8SRCA_PF_W8", w8.rstrip("m"))
+        monkeypatch.setenv("K8SRCA_PF_MERGE16", "0" if w8.endswith("m") else "1")
         torch.manual_seed(7)  # the same block tables for both kernels
         meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
         outs[w8] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
@@ -749,6 +750,7 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     for k in ("2", "4", "5"):
         torch.testing.assert_close(outs[k].cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
     assert torch.equal(outs["6"], outs["5"])  # the same arithmetic in the same order, other waits
+    assert torch.equal(outs["6"], outs["6m"])  # the 16-B-per-lane merge: same per-element arithmetic
     # 5 = 4 with the LDS-staged store: final rows bit-identical, split tiles via bf16 O / l partials
     torch.testing.assert_close(outs["5"].float(), outs["4"].float(), atol=4e-3, rtol=4e-3)
     torch.testing.assert_close(outs["2"].float(), outs["0"].float(), atol=1e-2, rtol=1e-2)

@@ -179,7 +179,9 @@ def main():
             ql = [q for c, q in pre[i]]
             T = sum(ql)
             for k in kinds:
-                os.environ["K8SRCA_PF_W8"] = k.split("@")[0]
+                os.environ["K8SRCA_PF_W8"] = k.split("@")[0].rstrip("m")
+                # "<kind>m": the 2-dims-per-lane merge kernel (K8SRCA_PF_MERGE16=0)
+                os.environ["K8SRCA_PF_MERGE16"] = "0" if k.split("@")[0].endswith("m") else "1"
                 arm = k.split("@")[1] if "@" in k else None
                 # "@o<pages>": makespan split choice everywhere; "@h<pages>": only where the
                 # fixed-target rule would split; "@<n>": fixed target of n workgroups

@@ -430,6 +430,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "forward_s": round(d["forward_s"], 3), "sample_s": round(d["sample_s"], 3),
                    "host_s": round(d["host_s"], 3), "evictions": d["evictions"],
                    "preemptions": d.get("preemptions", 0), "requests": d["requests"],
+                   "nonfinite_rows": d.get("nonfinite_rows", 0),
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,

@@ -183,6 +183,8 @@ __device__ void radix_pass(const T* lr, int V, int vocab_off, float it, const in
   __syncthreads();
 }
 
+constexpr int kNonFinite = -2;
+
 template <typename T>
 __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logits, int ld, int V, int vocab_off,
                                                      const float* __restrict__ temperature,
@@ -346,17 +348,24 @@ __global__ void __launch_bounds__(256) sample_kernel(const T* __restrict__ logit
     __syncthreads();
   }
 
-  // ---- Gumbel-max (or argmax) over the survivors
+  // ---- Gumbel-max (or argmax) over the survivors.  A row with a non-finite
+  // allowed logit (NaN / +-inf: the model's output went bad) returns kNonFinite
+  // (-2), never a token picked from garbage: the engine fails that request
+  // loudly (-1 stays "no allowed token").
   Best best{-INFINITY, -1};
+  int nonfin = 0;
   for_allowed(lr, V, vocab_off, it, lst, ll, mk, [&](int gi, float v) {
+    nonfin |= !(fabsf(v) <= 3.402823466e38f);
     if (filt && okey(v) < thr) return;
     if (!greedy) v += gumbel(seed, 0u, step, gi);
     best = better(best, Best{v, gi});
   });
   const Best b = block_best(best, sv, si);
+  const int bad = __syncthreads_or(nonfin);
   if (threadIdx.x == 0) {
-    if (out) out[row] = b.i;
-    if (out_pair) out_pair[row] = make_float2(b.v, (float)b.i);  // ids < 2^24: exact in f32
+    if (out) out[row] = bad ? kNonFinite : b.i;
+    // pairs (TP shards): +inf wins the cross-shard max, so the -2 reaches the engine
+    if (out_pair) out_pair[row] = bad ? make_float2(INFINITY, (float)kNonFinite) : make_float2(b.v, (float)b.i);
   }
 }
 

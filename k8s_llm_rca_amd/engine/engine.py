@@ -294,6 +294,7 @@ class LLMEngine:
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
                       "prefix_hit_tokens": 0, "prefill_deferred_steps": 0, "preemptions": 0, "cancelled": 0,
+                      "nonfinite_rows": 0,
                       "timeouts": 0,
                       "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
                       "tiny_chunk_tokens": 0}
@@ -1557,7 +1558,14 @@ class LLMEngine:
                 continue
             if r.t_first is None:
                 r.t_first = now
-            if t < 0:
+            if t == SMP.NON_FINITE:  # the model's logits went non-finite: fail loudly, never emit garbage
+                self.stats["nonfinite_rows"] += 1
+                if self.stats["nonfinite_rows"] == 1:
+                    log.error("non-finite logits (NaN / inf) in a sampled row (sequence %d): failing its request",
+                              s.id)
+                self._fail_req(r, "non-finite logits (NaN / inf) in this request's row")
+                continue
+            if t < 0:  # no allowed token left
                 self._finish(r)
                 continue
             r.n_sampled += 1

@@ -31,8 +31,10 @@ def sample(logits: torch.Tensor, temperature: Optional[torch.Tensor], seeds: Opt
 
     Vocab-parallel use: ``logits`` holds global columns ``vocab_off ..``; with
     ``pairs=True`` the result is [B, 2] float32 (winning perturbed score,
-    global id; -inf / -1 when the shard has no allowed token) to be combined
-    across ranks by :func:`combine_pairs`.  ``candidates=True`` (with pairs)
+    global id; -inf / -1 when the shard has no allowed token; +inf /
+    ``NON_FINITE`` when an allowed logit is NaN / inf) to be combined across
+    ranks by :func:`combine_pairs`.  A row with a non-finite allowed logit
+    samples ``NON_FINITE`` (-2): the engine fails its request.  ``candidates=True`` (with pairs)
     also returns [B, CAND_K, 3] (v, id, v + Gumbel noise) shard candidates of
     the top-k / top-p rows for :func:`combine_candidates`.
     """
@@ -160,6 +162,11 @@ def filter_threshold(v: torch.Tensor, k: int, p: float) -> torch.Tensor:
     return keep
 
 
+# token id a sampler returns for a row whose allowed logits are not all finite
+# (csrc/kernels/sampling.hip kNonFinite); -1 = no allowed token
+NON_FINITE = -2
+
+
 def _sample_ref(logits, temperature, seeds, steps, mask_id, mask_table, list_off, list_len, lists, vocab, out,
                 vocab_off=0, pairs=False, top_k=None, top_p=None, cand=None):
     """``vocab`` = local columns to consider; ids are global (``+ vocab_off``)."""
@@ -199,6 +206,12 @@ def _sample_ref(logits, temperature, seeds, steps, mask_id, mask_table, list_off
                 cand[b, :len(cv), 0] = cv
                 cand[b, :len(cv), 1] = ci.float()
                 cand[b, :len(cv), 2] = cv + gumbel_ref(int(seeds[b]), 0, int(steps[b]), ci) if temp > 0 else cv
+        if len(c) and not bool(torch.isfinite(v).all()):  # the kernel's kNonFinite row
+            if pairs:
+                out[b, 0], out[b, 1] = float("inf"), float(NON_FINITE)
+            else:
+                out[b] = NON_FINITE
+            continue
         if len(c) and temp > 0 and (k > 0 or p < 1.0):
             keep = filter_threshold(v, k, p)
             c, v = c[keep], v[keep]

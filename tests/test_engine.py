@@ -551,3 +551,19 @@ def test_replay_free_text_runs_to_budget():
     rep = _Replay(rt, [tok.eot_id, tok.eos_id], True, seed=0)
     out = rep.generate(F.semantic_grammar(F.GenerationBudget(semantic_tokens=40)), 64)
     assert len(out) == 40 and tok.eot_id not in out
+
+
+def test_nonfinite_logits_fail_the_request_loudly():
+    """Logits that went NaN (here: a poisoned final norm) must fail the request
+    with an error -- never finish it silently with a token sampled from garbage
+    (the sampler's NON_FINITE row, ops/sampling.py) -- and be counted."""
+    eng = _engine(temperature=0.0)
+    eng.model.final_norm.fill_(float("nan"))
+    sid = eng.new_sequence()
+    p = eng.tok.system_prefix("sys") + eng.tok.message("user", "hello") + eng.tok.header("assistant")
+    out = {}
+    eng.submit(sid, p, None, 10, on_done=lambda g, st: out.setdefault("a", (g, st)))
+    eng.run_until_idle()
+    g, st = out["a"]
+    assert g is None and "non-finite" in st["error"]
+    assert eng.stats["nonfinite_rows"] >= 1

@@ -94,3 +94,51 @@ def test_candidates_combine_matches_single_device(tp):
     ct = SMP.combine_candidates(torch.stack(cands), a["top_k"], a["top_p"])
     got = torch.where(filt, ct, tok)
     assert torch.equal(got, full), (got, full)
+
+
+def _nonfinite_case(dev):
+    B, V = 5, 1024
+    torch.manual_seed(4)
+    logits = torch.randn(B, V)
+    logits[0, 17] = float("nan")     # allowed NaN -> NON_FINITE
+    logits[1, 900] = float("inf")    # allowed +inf -> NON_FINITE
+    logits[2, 3] = -float("inf")     # allowed -inf -> NON_FINITE (the model's output went bad)
+    logits[3, 40] = float("nan")     # NaN only in a token the row's list excludes -> a normal pick
+    lists = torch.tensor([1, 2, 3, 5, 8], dtype=torch.int32)
+    a = _args(B, [0.0, 0.7, 0.0, 0.9, 0.0], [0] * B, [1.0] * B)
+    a["list_len"][3] = len(lists)
+    a["lists"] = lists
+    out = torch.empty(B, dtype=torch.int32, device=dev)
+    return logits.to(dev), a, out, V
+
+
+def test_sampler_flags_nonfinite_rows_reference():
+    """A row whose allowed logits are not all finite returns SMP.NON_FINITE (the
+    engine then fails that request: engine._process_tokens) instead of a token
+    picked from garbage; NaN outside the allowed set does not matter."""
+    logits, a, out, V = _nonfinite_case("cpu")
+    SMP._sample_ref(logits, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                    a["list_len"], a["lists"], V, out)
+    assert out[:3].tolist() == [SMP.NON_FINITE] * 3
+    assert int(out[3]) in (1, 2, 3, 5, 8) and 0 <= int(out[4]) < V
+    pairs = torch.empty(5, 2)
+    SMP._sample_ref(logits, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                    a["list_len"], a["lists"], V, pairs, pairs=True)
+    # a bad shard's +inf wins the cross-shard max: the TP combine returns NON_FINITE too
+    assert SMP.combine_pairs(torch.stack([pairs, pairs])).tolist()[:3] == [SMP.NON_FINITE] * 3
+
+
+@pytest.mark.gpu
+def test_sampler_flags_nonfinite_rows_kernel():
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    logits, a, out, V = _nonfinite_case("cuda")
+    a = {k: (v.cuda() if isinstance(v, torch.Tensor) else v) for k, v in a.items()}
+    for lg in (logits, logits.bfloat16()):
+        ref = torch.empty(5, dtype=torch.int32)
+        SMP._sample_ref(lg.float().cpu(), *(a[k].cpu() for k in ("temperature", "seeds", "steps", "mask_id")), None,
+                        a["list_off"].cpu(), a["list_len"].cpu(), a["lists"].cpu(), V, ref)
+        got = SMP.sample(lg, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                         a["list_len"], a["lists"], V)
+        assert got.cpu().tolist()[:3] == [SMP.NON_FINITE] * 3
+        assert torch.equal(got.cpu()[3:], ref[3:])

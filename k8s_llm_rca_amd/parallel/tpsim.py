@@ -211,6 +211,23 @@ def _time_us(fn, reps: int = 20) -> float:
     return ev0.elapsed_time(ev1) * 1e3 / reps
 
 
+def _fused_epilogue(car, T: int, H: int, mode: int) -> bool:
+    """The layer executor's fused all-reduce + add + RMSNorm applies (ops/layer_exec.py fits / ar_fuse)."""
+    return (car is not None and mode in (1, 2) and hasattr(car, "addnorm")
+            and T * H * 2 + 4 * T <= car.max_bytes and (mode == 1 or (H // 8) % car.world == 0))
+
+
+def _fused_standin_us(car, T: int, H: int, mode: int, device) -> float:
+    from ..ops import norm as NORM
+    x = torch.zeros(T, H, dtype=torch.bfloat16, device=device)
+    res = torch.zeros_like(x)
+    y = torch.empty_like(x)
+    w = torch.ones(H, dtype=torch.bfloat16, device=device)
+    fused = _time_us(lambda: car.addnorm(x, res, w, y, 1e-5, mode))
+    plain = _time_us(lambda: NORM.rmsnorm(x, w, 1e-5, residual=res, out=y))
+    return max(0.0, fused - plain)
+
+
 def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int, device, moe_k: int = 0) -> dict:
     """Collective time of a simulated run: for every forward size T seen
     (``rows_hist`` = {T: forwards}) the layer's collectives, timed as stood in
@@ -220,7 +237,10 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
     fixed-capacity all-to-alls of ``parallel/ep.py`` (dispatch, combine, row
     all-gather).  ``projected`` wall = measured wall - stand-in + modelled (the
     collectives are serial in the step's stream).  ``modelled_s_by_hop``: the
-    same model at each hop latency of ``HOP_SENSITIVITY_US``."""
+    same model at each hop latency of ``HOP_SENSITIVITY_US``.  Dense steps whose
+    all-reduces the layer executor fuses with the residual add + RMSNorm time
+    that fused kernel less the rmsnorm it replaces (``per_T[T]["standin"]``);
+    the others time the plain all-reduce."""
     standin_us = model_us = 0.0
     by_hop = {h: 0.0 for h in HOP_SENSITIVITY_US}
     per_t = {}
@@ -229,7 +249,15 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
         t = torch.zeros(T * hidden, dtype=torch.bfloat16, device=device)
         car = pc.custom_ar
         mode = car.mode_for(t) if car is not None else 0
-        s_us = _time_us(lambda: pc.all_reduce(t))
+        if not moe_k and _fused_epilogue(car, T, hidden, mode):
+            # the dense executor's collective: the fused all-reduce + add + RMSNorm, less
+            # the rmsnorm launch it replaces (ops/layer_exec.py ar_fuse)
+            s_us = _fused_standin_us(car, T, hidden, mode, device)
+            kind = "fused"
+        else:
+            s_us = _time_us(lambda: pc.all_reduce(t))
+            kind = "allreduce"
+
         m_us = xgmi_model_us(T * hidden * 2, N, mode)
         n_ar = 1 if moe_k else 2
         s_tot, m_tot = n_ar * s_us, n_ar * m_us
@@ -250,7 +278,7 @@ def project(rows_hist: dict, pc: SimParallelContext, hidden: int, n_layers: int,
             by_hop[h] += k * h_tot[h]
         standin_us += k * s_tot
         model_us += k * m_tot
-        per_t[int(T)] = {"forwards": int(n), "mode": mode, "standin_us": round(s_tot, 2),
+        per_t[int(T)] = {"forwards": int(n), "mode": mode, "standin": kind, "standin_us": round(s_tot, 2),
                          "model_us": round(m_tot, 2)}
     return {"standin_s": standin_us / 1e6, "modelled_s": model_us / 1e6, "per_T": per_t,
             "modelled_s_by_hop": {h: v / 1e6 for h, v in by_hop.items()}}

@@ -17,3 +17,20 @@ def test_hop_latency_terms():
     assert T.xgmi_model_us(nb, n, 1, 0.0) == pytest.approx(nb / (T.XGMI_LINK_GBPS * 1e3))
     assert T.xgmi_model_us(nb, n, 2, 0.0) == pytest.approx(2 * nb / (n * T.XGMI_LINK_GBPS * 1e3))
     assert tuple(T.HOP_SENSITIVITY_US) == (2.5, 5.0, 10.0)
+
+
+def test_fused_standin_selection_follows_the_executor():
+    """The projection times the fused all-reduce + add + RMSNorm exactly where the
+    layer executor would fuse (message + row sums fit the buffer; two-shot needs
+    H / 8 chunks divisible by the world), else the plain all-reduce."""
+    class Car:
+        max_bytes, world = 8 << 20, 8
+
+        def addnorm(self, *a, **k):  # presence is what the selection checks
+            return None
+    car, H = Car(), 8192
+    assert T._fused_epilogue(car, 32, H, 1) and T._fused_epilogue(car, 256, H, 2)
+    assert not T._fused_epilogue(car, 512, H, 2)      # 8 MiB + row sums > the buffer
+    assert not T._fused_epilogue(car, 32, H, 0)       # RCCL-size message
+    assert not T._fused_epilogue(car, 32, 8200, 2)    # 1025 chunks do not split over 8 ranks
+    assert not T._fused_epilogue(None, 32, H, 1)

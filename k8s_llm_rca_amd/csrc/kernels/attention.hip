@@ -452,6 +452,13 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
 // so a row costs a few memory latencies instead of 2 * n_parts serial ones
 // (9.1 us per layer at one decode row with ~12 partitions before, c=1 profile).
 // Same max and the same summation order as the serial form.
+// PRE: a row of at most kRedPre partitions loads every partition's (m, l) and
+// its partial-O column in ONE round (unconditional, clamped to the last
+// partition) and merges from registers -- no LDS exchange, no barriers; the
+// same max and the same per-partition arithmetic in the same order
+// (bit-identical).  Longer rows take the LDS form below.
+constexpr int kRedPre = 16;
+template <bool PRE>
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   __shared__ float sf[128], sl[128], scratch[16];
   const int qh = blockIdx.x, seq = blockIdx.y, d = threadIdx.x;
@@ -460,6 +467,31 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   const int np = min(a.n_parts, (ctx + part_size - 1) / part_size);
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
+  if (PRE && np <= kRedPre) {
+    float mm[kRedPre], ml[kRedPre], po[kRedPre];
+#pragma unroll
+    for (int p = 0; p < kRedPre; ++p) {
+      const size_t b = base + min(p, np - 1);
+      mm[p] = a.part_ml[b * 2];
+      ml[p] = a.part_ml[b * 2 + 1];
+      po[p] = a.part_o[b * D + d];
+    }
+    float M = -INFINITY;
+#pragma unroll
+    for (int p = 0; p < kRedPre; ++p)
+      if (p < np) M = fmaxf(M, mm[p]);
+    float L = 0.f, acc = 0.f;
+#pragma unroll
+    for (int p = 0; p < kRedPre; ++p)
+      if (p < np) {
+        const float f = (mm[p] == -INFINITY) ? 0.f : exp2f(mm[p] - M);
+        L += __fmul_rn(ml[p], f);  // rounded product, then the add: the LDS form's l * f via sl[]
+        acc += po[p] * f;          // contracted like the LDS form's po * sf[j]
+      }
+    const int qrow = a.q_start[seq];
+    a.out[(size_t)qrow * a.out_stride + qh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+    return;
+  }
   float M = -INFINITY;
   for (int p = d; p < np; p += 128) M = fmaxf(M, a.part_ml[(base + p) * 2]);
   M = block_max(M, scratch);
@@ -1246,6 +1278,13 @@ __global__ void __launch_bounds__(256) attn_prefill_merge16_kernel(AttnArgs a) {
   *reinterpret_cast<u16x8*>(a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D + 8 * c16) = r;
 }
 
+// K8SRCA_DECODE_REDUCE_PRE=1: the decode split-KV reduce's register form for rows of <= kRedPre
+// partitions (A/B, read per launch; off until measured on the GPU)
+static bool decode_reduce_pre() {
+  const char* e = std::getenv("K8SRCA_DECODE_REDUCE_PRE");
+  return e && e[0] == '1';
+}
+
 // K8SRCA_PF_MERGE16=0: the 2-dims-per-lane merge for bf16 partials too (A/B, read per launch)
 static bool pf_merge16() {
   const char* e = std::getenv("K8SRCA_PF_MERGE16");
@@ -1292,7 +1331,12 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
     const long nw = (long)S * nkv * n_parts;
     hipLaunchKernelGGL(attn_decode_kernel, dim3((unsigned)nw), dim3(64), 0, stream, a, S);
   }
-  if (n_parts > 1) hipLaunchKernelGGL(attn_reduce_kernel, dim3(nq, S), dim3(128), 0, stream, a);
+  if (n_parts > 1) {
+    if (decode_reduce_pre())
+      hipLaunchKernelGGL(attn_reduce_kernel<true>, dim3(nq, S), dim3(128), 0, stream, a);
+    else
+      hipLaunchKernelGGL(attn_reduce_kernel<false>, dim3(nq, S), dim3(128), 0, stream, a);
+  }
   return (int)hipGetLastError();
 }
 

@@ -188,7 +188,7 @@ def _cpu_meta(meta):
 @pytest.mark.parametrize("BS", [64, 32])  # 64: persistent work-list kernel; 32: (seq, part) grid kernel
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 8)])
 @pytest.mark.parametrize("ctx", [[1], [17, 64, 65], [1000, 3, 2500, 128], [5000], [130] * 300])
-def test_paged_decode(nq, nkv, ctx, BS):
+def test_paged_decode(nq, nkv, ctx, BS, monkeypatch):
     _need_gpu()
     torch.manual_seed(1)
     NB = sum((c + BS - 1) // BS for c in ctx) + 4
@@ -199,6 +199,12 @@ def test_paged_decode(nq, nkv, ctx, BS):
     out = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
     ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
     torch.testing.assert_close(out.cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
+    # the split-KV reduce's register form (<= 16 partitions) == its LDS form, bit for bit
+    outs = {}
+    for pre in ("1", "0"):
+        monkeypatch.setenv("K8SRCA_DECODE_REDUCE_PRE", pre)
+        outs[pre] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
+    assert torch.equal(outs["1"], outs["0"])
 
 
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (64, 8), (8, 1)])

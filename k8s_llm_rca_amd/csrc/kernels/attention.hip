@@ -467,7 +467,7 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   const int np = min(a.n_parts, (ctx + part_size - 1) / part_size);
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
-  if (PRE && np <= kRedPre) {
+  if (PRE && np >= 1 && np <= kRedPre) {  // (np == 0, an empty row: the LDS form writes its zero)
     float mm[kRedPre], ml[kRedPre], po[kRedPre];
 #pragma unroll
     for (int p = 0; p < kRedPre; ++p) {

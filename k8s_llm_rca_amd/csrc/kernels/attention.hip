@@ -452,11 +452,11 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
 // so a row costs a few memory latencies instead of 2 * n_parts serial ones
 // (9.1 us per layer at one decode row with ~12 partitions before, c=1 profile).
 // Same max and the same summation order as the serial form.
-// PRE: a row of at most kRedPre partitions loads every partition's (m, l) and
-// its partial-O column in ONE round (unconditional, clamped to the last
-// partition) and merges from registers -- no LDS exchange, no barriers; the
-// same max and the same per-partition arithmetic in the same order
-// (bit-identical).  Longer rows take the LDS form below.
+// PRE: a row of at most kRedPre partitions issues every partition's partial-O
+// column load up front (unconditional, clamped to the last partition), beside
+// the (m, l) loads, instead of after the max / weights exchange; the exchange
+// and the summation are the LDS form's own (bit-identical).  Longer rows take
+// the LDS form below.
 constexpr int kRedPre = 16;
 template <bool PRE>
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
@@ -468,25 +468,28 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
   if (PRE && np >= 1 && np <= kRedPre) {  // (np == 0, an empty row: the LDS form writes its zero)
-    float mm[kRedPre], ml[kRedPre], po[kRedPre];
+    // the partial-O column of every partition in flight first (clamped: unconditional),
+    // then the LDS form's own max / weights exchange, so the arithmetic is the same
+    float po[kRedPre];
 #pragma unroll
-    for (int p = 0; p < kRedPre; ++p) {
-      const size_t b = base + min(p, np - 1);
-      mm[p] = a.part_ml[b * 2];
-      ml[p] = a.part_ml[b * 2 + 1];
-      po[p] = a.part_o[b * D + d];
+    for (int p = 0; p < kRedPre; ++p) po[p] = a.part_o[(base + min(p, np - 1)) * D + d];
+    float M = d < np ? a.part_ml[(base + d) * 2] : -INFINITY;
+    M = block_max(M, scratch);
+    float f = 0.f, lf = 0.f;
+    if (d < np) {
+      const float m = a.part_ml[(base + d) * 2];
+      f = (m == -INFINITY) ? 0.f : exp2f(m - M);
+      lf = a.part_ml[(base + d) * 2 + 1] * f;
     }
-    float M = -INFINITY;
-#pragma unroll
-    for (int p = 0; p < kRedPre; ++p)
-      if (p < np) M = fmaxf(M, mm[p]);
+    sf[d] = f;
+    sl[d] = lf;
+    __syncthreads();
     float L = 0.f, acc = 0.f;
 #pragma unroll
-    for (int p = 0; p < kRedPre; ++p)
-      if (p < np) {
-        const float f = (mm[p] == -INFINITY) ? 0.f : exp2f(mm[p] - M);
-        L += __fmul_rn(ml[p], f);  // rounded product, then the add: the LDS form's l * f via sl[]
-        acc += po[p] * f;          // contracted like the LDS form's po * sf[j]
+    for (int j = 0; j < kRedPre; ++j)
+      if (j < np) {
+        L += sl[j];
+        acc = fmaf(po[j], sf[j], acc);  // explicit: an unrolled, predicated a * b + c may not contract
       }
     const int qrow = a.q_start[seq];
     a.out[(size_t)qrow * a.out_stride + qh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
@@ -513,7 +516,7 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
 #pragma unroll 8
     for (int j = 0; j < n; ++j) {
       L += sl[j];
-      acc += po[(size_t)j * D] * sf[j];
+      acc = fmaf(po[(size_t)j * D], sf[j], acc);
     }
   }
   const int qrow = a.q_start[seq];
@@ -1278,11 +1281,12 @@ __global__ void __launch_bounds__(256) attn_prefill_merge16_kernel(AttnArgs a) {
   *reinterpret_cast<u16x8*>(a.out + (size_t)(tok0 + tt) * a.out_stride + (kvh * a.G + g) * D + 8 * c16) = r;
 }
 
-// K8SRCA_DECODE_REDUCE_PRE=1: the decode split-KV reduce's register form for rows of <= kRedPre
-// partitions (A/B, read per launch; off until measured on the GPU)
+// the decode split-KV reduce's prefetch form for rows of <= kRedPre partitions (default;
+// K8SRCA_DECODE_REDUCE_PRE=0: the LDS form everywhere, A/B, read per launch).  Bit-identical;
+// 8.5 -> 6.4 us per call on the steady-state decode replay (profiles/r4/reduce_pre/)
 static bool decode_reduce_pre() {
   const char* e = std::getenv("K8SRCA_DECODE_REDUCE_PRE");
-  return e && e[0] == '1';
+  return !(e && e[0] == '0');
 }
 
 // K8SRCA_PF_MERGE16=0: the 2-dims-per-lane merge for bf16 partials too (A/B, read per launch)

@@ -39,7 +39,8 @@ def test_rmsnorm(T, H):
     torch.testing.assert_close(y2.cpu().float(), y2_ref.float(), atol=2e-2, rtol=2e-2)
 
 
-@pytest.mark.parametrize("S,T,H", [(8, 96, 4096), (2, 5, 4096), (4, 33, 8192), (8, 3, 768)])
+@pytest.mark.parametrize("S,T,H", [(8, 96, 4096), (2, 5, 4096), (4, 33, 8192), (8, 3, 768), (3, 17, 4096),
+                                   (2, 128, 4096), (4, 128, 4096)])
 def test_splitk_addnorm(S, T, H):
     """Fused split-K reduce + residual add + RMSNorm == reduce kernel order +
     rmsnorm kernel, bit for bit (the executor relies on it), and close to fp32."""

@@ -1,4 +1,5 @@
 #!/bin/bash
+# (tools/splitk_an_ab.py was removed with the reverted kernel change; results in profiles/r4/splitk_an/)
 # round 4: split-count-templated split-K add+norm -- norm kernel tests (bit-identity vs reduce + rmsnorm), A/B
 set -o pipefail
 cd $GRAFT_REPO_ROOT; export TMPDIR=/tmp; O=gpurun_out/r4am; mkdir -p $O

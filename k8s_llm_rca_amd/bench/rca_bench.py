@@ -30,6 +30,15 @@ from typing import Any, Dict, List, Optional
 import torch
 
 METRIC = "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-node graph"
+# The thread-truncation contract is part of the workload definition: the
+# reference's threads grow for the whole batch (test_with_file.py:28-38) and its
+# server cuts them at the model window; here an overflowing thread drops its
+# oldest non-seed turns down to TRUNC_LOW of the window, keeps the system prompt
+# and the first KEEP_SEED messages (the reference's seeding messages), and the
+# cut point is sticky (engine/backend.py).  These two numbers set how much of
+# the prefill is re-prefill after a cut (~half in the steady state), so they
+# are pinned here, checked against the backend and reported in the JSON config.
+TRUNCATION_CONTRACT = {"trunc_low": 0.5, "keep_seed": 2, "policy": "sticky"}
 REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
 
 
@@ -114,12 +123,18 @@ def _thread_cpu() -> Dict[str, float]:
     return out
 
 
-def _dist_init():
+def _dist_init(tp_mode: bool, same_gpu: bool):
+    """Data-parallel replicas exchange only host-side metrics (a barrier, the
+    max elapsed time, latency lists): a gloo group, so the DP bench never
+    initialises RCCL and runs the same code with any device mapping.  A TP
+    engine over separate GPUs uses RCCL's group for the xGMI communicator's
+    setup (its data collectives run on the xGMI kernels); TP ranks sharing one
+    GPU use gloo (RCCL refuses duplicate devices)."""
     import torch.distributed as dist
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world > 1 and not dist.is_initialized():
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
+        backend = "nccl" if (torch.cuda.is_available() and tp_mode and not same_gpu) else "gloo"
         if backend == "nccl":
             torch.cuda.set_device(int(os.environ.get("LOCAL_RANK", "0")))
         dist.init_process_group(backend)
@@ -141,7 +156,8 @@ def _allreduce_max(x: float, world: int, device) -> float:
     if world == 1:
         return x
     import torch.distributed as dist
-    t = torch.tensor([x], dtype=torch.float64, device=device if device.type == "cuda" else "cpu")
+    on_dev = device.type == "cuda" and dist.get_backend() == "nccl"
+    t = torch.tensor([x], dtype=torch.float64, device=device if on_dev else "cpu")
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())
 
@@ -164,6 +180,39 @@ def _allgather_list(xs: List[float], world: int, device) -> List[float]:
     return [v for part in out for v in part]
 
 
+def _window_mark(tag: int, cuda: bool) -> None:
+    """A named one-wave kernel at the start (1) / end (2) of the timed window:
+    ``tools/window_summary.py`` cuts a rocprofv3 kernel trace to exactly the
+    kernels between the two marks (the engine issues on the same stream)."""
+    if cuda:
+        from ..ops._lib import lib, stream_ptr
+        lib().k8s_window_mark(tag, stream_ptr())
+
+
+# A window whose analyses sampled almost nothing did almost no work (e.g. every
+# request ending after a few tokens): such a line is not a measurement.  The
+# conclusion + resolution budgets alone are 160 sampled tokens per analysis; a
+# normal window samples ~960 (BENCH_r04 work_per_analysis).
+SANITY_MIN_SAMPLED_PER_ANALYSIS = 80
+
+
+def sanity(res: Dict[str, Any]) -> Dict[str, Any]:
+    """Checks that the timed window did the work it claims (``ok`` false makes
+    bench.py exit non-zero after printing the line)."""
+    why = []
+    if res["engine"].get("nonfinite_rows", 0):
+        why.append(f"{res['engine']['nonfinite_rows']} sampled rows had non-finite logits")
+    n = max(1, res["analyses_timed"])
+    if res["errors"] > 0.05 * n:
+        why.append(f"{res['errors']} of {n} timed analyses failed")
+    sp = res["work_per_analysis"]["sampled_tokens"]
+    if res["config"]["grammar_hints"] and sp < SANITY_MIN_SAMPLED_PER_ANALYSIS:
+        why.append(f"{sp} sampled tokens per analysis (< {SANITY_MIN_SAMPLED_PER_ANALYSIS}): the runs ended early")
+    if res["truncated_by_time_budget"]:
+        why.append("the time budget cut the window short")
+    return {"ok": not why, "reasons": why}
+
+
 def run(args) -> Optional[Dict[str, Any]]:
     logging.basicConfig(level=logging.WARNING)
     # bind this rank to its GPU's NUMA-local CPU slice before anything starts a
@@ -171,11 +220,17 @@ def run(args) -> Optional[Dict[str, Any]]:
     from ..utils.placement import bind_rank
     placement = bind_rank(int(os.environ.get("LOCAL_RANK", "0")),
                           int(os.environ.get("LOCAL_WORLD_SIZE", os.environ.get("WORLD_SIZE", "1"))))
-    world, rank = _dist_init()
+    world, rank = _dist_init(args.tp > 1, args.same_gpu)
     if args.gpus is not None and args.gpus != world:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world} (bench.py spawns the ranks itself)")
     cuda = torch.cuda.is_available() and args.device != "cpu"
-    device = torch.device(f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}" if cuda else "cpu")
+    # --same-gpu: every rank on cuda:0 (the one-GPU rehearsal of an N-GPU job: N DP
+    # replicas or N TP ranks sharing one MI355X; give each replica --kv-gb)
+    device = torch.device(("cuda:0" if args.same_gpu else f"cuda:{int(os.environ.get('LOCAL_RANK', '0'))}")
+                          if cuda else "cpu")
+    if args.same_gpu and cuda and world > 1 and args.kv_gb is None:
+        raise SystemExit("--same-gpu with several ranks needs --kv-gb (each rank would size its KV pool "
+                         "from the whole GPU's free memory)")
     # CPU-side torch ops of the serving process are tiny (metadata packing, pinned
     # staging): an intra-op pool of OMP_NUM_THREADS spinning workers only competes
     # with the engine thread for the rank's CPU share.  K8SRCA_TORCH_THREADS=N
@@ -214,7 +269,8 @@ def run(args) -> Optional[Dict[str, Any]]:
         if world != args.tp:
             raise SystemExit(f"--tp {args.tp} needs WORLD_SIZE={args.tp} (one TP engine over all ranks)")
         pc = attach_custom_allreduce(ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD,
-                                                     ep_size=world, ep_rank=rank, ep_group=dist.group.WORLD))
+                                                     ep_size=world, ep_rank=rank, ep_group=dist.group.WORLD),
+                                     same_gpu=args.same_gpu and cuda)
     eng = LLMEngine(EngineConfig(model=args.model, device=str(device),
                                  dtype=torch.bfloat16 if cuda else torch.float32,
                                  kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,
@@ -239,7 +295,11 @@ def run(args) -> Optional[Dict[str, Any]]:
             to_device(g, device)
             batchers.append(enable_batching(g))
     eng.start()
-    backend = EngineBackend(eng, temperature=args.temperature)
+    backend = EngineBackend(eng, temperature=args.temperature, keep_seed=TRUNCATION_CONTRACT["keep_seed"],
+                            trunc_low=TRUNCATION_CONTRACT["trunc_low"])
+    if (backend.trunc_low, backend.keep_seed) != (TRUNCATION_CONTRACT["trunc_low"], TRUNCATION_CONTRACT["keep_seed"]):
+        raise SystemExit(f"truncation {backend.trunc_low}/{backend.keep_seed} differs from the bench contract "
+                         f"{TRUNCATION_CONTRACT}")
     svc = AssistantService(backend)
     budget = GenerationBudget(semantic_tokens=args.semantic_tokens, explanation_tokens=args.explanation_tokens,
                               conclusion_tokens=args.conclusion_tokens, resolution_tokens=args.resolution_tokens)
@@ -300,10 +360,12 @@ def run(args) -> Optional[Dict[str, Any]]:
     ctx0 = backend.thread_stats()
     t_wall0 = time.time()
     cpu0, ncpu0 = _thread_cpu(), _native_cpu()
+    _window_mark(1, cuda)
     t0 = time.perf_counter()
     base = stream.n_ok
     done_all = stream.wait_ok(base + n_steps * quantum, deadline, _poll)
     t_end = time.perf_counter()
+    _window_mark(2, cuda)
     cpu1, ncpu1 = _thread_cpu(), _native_cpu()
     ctx1 = backend.thread_stats()
     # the busiest native threads over the window (HIP runtime / torch pools: one
@@ -403,7 +465,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "graph_nodes": cluster.stategraph.num_nodes, "graph_nodes_target": args.graph_nodes,
                    "distinct_incidents": len(cluster.incidents),
                    "concurrent_analyses_per_gpu": conc, "analyses_per_step": quantum * sync_world,
-                   "grammar_hints": not args.no_hints, "step_mode": "stream"},
+                   "grammar_hints": not args.no_hints, "step_mode": "stream",
+                   "truncation": dict(TRUNCATION_CONTRACT, max_context=eng.max_context)},
         "p50_latency_s": round(p50, 3),
         "p90_latency_s": round(p90, 3),
         "analyses_timed": total,
@@ -432,6 +495,9 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "preemptions": d.get("preemptions", 0), "requests": d["requests"],
                    "nonfinite_rows": d.get("nonfinite_rows", 0),
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
+                   # work counters of tools/window_summary.py's roofline accounting
+                   "prefill_attn_pairs": d["prefill_attn_pairs"], "small_steps": d["small_steps"],
+                   "small_rows": d["small_rows"], "big_rows": d["big_rows"],
                    "kv_blocks": eng.kv.num_blocks, "wait_s": round(d["wait_s"], 3),
                    "prefix_hit_tokens": d["prefix_hit_tokens"], "shared_kv_blocks": eng.kv.shared_blocks,
                    "captures": d["captures"], "capture_s": round(d["capture_s"], 3),
@@ -475,6 +541,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                   "kernel_batches": int(sum(b["launches"] for b in bstats)),
                   "max_batch": int(max([b["max_batch"] for b in bstats] or [0]))},
     }
+    res["sanity"] = sanity(res)
     if world > 1 and not tp_mode:
         import torch.distributed as dist
         dist.barrier()
@@ -504,6 +571,9 @@ def parser() -> argparse.ArgumentParser:
                    help="project a TP=N engine from ONE GPU: rank 0's shard at real shapes, collectives stood "
                         "in by local kernels moving the same bytes (result line: tp_sim)")
     p.add_argument("--device", default="cuda")
+    p.add_argument("--same-gpu", action="store_true",
+                   help="every rank on cuda:0: N DP replicas (with --kv-gb) or N TP ranks (xGMI kernels over "
+                        "IPC, gloo host group) sharing one GPU -- the one-GPU rehearsal of an N-GPU job")
     p.add_argument("--incidents", type=int, default=128, help="concurrent RCA analyses (pipelines) per GPU")
     p.add_argument("--graph-nodes", type=int, default=10_000)
     p.add_argument("--no-graph-device", action="store_true",
@@ -604,8 +674,12 @@ def main(argv=None) -> int:
         logging.warning("--tp %d > %d ranks: running TP=%d", args.tp, world, world)
         args.tp = world
     res = run(args)
+    rc = 0
     if res is not None:
         print(json.dumps(res), flush=True)
+        if not res["sanity"]["ok"]:
+            print(f"[bench] INVALID window: {'; '.join(res['sanity']['reasons'])}", file=sys.stderr, flush=True)
+            rc = 3
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized():
@@ -613,7 +687,7 @@ def main(argv=None) -> int:
         # threads still reference it (an abort at exit fails the torchrun job).
         dist.barrier()
         dist.destroy_process_group()
-    return 0
+    return rc
 
 
 def exit_now(rc: int) -> None:

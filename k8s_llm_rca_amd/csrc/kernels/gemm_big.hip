@@ -576,10 +576,18 @@ __global__ void __launch_bounds__(256) big_reduce_kernel(const float* __restrict
 
 // Split-tail workspace (per device, set once by the host: k8s_gemm_big_set_ws):
 // 256 partial tiles of 256 KB + 256 tickets, zeroed at allocation.  One GEMM at
-// a time per workspace: the engine issues every projection on one stream.
+// a time per workspace: two launches in flight on different streams would mix
+// their partials and leave tickets non-zero, and every later launch would then
+// sum the wrong slices.  So the workspace belongs to ONE stream: the first
+// launch that uses it claims it (g_tail_owner), and a launch on any other
+// stream runs without the split tail (whole-tile last wave: slower, never
+// wrong).  k8s_gemm_big_set_ws releases the claim.  
 constexpr int kTailUnits = 256;
 constexpr size_t kTailWsBytes = (size_t)kTailUnits * BM * BN * 4 + kTailUnits * 4;
 static void* g_tail_ws[16] = {};
+static hipStream_t g_tail_owner[16] = {};
+static bool g_tail_claimed[16] = {};
+static long g_tail_foreign[16] = {};  // launches that skipped the tail (another stream owns it)
 
 // (tail tiles r, split S) for T tiles of nt K-tiles on 256 CUs: the last partial
 // wave's r tiles in r x S units (S in {4, 2}: r S <= 256, nt % (2 S) == 0, >= 8 K-tiles each).
@@ -610,9 +618,17 @@ static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M
   if (splits == 1) {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16 && g_tail_ws[dev]) {
-      tail_plan(T, K / BK, tr, ts);
-      tws = (float*)g_tail_ws[dev];
-      tick = (int*)((char*)g_tail_ws[dev] + (size_t)kTailUnits * BM * BN * 4);
+      if (!g_tail_claimed[dev]) {
+        g_tail_claimed[dev] = true;
+        g_tail_owner[dev] = s;
+      }
+      if (g_tail_owner[dev] != s) {
+        ++g_tail_foreign[dev];
+      } else {
+        tail_plan(T, K / BK, tr, ts);
+        tws = (float*)g_tail_ws[dev];
+        tick = (int*)((char*)g_tail_ws[dev] + (size_t)kTailUnits * BM * BN * 4);
+      }
     }
   }
   const int grid = splits > 1 ? T * splits : T - tr + tr * ts;
@@ -694,7 +710,15 @@ K8S_API int k8s_gemm_big_set_ws(void* ws) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return (int)hipErrorInvalidValue;
   k8s::big::g_tail_ws[dev] = ws;
+  k8s::big::g_tail_claimed[dev] = false;  // the next launch that uses it claims it for its stream
   return 0;
+}
+// launches on this device that ran without the split tail because another
+// stream owns the workspace (test / diagnostics)
+K8S_API long k8s_gemm_big_tail_foreign() {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return -1;
+  return k8s::big::g_tail_foreign[dev];
 }
 
 // mode 0: y[M][N] = x . w^T (w [N][K], N % 256 == 0);

@@ -291,6 +291,7 @@ class LLMEngine:
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
+                      "prefill_attn_pairs": 0, "small_steps": 0, "small_rows": 0, "big_rows": 0,
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
                       "prefix_hit_tokens": 0, "prefill_deferred_steps": 0, "preemptions": 0, "cancelled": 0,
@@ -719,11 +720,19 @@ class LLMEngine:
             for s, _ in chunks:  # publish the pages this prefill completed (their KV write is enqueued)
                 self._register_blocks(s)
         self.stats["steps"] += 1
+        n_rows = len(drows) + sum(q for _, q in big)
+        if n_rows <= 256:  # decode-size step: the projections stream every weight once (M <= 256 kernels)
+            self.stats["small_steps"] += 1
+            self.stats["small_rows"] += n_rows
+        else:
+            self.stats["big_rows"] += n_rows
         self.stats["prefill_tokens"] += sum(q for _, q in chunks)
         self.stats["tiny_chunk_tokens"] += len(drows) - len(decode)
         self.stats["decode_tokens"] += len(decode)
         self.stats["decode_ctx_tokens"] += sum(s.n_cached for s in decode)
         self.stats["prefill_ctx_tokens"] += sum(s.n_cached * q for s, q in chunks)
+        # (query, key) pairs the prefill attention computes: the cached keys plus the causal chunk
+        self.stats["prefill_attn_pairs"] += sum((s.n_cached - q) * q + q * (q + 1) // 2 for s, q in chunks)
         if infl is not None:
             # host side of the previous step, overlapped with this step's forward
             toks = self._process_tokens(infl, placeholders=True)
@@ -1125,12 +1134,11 @@ class LLMEngine:
             comm = SMP.sample(logits, temps, seeds, steps, mask_id, table, list_off, list_len, lists, self.vocab,
                               vocab_off=off, pairs=True).to(cdev)
         g = self._all_gather(comm)
-        tok = SMP.combine_pairs(g[:, :, :2].contiguous())
         if cand_h.any():
-            sel = self._h2d(cand_h, g.device)
-            ct = SMP.combine_candidates(g[:, :, 2:].reshape(self.pc.tp_size, B, -1, 3), topk.to(g.device),
-                                        topp.to(g.device))
-            tok = torch.where(sel, ct, tok)
+            tok = SMP.combine_shards(g[:, :, :2].contiguous(), g[:, :, 2:].reshape(self.pc.tp_size, B, -1, 3),
+                                     self._h2d(cand_h, g.device), topk.to(g.device), topp.to(g.device))
+        else:
+            tok = SMP.combine_pairs(g[:, :, :2].contiguous())
         tok = tok.to(self.device)
         if full_h.size:
             tok[self._h2d(full_h.astype(np.int64), self.device)] = self._sample_gathered(
@@ -1144,11 +1152,9 @@ class LLMEngine:
         the same tokens)."""
         import torch.distributed as dist
         idx = self._h2d(rows_h.astype(np.int64), self.device)
-        cdev = self._comm_device()
-        shard = logits.index_select(0, idx).float().contiguous().to(cdev)
-        parts = [torch.empty_like(shard) for _ in range(self.pc.tp_size)]
-        dist.all_gather(parts, shard, group=self.pc.tp_group)
-        full = torch.cat(parts, 1).to(self.device)  # rank r holds columns [r * vocab_local, ...)
+        shard = logits.index_select(0, idx).float().contiguous().to(self._gather_device())
+        g = self._all_gather(shard)                         # [tp, rows, vocab_local]
+        full = torch.cat(list(g.unbind(0)), 1).to(self.device)  # rank r holds columns [r * vocab_local, ...)
 
         def pick(t):
             return t.index_select(0, idx)
@@ -1175,8 +1181,7 @@ class LLMEngine:
         """[tp, *comm.shape]: every TP rank's ``comm``."""
         import torch.distributed as dist
         car = self.pc.custom_ar
-        if car is not None and comm.is_cuda and car.a2a_fits(self.pc.tp_size * (-(-comm.numel() * comm.element_size()
-                                                                                   // 16) * 16)):
+        if car is not None and comm.is_cuda:  # device-side xGMI all-gather, any size (buffer-sized pieces)
             return car.all_gather(comm)
         parts = [torch.empty_like(comm) for _ in range(self.pc.tp_size)]
         dist.all_gather(parts, comm, group=self.pc.tp_group)

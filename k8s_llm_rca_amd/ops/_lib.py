@@ -68,6 +68,7 @@ _SIGS = {
     "k8s_substr_search": [P, P, P, I, P, I, P, P, P],
     "k8s_graph_expand2": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],
+    "k8s_window_mark": [I, P],
     "k8s_walks": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P],
 }
 

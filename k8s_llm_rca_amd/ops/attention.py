@@ -451,13 +451,7 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
     else:
         # enough tiles to fill the chip (two 4-wave workgroups per CU): no split
         part = max(pages) if pages and enough else max(4, -(-total * nkv // target_wgs))
-    if max_part is not None:
-        part = min(part, max_part)
-    while sum(-(-p // part) for p in pages if p > part) > max_slots:
-        if max_part is not None and part * 2 > max_part:
-            raise ValueError(f"prefill plan needs more than {max_slots} split-KV slots at "
-                             f"{max_part} pages per item (context too long for the workspace)")
-        part *= 2
+    part = _fit_slots(pages, part, max_part, max_slots)
     items = []
     slot = 0
     for (end, s, t, n), p in zip(tiles, pages):
@@ -482,6 +476,21 @@ def plan_prefill(q_start_host: list, G: int, block_size: int = 64, ctx_lens_host
 
 _PART_CANDIDATES = (4, 5, 6, 7, 8, 10, 12, 14, 16, 20, 24, 28, 32, 40, 48, 56, 64, 80, 96, 128, 160, 192, 256, 384,
                     512, 768, 1024)
+
+
+def _fit_slots(pages: List[int], part: int, max_part: Optional[int], max_slots: int) -> int:
+    """Grow ``part`` (pages per split item) until the split tiles need at most
+    ``max_slots`` partial-result slots.  ``part`` need not be a power of two
+    (makespan candidates such as 384 / 768), so the doubling is clamped at
+    ``max_part``; only ``max_part`` itself overflowing is an error."""
+    if max_part is not None:
+        part = min(part, max_part)
+    while sum(-(-p // part) for p in pages if p > part) > max_slots:
+        if max_part is not None and part >= max_part:
+            raise ValueError(f"prefill plan needs more than {max_slots} split-KV slots at "
+                             f"{max_part} pages per item (context too long for the workspace)")
+        part = part * 2 if max_part is None else min(part * 2, max_part)
+    return part
 
 
 def _makespan_part(pages: List[int], nkv: int, overhead: float, max_part: Optional[int], max_slots: int,

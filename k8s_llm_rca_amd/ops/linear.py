@@ -369,8 +369,11 @@ def load_big(path: str) -> int:
     for tag in ("ranges", "silu", "rope"):
         for key, rows in d.get(tag, {}).items():
             N, K = (int(v) for v in key.split(","))
-            _big_ranges[(tag, N, K) if tag != "ranges" else (N, K)] = [
-                (int(r[0]), int(r[1]), int(r[2]) if len(r) > 2 else 1) for r in rows]
+            parsed = [(int(r[0]), int(r[1]), int(r[2]) if len(r) > 2 else 1) for r in rows]
+            if tag != "ranges" and any(s != 1 for _, _, s in parsed):
+                # the SwiGLU / RoPE epilogue forms have no split-K variant
+                raise ValueError(f"{path}: {tag} row for {key} carries splits > 1")
+            _big_ranges[(tag, N, K) if tag != "ranges" else (N, K)] = parsed
             n += len(rows)
     return n
 
@@ -416,7 +419,7 @@ def big_scratch_elems() -> int:
     (the gemm_mid scratch, reserved before any capture)."""
     need = 0
     for key, rows in _big_ranges.items():
-        if key[0] == "silu":
+        if isinstance(key[0], str):  # ("silu" / "rope", N, K): no split-K form (load_big rejects splits > 1)
             continue
         for lo, hi, splits in rows:
             if splits > 1:
@@ -592,9 +595,26 @@ def mid_configs():
     return _mid_cfgs
 
 
+# Split-K partial buffers that were replaced by a larger one.  They are never
+# freed: a HIP graph captured before the growth still writes (and reads back)
+# its partials at the old address on every replay.  Freed, that memory would go
+# back to the caching allocator and be handed to some later tensor -- the
+# grammar mask table, an activation, a sampling input -- which each replay would
+# then overwrite with fp32 partials: silent corruption of every request that
+# tensor serves, for the rest of the run.  Growth after the engine's up-front
+# reservation is rare (reserve_dispatch_scratch sizes it for the whole table);
+# keeping the old buffer costs its bytes once.
+_retired_scratch: List[torch.Tensor] = []
+scratch_growths = 0
+
+
 def _scratch(dev: torch.device, n: int) -> torch.Tensor:
+    global scratch_growths
     t = _mid_scratch.get(dev)
     if t is None or t.numel() < n:
+        if t is not None:
+            _retired_scratch.append(t)
+            scratch_growths += 1
         t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
         _mid_scratch[dev] = t
     return t

@@ -133,6 +133,9 @@ _scratch = {}
 def _split_scratch(dev: torch.device, n: int) -> torch.Tensor:
     t = _scratch.get(dev)
     if t is None or t.numel() < n:
+        if t is not None:  # never freed: graphs captured earlier replay at its address (ops/linear.py _scratch)
+            from . import linear as LIN
+            LIN._retired_scratch.append(t)
         t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
         _scratch[dev] = t
     return t

@@ -112,6 +112,21 @@ def combine_candidates(cands: torch.Tensor, top_k: torch.Tensor, top_p: torch.Te
     return first.to(torch.int32)
 
 
+def combine_shards(pairs: torch.Tensor, cands: Optional[torch.Tensor], cand_rows: Optional[torch.Tensor],
+                   top_k: Optional[torch.Tensor], top_p: Optional[torch.Tensor]) -> torch.Tensor:
+    """The TP sampler's combine (``LLMEngine._sample_shard``): [tp, B, 2]
+    winners -> [B] tokens, and for the ``cand_rows`` (bool [B]: top-k rows with
+    ``k <= CAND_K``) the exact top-k / top-p pick from the [tp, B, C, 3]
+    candidates.  A row that any shard flagged ``NON_FINITE`` keeps the flag:
+    its candidates come from the same poisoned logits (NaN fails every
+    comparison), so they would hand back a token picked from garbage."""
+    tok = combine_pairs(pairs)
+    if cands is None:
+        return tok
+    ct = combine_candidates(cands, top_k, top_p)
+    return torch.where(cand_rows & (tok != NON_FINITE), ct, tok)
+
+
 def _mix32(x: torch.Tensor) -> torch.Tensor:
     M = 0xFFFFFFFF
     x = x & M

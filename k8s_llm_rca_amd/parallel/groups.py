@@ -28,16 +28,26 @@ class ParallelContext:
     custom_ar: Optional[object] = None    # parallel.xgmi.XgmiAllReduce for small TP messages
     ar_chunks: int = 4                    # GEMM / all-reduce pipeline depth (linear_all_reduce)
     overlap_min_bytes: int = 256 << 10    # below this an all-reduce is latency-bound: no chunking
+    # every TP / EP data collective on the xGMI kernels (larger-than-buffer
+    # messages in buffer-sized chunks): no RCCL call on the data path.  Required
+    # when ranks share one GPU (RCCL refuses duplicate devices), and the mode a
+    # TP group runs in whenever its communicator is up (attach_custom_allreduce)
+    xgmi_only: bool = False
 
     @property
     def is_tp(self) -> bool:
         return self.tp_size > 1
 
+    def _xgmi(self, t: torch.Tensor) -> bool:
+        car = self.custom_ar
+        return car is not None and t.is_cuda and (car.mode_for(t) != 0 or (self.xgmi_only and car.eligible(t)))
+
     def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
         if self.tp_size > 1:
-            car = self.custom_ar
-            if car is not None and car.mode_for(t):
-                return car(t)
+            if self._xgmi(t):
+                return self.custom_ar(t)
+            if self.xgmi_only and t.is_cuda:
+                raise ValueError(f"xgmi_only: a {t.dtype} all-reduce of shape {tuple(t.shape)} has no xGMI path")
             dist.all_reduce(t, group=self.tp_group)
         return t
 
@@ -46,7 +56,7 @@ class ParallelContext:
         stream; returns a handle whose ``wait()`` orders the compute stream
         after it."""
         car = self.custom_ar
-        if car is not None and t.is_cuda and car.mode_for(t):
+        if self._xgmi(t):
             cur = torch.cuda.current_stream(t.device)
             if self.comm_stream is None:
                 self.comm_stream = torch.cuda.Stream(t.device)
@@ -103,6 +113,10 @@ class ParallelContext:
         """[n, v_local] on every rank -> [n, v_local * tp] (rank-major)."""
         if self.tp_size == 1:
             return t
+        car = self.custom_ar
+        if car is not None and t.is_cuda:  # device-side, any size (buffer-sized pieces)
+            g = car.all_gather(t)                                   # [tp, n, v_local]
+            return g.permute(1, 0, *range(2, g.dim())).reshape(*t.shape[:-1], -1)
         parts = [torch.empty_like(t) for _ in range(self.tp_size)]
         dist.all_gather(parts, t.contiguous(), group=self.tp_group)
         return torch.cat(parts, dim=-1)
@@ -128,18 +142,36 @@ def init_distributed(backend: Optional[str] = None) -> ParallelContext:
     return pc
 
 
-def attach_custom_allreduce(pc: ParallelContext) -> ParallelContext:
-    """Give a GPU TP context the xGMI one/two-shot all-reduce for small
-    messages (``K8S_RCA_CUSTOM_AR=0`` keeps every all-reduce on RCCL)."""
-    if (pc.tp_size > 1 and torch.cuda.is_available() and os.environ.get("K8S_RCA_CUSTOM_AR", "1") != "0"
-            and dist.get_backend(pc.tp_group) == "nccl"):
+# grid cap of the xGMI collectives when the TP ranks share one GPU
+SHARED_GPU_AR_BLOCKS = 32
+
+
+def attach_custom_allreduce(pc: ParallelContext, same_gpu: bool = False) -> ParallelContext:
+    """Give a GPU TP context the xGMI communicator (``parallel/xgmi.py``):
+    one-/two-shot all-reduce, fused all-reduce + add + RMSNorm, all-to-all and
+    all-gather over hipIpc-mapped peer buffers, every data collective on it
+    (``xgmi_only``).  ``K8S_RCA_CUSTOM_AR=0`` keeps every collective on RCCL.
+    ``same_gpu``: the ranks share one device over a gloo group (the one-GPU
+    rehearsal of a TP deployment: RCCL refuses duplicate devices, so the xGMI
+    kernels are the only data path and a failure to map them is fatal)."""
+    if pc.tp_size > 1 and torch.cuda.is_available() and os.environ.get("K8S_RCA_CUSTOM_AR", "1") != "0":
+        from .xgmi import XgmiAllReduce
+        # 64 MiB: every TP all-reduce up to 4,096 tokens of 70B (8,192 x bf16) in one xGMI
+        # two-shot, which reads the N-1 peers over N-1 links at once; larger ones in
+        # 64 MiB chunks (640 MiB of uncached HBM a rank)
+        mb = int(os.environ.get("K8S_RCA_AR_MAX_MB", "64"))
+        nccl = dist.get_backend(pc.tp_group) == "nccl"
+        if not nccl and not same_gpu:
+            return pc  # a gloo group on separate devices (CPU-side tests): the dist.* collectives
         try:
-            from .xgmi import XgmiAllReduce
-            # 64 MiB: every TP all-reduce up to 4,096 tokens of 70B (8,192 x bf16) stays on the
-            # xGMI two-shot, which reads the N-1 peers over N-1 links at once (512 MiB of HBM a rank)
-            mb = int(os.environ.get("K8S_RCA_AR_MAX_MB", "64"))
-            pc.custom_ar = XgmiAllReduce(pc.tp_group, max_bytes=mb << 20)
-        except Exception as e:  # noqa: BLE001 - RCCL remains correct, only slower for small messages
+            # ranks sharing one GPU: cap the collectives' grids so a rank's blocks spinning for
+            # its peer never hold every CU its peer's next kernel needs (XgmiAllReduce max_blocks)
+            pc.custom_ar = XgmiAllReduce(pc.tp_group, max_bytes=mb << 20, timeout_s=60.0 if same_gpu else 10.0,
+                                         max_blocks=SHARED_GPU_AR_BLOCKS if same_gpu else None)
+            pc.xgmi_only = True
+        except Exception as e:  # noqa: BLE001
+            if same_gpu:
+                raise  # RCCL cannot run two ranks on one device: nothing to fall back to
             import logging
             logging.getLogger(__name__).warning("xGMI all-reduce unavailable (%s); using RCCL", e)
     return pc

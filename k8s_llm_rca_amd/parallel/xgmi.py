@@ -113,13 +113,40 @@ class XgmiAllReduce:
         dist.barrier(group=group)
 
     def mode_for(self, t: torch.Tensor) -> int:
-        """1 one-shot, 2 two-shot, 0 = not applicable (use RCCL)."""
+        """1 one-shot, 2 two-shot, 0 = not applicable in one call (RCCL, or
+        :meth:`__call__`'s chunked form when :meth:`eligible`)."""
         nb = t.numel() * t.element_size()
-        if t.dtype != torch.bfloat16 or not t.is_contiguous() or t.numel() % 8 or nb > self.max_bytes:
+        if not self.eligible(t) or nb > self.max_bytes:
             return 0
         return 1 if nb <= ONE_SHOT_MAX else 2
 
+    @staticmethod
+    def eligible(t: torch.Tensor) -> bool:
+        """Any size: a larger tensor is reduced in buffer-sized chunks."""
+        return t.dtype == torch.bfloat16 and t.is_contiguous() and t.numel() % 8 == 0
+
+    def chunk_elems(self) -> int:
+        """Elements per chunk of a larger-than-buffer all-reduce: the buffer's
+        capacity, whole 8 x world-element units (the two-shot's slice unit)."""
+        unit = 8 * self.world
+        return (self.max_bytes // 2) // unit * unit
+
     def __call__(self, t: torch.Tensor, mode: Optional[int] = None) -> torch.Tensor:
+        """In-place sum over the group.  Tensors larger than the buffer (the
+        prefill-size TP all-reduces: 70B at 8,192 tokens is 128 MiB) run as
+        consecutive two-shot calls over buffer-sized chunks on the same stream
+        -- each chunk reads the N-1 peers over N-1 links at once, so the whole
+        TP data path stays on the xGMI kernels (no RCCL call)."""
+        nb = t.numel() * t.element_size()
+        if nb > self.max_bytes and mode is None and self.eligible(t):
+            flat = t.view(-1)
+            step = self.chunk_elems()
+            for a in range(0, flat.numel(), step):
+                c = flat[a:a + step]
+                _check(self.L.k8s_ar_allreduce_bf16(self.id, c.data_ptr(), c.data_ptr(), c.numel(),
+                                                    1 if c.numel() * 2 <= ONE_SHOT_MAX else 2, stream_ptr(t)),
+                       "k8s_ar_allreduce_bf16")
+            return t
         m = self.mode_for(t) if mode is None else mode
         if m == 0:
             raise ValueError("tensor not eligible for the xGMI all-reduce")
@@ -166,17 +193,25 @@ class XgmiAllReduce:
         """[world, *x.shape] = every rank's ``x`` (any dtype: the bytes are
         moved as bf16 pairs through :meth:`all_to_all` with the row replicated
         for every destination).  Device-side, no host sync: the TP sampler's
-        winners / candidates travel this way (``LLMEngine._sample_shard``)."""
+        winners / candidates travel this way (``LLMEngine._sample_shard``).
+        Larger than the buffer: consecutive buffer-sized pieces."""
         flat = x.contiguous().view(-1).view(torch.uint8)
         nb = flat.numel()
-        pad = (-nb) % 16
+        pad = (-nb) % (16 * self.world)
         if pad:
             flat = torch.cat([flat, flat.new_zeros(pad)])
         row = flat.view(torch.bfloat16)
-        send = row.unsqueeze(0).expand(self.world, -1).contiguous()
-        recv = torch.empty_like(send)
-        self.all_to_all(send, recv)
-        out = recv.view(torch.uint8)[:, :nb].contiguous()
+        n = row.numel()
+        # bf16 elements per piece: the a2a moves world x piece, within 2 x max_bytes
+        step = max(8, (self.max_bytes // self.world) // 8 * 8)
+        out = torch.empty(self.world, n, dtype=torch.bfloat16, device=x.device)
+        for a in range(0, n, step):
+            piece = row[a:a + step]
+            send = piece.unsqueeze(0).expand(self.world, -1).contiguous()
+            recv = torch.empty_like(send)
+            self.all_to_all(send, recv)
+            out[:, a:a + piece.numel()] = recv
+        out = out.view(torch.uint8)[:, :nb].contiguous()
         return out.view(x.dtype).view(self.world, *x.shape)
 
     def status_async(self, host: torch.Tensor) -> None:

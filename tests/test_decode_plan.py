@@ -1,4 +1,5 @@
 """Decode work-list planning on the host (no GPU): multi-token items."""
+import pytest
 import numpy as np
 
 from k8s_llm_rca_amd.ops import attention as A
@@ -115,3 +116,15 @@ def test_prefill_makespan_planner_covers_keys_and_balances(monkeypatch):
     monkeypatch.setattr(A, "PF_OVERHEAD_PAGES", 8.0)
     monkeypatch.setattr(A, "PF_MAKESPAN_ALL", False)
     assert A.plan_prefill([0, 8192], 4, 64, [8192], nkv=8).n_merge == 0
+
+
+def test_fit_slots_clamps_non_power_of_two_part():
+    """a makespan part such as 768 must clamp its doubling at
+    max_part (1024) instead of jumping to 1536 and failing a plan that fits."""
+    from k8s_llm_rca_amd.ops import attention as A
+    pages = [1024 * 3] * 4                   # 12 slots at part 1024, 16 at 768
+    assert A._fit_slots(pages, 768, 1024, 12) == 1024
+    assert A._fit_slots(pages, 384, 1024, 12) == 1024
+    assert A._fit_slots(pages, 256, None, 12) == 1024
+    with pytest.raises(ValueError):
+        A._fit_slots(pages, 768, 1024, 11)   # max_part itself overflows

@@ -962,6 +962,42 @@ def test_gemm_big_split_tail(M, N, K, silu, var, monkeypatch):
     torch.testing.assert_close(y1.float(), y0.float(), atol=2e-2, rtol=2e-2)
 
 
+def test_gemm_big_split_tail_owned_by_one_stream():
+    """the split-tail workspace belongs to the stream that first
+    used it; gemm_big on another stream runs without the tail (whole tiles)
+    instead of sharing partials / tickets, and both streams' results are
+    right -- also when the two launches are in flight at once."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops._lib import lib
+    M, N, K = 6144, 4096, 1024      # 384 tiles: a 128-tile tail split 2 ways
+    torch.manual_seed(3)
+    x = torch.randn(M, K, device=dev).bfloat16()
+    w = (torch.randn(N, K, device=dev) * 0.03).bfloat16()
+    LIN.reserve_big_ws(dev, enable=True)  # (re)registers: the next launch claims it
+    try:
+        y_main = LIN.gemm_big(x, w)       # claims the workspace for the current stream
+        f0 = lib().k8s_gemm_big_tail_foreign()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        ys = []
+        with torch.cuda.stream(side):
+            for _ in range(3):
+                ys.append(LIN.gemm_big(x, w))
+        for _ in range(3):                # concurrently on the owner stream
+            ys.append(LIN.gemm_big(x, w))
+        torch.cuda.current_stream(dev).wait_stream(side)
+        torch.cuda.synchronize()
+        assert lib().k8s_gemm_big_tail_foreign() - f0 == 3
+        y_after = LIN.gemm_big(x, w)      # tickets intact: the owner's tail still sums right
+    finally:
+        LIN.reserve_big_ws(dev)
+    ref = x.float() @ w.float().t()
+    for y in [y_main, y_after] + ys:
+        torch.testing.assert_close(y.float(), ref, atol=3e-2, rtol=3e-2)
+    assert torch.equal(y_main, y_after) and all(torch.equal(y_main, y) for y in ys[3:])
+
+
 @pytest.mark.parametrize("pipe", [1, 5])
 @pytest.mark.parametrize("M,I,K", [(5, 128, 128), (300, 384, 512), (1500, 1024, 4096), (4100, 14336, 256)])
 def test_gemm_big_silu_epilogue(M, I, K, pipe):

@@ -128,6 +128,36 @@ def test_sampler_flags_nonfinite_rows_reference():
     assert SMP.combine_pairs(torch.stack([pairs, pairs])).tolist()[:3] == [SMP.NON_FINITE] * 3
 
 
+@pytest.mark.parametrize("tp", [2, 4])
+def test_tp_candidates_keep_nonfinite_flag(tp):
+    """under TP a top-k row whose logits are NaN in ONE
+    shard must come out of the combine as NON_FINITE -- the candidates path
+    must not replace the flag with a token picked from the poisoned logits."""
+    B, V = 4, 2048
+    torch.manual_seed(9)
+    logits = torch.randn(B, V)
+    vl = V // tp
+    logits[1, vl + 5] = float("nan")   # row 1: NaN in shard 1 only, a top-k row
+    logits[2, 7] = float("inf")        # row 2: +inf in shard 0, a top-k row
+    a = _args(B, [0.8, 0.8, 0.8, 0.8], [8, 8, 16, 0], [1.0, 0.9, 1.0, 1.0])
+    pairs, cands = [], []
+    for r in range(tp):
+        o, c = SMP.sample(logits[:, r * vl:(r + 1) * vl].contiguous(), a["temperature"], a["seeds"], a["steps"],
+                          a["mask_id"], None, a["list_off"], a["list_len"], a["lists"], V, vocab_off=r * vl,
+                          pairs=True, top_k=a["top_k"], top_p=a["top_p"], candidates=True)
+        pairs.append(o)
+        cands.append(c)
+    sel = (a["top_k"] > 0) & (a["top_k"] <= SMP.CAND_K)
+    got = SMP.combine_shards(torch.stack(pairs), torch.stack(cands), sel, a["top_k"], a["top_p"])
+    assert got[1].item() == SMP.NON_FINITE and got[2].item() == SMP.NON_FINITE
+    assert got[0].item() >= 0 and got[3].item() >= 0
+    # the healthy rows equal the single-device pick
+    full = torch.empty(B, dtype=torch.int32)
+    SMP._sample_ref(logits, a["temperature"], a["seeds"], a["steps"], a["mask_id"], None, a["list_off"],
+                    a["list_len"], a["lists"], V, full, top_k=a["top_k"], top_p=a["top_p"])
+    assert got[0] == full[0] and got[3] == full[3]
+
+
 @pytest.mark.gpu
 def test_sampler_flags_nonfinite_rows_kernel():
     if not torch.cuda.is_available():

@@ -15,12 +15,12 @@ CATS = [
     ("attn_prefill", r"attn_prefill"),
     ("gemm_hipblaslt", r"^(Custom_)?Cijk"),
     ("gemm_big", r"gemm_big|big_reduce"),  # hand-written 256x256 prefill GEMM (+ fused epilogues)
-    ("gemm_skinny", r"gemm_skinny|gemm_mid"),
-    ("gemm_grouped", r"grouped_gemm|grouped_reduce"),  # MoE experts, and split-K dense GEMMs (dispatch 'grp')
+    ("gemm_decode", r"gemm_skinny|gemm_mid|gemm_glds|gemm_stream"),  # M <= 256 weight-streaming kernels
+    ("gemm_grouped", r"grouped_gemm|grouped_glds|grouped_reduce"),  # MoE experts, and split-K dense GEMMs (dispatch 'grp')
     ("moe", r"moe"),
     ("norm_rope_act", r"rmsnorm|rope|silu|layernorm|relu"),
     ("sampling", r"sample|gumbel|argmax"),
-    ("allreduce", r"allreduce|ncclDevKernel|rccl"),
+    ("allreduce", r"allreduce|\bar_kernel|ar_addnorm|a2a_kernel|ncclDevKernel|rccl"),
     ("graph", r"graph|csr|contains|walk|expand"),
 ]
 

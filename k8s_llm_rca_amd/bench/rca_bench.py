@@ -29,6 +29,8 @@ from typing import Any, Dict, List, Optional
 
 import torch
 
+from ..knobs import KNOBS
+
 METRIC = "RCA analyses/sec + p50 end-to-end latency, Llama-3-8B backend, 10k-node graph"
 # The thread-truncation contract is part of the workload definition: the
 # reference's threads grow for the whole batch (test_with_file.py:28-38) and its
@@ -235,7 +237,7 @@ def run(args) -> Optional[Dict[str, Any]]:
     # staging): an intra-op pool of OMP_NUM_THREADS spinning workers only competes
     # with the engine thread for the rank's CPU share.  K8SRCA_TORCH_THREADS=N
     # sets the pool size (unset: torch's default).
-    nthr = os.environ.get("K8SRCA_TORCH_THREADS")
+    nthr = KNOBS.torch_threads
     if nthr:
         torch.set_num_threads(int(nthr))
     if cuda:
@@ -494,6 +496,11 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "host_s": round(d["host_s"], 3), "evictions": d["evictions"],
                    "preemptions": d.get("preemptions", 0), "requests": d["requests"],
                    "nonfinite_rows": d.get("nonfinite_rows", 0),
+                   # knob nonfinite_check: steps whose layer flags fired, and the first layer seen
+                   "nonfinite_flag_steps": d.get("nonfinite_flag_steps", 0),
+                   "nonfinite_first_layer": eng.stats.get("nonfinite_first_layer", -1),
+                   # why the window's requests ended (a collapse to early ends shows here)
+                   "ends": {k[4:]: d.get(k, 0) for k in ("end_grammar", "end_eos", "end_no_allowed", "end_cap")},
                    "decode_ctx_tokens": d["decode_ctx_tokens"], "prefill_ctx_tokens": d["prefill_ctx_tokens"],
                    # work counters of tools/window_summary.py's roofline accounting
                    "prefill_attn_pairs": d["prefill_attn_pairs"], "small_steps": d["small_steps"],
@@ -509,7 +516,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                    # measured GEMM tables in use (decode dispatch; hipBLASLt solution buckets registered)
                    "gemm_dispatch": bool(getattr(eng, "gemm_dispatch", False)),
                    "blaslt_buckets": int(getattr(eng, "lib_algos", 0) or 0),
-                   # K8S_RCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
+                   # K8SRCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
                    **({k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}
                       if d["eager_gpu_s"] or d["graph_gpu_s"] else {})},
         # the work behind each timed analysis (sampling varies it run to run by a few %:
@@ -581,7 +588,7 @@ def parser() -> argparse.ArgumentParser:
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
     p.add_argument("--max-batch-tokens", type=int,
-                   default=int(os.environ.get("K8SRCA_MAX_BATCH_TOKENS", "8192")))
+                   default=KNOBS.max_batch_tokens)
     p.add_argument("--temperature", type=float, default=0.7)
     p.add_argument("--semantic-tokens", type=int, default=192)
     p.add_argument("--explanation-tokens", type=int, default=40)

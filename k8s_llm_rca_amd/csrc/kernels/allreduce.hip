@@ -37,6 +37,7 @@
 #include <cstring>
 
 #include "common.h"
+#include "knobs.h"
 
 namespace k8s {
 
@@ -72,11 +73,8 @@ struct ARCtx {
 
 static ARCtx g_ctx[16];
 
-// K8SRCA_AR_FENCE_ALL=1: the old publish (a system fence in every wave), for A/B
-static int fence_all() {
-  const char* e = std::getenv("K8SRCA_AR_FENCE_ALL");  // per launch: A/B-able in one process
-  return (e && e[0] == '1') ? 1 : 0;
-}
+// knob ar_fence_all: the old publish (a system fence in every wave), for A/B (per launch)
+static int fence_all() { return knob(kKnobArFenceAll) ? 1 : 0; }
 
 // Publish this block's stores, then raise its flag in every rank's buffer.
 // Every storing wave drains its own stores (vmcnt(0)) before the barrier; ONE

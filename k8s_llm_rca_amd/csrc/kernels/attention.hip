@@ -29,6 +29,7 @@
 #include <utility>
 
 #include "common.h"
+#include "knobs.h"
 
 namespace k8s {
 
@@ -1282,18 +1283,12 @@ __global__ void __launch_bounds__(256) attn_prefill_merge16_kernel(AttnArgs a) {
 }
 
 // the decode split-KV reduce's prefetch form for rows of <= kRedPre partitions (default;
-// K8SRCA_DECODE_REDUCE_PRE=0: the LDS form everywhere, A/B, read per launch).  Bit-identical;
+// knob decode_reduce_pre=0: the LDS form everywhere, A/B, read per launch).  Bit-identical;
 // 8.5 -> 6.4 us per call on the steady-state decode replay (profiles/r4/reduce_pre/)
-static bool decode_reduce_pre() {
-  const char* e = std::getenv("K8SRCA_DECODE_REDUCE_PRE");
-  return !(e && e[0] == '0');
-}
+static bool decode_reduce_pre() { return knob(kKnobDecodeReducePre) != 0; }
 
-// K8SRCA_PF_MERGE16=0: the 2-dims-per-lane merge for bf16 partials too (A/B, read per launch)
-static bool pf_merge16() {
-  const char* e = std::getenv("K8SRCA_PF_MERGE16");
-  return !(e && e[0] == '0');
-}
+// knob pf_merge16=0: the 2-dims-per-lane merge for bf16 partials too (A/B, read per launch)
+static bool pf_merge16() { return knob(kKnobPfMerge16) != 0; }
 
 }  // namespace k8s
 
@@ -1354,9 +1349,8 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
 // one process): 6 = 711 / 5 = 684 TFLOP/s; earlier pairs 5 = 649 / 4 = 624 / 2 = 628
 // and 4 = 669 / 2 = 648, pg64 633 (r3: static priority 651, staggered late waves 608).
 static int prefill_w8() {
-  const char* v = std::getenv("K8SRCA_PF_W8");
-  if (!v || !v[0] || v[0] == '1') return 6;
-  return v[0] - '0';
+  const int v = knob(kKnobPfW8);
+  return v == 1 ? 6 : v;
 }
 
 K8S_API int k8s_attn_prefill(const void* q, int q_stride, const void* kc, const void* vc, const int* block_tables,

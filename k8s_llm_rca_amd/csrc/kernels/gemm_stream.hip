@@ -26,6 +26,7 @@
 #include <cstdlib>
 
 #include "common.h"
+#include "knobs.h"
 
 namespace k8s {
 
@@ -530,14 +531,11 @@ __global__ void __launch_bounds__(256) gemm_stream_reduce_push_kernel(const floa
   push_publish(P, e, strip, n0);
 }
 
-// the hand-issued LDS reads of glds_strip (default; K8SRCA_GLDS_HAND=0: hipcc's
+// the hand-issued LDS reads of glds_strip (default; knob glds_hand=0: hipcc's
 // own reads, A/B, read per launch).  Bit-identical; 0-5 % faster per projection
 // at M = 64-192 (tools/glds_hand_ab.py, profiles/r4/glds_hand/): the decode GEMMs
 // are bound by their DMA stream more than by the exposed LDS latency.
-static bool glds_hand() {
-  const char* e = std::getenv("K8SRCA_GLDS_HAND");
-  return !(e && e[0] == '0');
-}
+static bool glds_hand() { return knob(kKnobGldsHand) != 0; }
 
 // push != nullptr: the push-epilogue form (splits == 1, plain output; hand reads)
 template <int MTW, int NB, int NF = 4>

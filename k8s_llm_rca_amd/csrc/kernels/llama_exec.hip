@@ -81,6 +81,7 @@ int k8s_gemm_stream_push(const void* x, int ldx, const void* w, int M, int N, in
                          int ar_id, int mode, hipStream_t s);
 int k8s_ar_push_addnorm_bf16(int id, void* res, const void* w, void* y, int T, int H, float eps, int mode, int S,
                              hipStream_t s);
+int k8s_nonfinite_flag(const void* x, long n, int* flag, hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
@@ -153,6 +154,9 @@ struct K8sLlamaStep {
   // all-reduce slots (k8s_gemm_stream_push) and the fused epilogue waits on
   // per-strip flags (k8s_ar_push_addnorm_bf16): no staging copy
   int ar_push;
+  // debug (knob nonfinite_check): nf_flags[l] = 1 when layer l's normed input
+  // holds a NaN / inf, nf_flags[L] for the last down output; nullptr = off
+  int* nf_flags;
 };
 
 namespace {
@@ -235,6 +239,7 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
                                  s.eps, st));
     else
       K8S_TRY(k8s_rmsnorm(s.prev, s.residual, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    if (s.nf_flags) K8S_TRY(k8s_nonfinite_flag(s.y, n_out, s.nf_flags + l, st));
     // a split-K qkv projection leaves its partials to the RoPE / KV-write kernel,
     // which reduces them first (k8s_splitk_rope_kv: bit-identical, one launch fewer)
     if (deferred(s.sel[0], true)) {
@@ -305,6 +310,7 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
     else if (tp)
       K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.prev, s.prev, n_out, s.ar_mode, st));
   }
+  if (s.nf_flags && !pend) K8S_TRY(k8s_nonfinite_flag(s.prev, n_out, s.nf_flags + s.L, st));
   return (int)hipGetLastError();
 }
 

@@ -342,3 +342,28 @@ K8S_API int k8s_window_mark(int tag, hipStream_t s) {
   hipLaunchKernelGGL(window_mark_kernel, dim3(tag), dim3(64), 0, s, tag);
   return (int)hipGetLastError();
 }
+
+// Debug (knob nonfinite_check): flag[0] = 1 when any of the n bf16 values is
+// NaN or inf (exponent all ones).  The engine passes one flag per layer and
+// reads them with the step's sampled tokens: no host sync of its own.  Every
+// offending lane stores the same 1 (plain vector store).
+__global__ void __launch_bounds__(256) nonfinite_flag_kernel(const uint16_t* __restrict__ x, long n,
+                                                             int* __restrict__ flag) {
+  const long n8 = n / 8;
+  bool bad = false;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n8; i += (long)gridDim.x * 256) {
+    const u16x8 v = *reinterpret_cast<const u16x8*>(x + i * 8);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) bad |= (v[c] & 0x7F80u) == 0x7F80u;
+  }
+  if (blockIdx.x == 0 && threadIdx.x < n - n8 * 8) bad |= (x[n8 * 8 + threadIdx.x] & 0x7F80u) == 0x7F80u;
+  if (bad) flag[0] = 1;
+}
+
+K8S_API int k8s_nonfinite_flag(const void* x, long n, int* flag, hipStream_t s) {
+  if (n <= 0) return 0;
+  if (!x || !flag || ((uintptr_t)x % 16)) return (int)hipErrorInvalidValue;
+  const long blocks = std::min<long>(512, (n / 8 + 255) / 256 + 1);
+  hipLaunchKernelGGL(nonfinite_flag_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint16_t*)x, n, flag);
+  return (int)hipGetLastError();
+}

@@ -39,9 +39,11 @@ from typing import Callable, Dict, List, Optional, Sequence as Seq, Tuple
 import numpy as np
 import torch
 
+from ..knobs import KNOBS
 from ..models.config import ModelConfig, get_config
 from ..ops import attention as A
 from ..ops import sampling as SMP
+from ..ops._lib import scratch
 from ..parallel.groups import ParallelContext, single
 from ..utils import tracing
 from .kv_cache import KVPool, chain_key
@@ -78,15 +80,22 @@ class _LazySample:
 
 class InFlight:
     """A sampled step whose tokens have not been processed on the host yet."""
-    __slots__ = ("seqs", "tok", "tok_host", "event", "t0", "status")
+    __slots__ = ("seqs", "tok", "tok_host", "event", "t0", "status", "nf")
 
-    def __init__(self, seqs, tok, tok_host, event, t0, status=None):
+    def __init__(self, seqs, tok, tok_host, event, t0, status=None, nf=None):
         self.seqs = seqs
         self.tok = tok            # [B] int32 on the device (feeds the next forward)
         self.tok_host = tok_host  # [B] int32 host copy (pinned on GPU), valid once `event` completes
         self.event = event
         self.t0 = t0
         self.status = status      # TP: pinned copy of the xGMI STATUS word, taken before the sampling
+        self.nf = nf              # knob nonfinite_check: pinned copy of the per-layer non-finite flags
+
+
+def _knob(name: str, default):
+    """An EngineConfig default with its knobs.py override (K8SRCA_<NAME>)."""
+    v = getattr(KNOBS, name)
+    return default if v is None else v
 
 
 @dataclass
@@ -111,19 +120,17 @@ class EngineConfig:
     # then 2048 / 0.1 s -> 4.544 / 4.593 vs 4096 / 0.3 s -> 4.606 / 4.601 (p50
     # 28.0 vs 28.1 s, TTFT p50 68 ms either way).
     # 0 disables
-    prefill_min_tokens: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_MIN", "4096")))
+    prefill_min_tokens: int = field(default_factory=lambda: _knob("prefill_min", 4096))
     # ... only while at least this many decode rows run (a busy, throughput-bound
     # engine): at low concurrency a held prompt would only add its wait to the
     # run's latency
-    prefill_defer_min_rows: int = field(default_factory=lambda: int(os.environ.get("K8SRCA_PREFILL_DEFER_ROWS",
-                                                                                   "96")))
-    prefill_max_defer_s: float = field(default_factory=lambda: float(os.environ.get("K8SRCA_PREFILL_DEFER_S",
-                                                                                    "0.3")))
+    prefill_defer_min_rows: int = field(default_factory=lambda: _knob("prefill_defer_rows", 96))
+    prefill_max_defer_s: float = field(default_factory=lambda: _knob("prefill_defer_s", 0.3))
     # prefill chunks of at most this many tokens (grammar jump-forward runs) are
     # run as rows of the decode-attention work list (one row per token, its own
     # causal key count) instead of a prefill tile that walks every page for a
     # few rows and then needs a split-KV merge; 0 disables
-    tiny_chunk_tokens: int = field(default_factory=lambda: int(os.environ.get("K8S_TINY_CHUNK_TOKENS", "8")))
+    tiny_chunk_tokens: int = field(default_factory=lambda: _knob("tiny_chunk_tokens", 8))
     max_context: Optional[int] = None
     use_graphs: bool = True
     # overlap the host's token processing of step n with the GPU's forward of
@@ -282,12 +289,17 @@ class LLMEngine:
         self._async = cfg.async_steps and (self.pc.tp_size == 1 or self._dist_sample or self._sim)
         self._mask_sent = 0      # rank 0: mask-table rows already broadcast to the workers
         self._wmask = None       # TP ranks: device copy of the mask table (rows received so far)
-        # K8S_RCA_SHAPE_TRACE=path: append every step's attention shapes as JSON
+        # knob shape_trace=path: append every step's attention shapes as JSON
         # lines (replayed by tools/bench_kernels.py --what replay)
-        self._shape_trace = os.environ.get("K8S_RCA_SHAPE_TRACE")
-        # K8S_RCA_STEP_TIMING=1: per-path host-issue vs GPU time of the forward
-        self._step_timing = os.environ.get("K8S_RCA_STEP_TIMING") == "1"
+        self._shape_trace = KNOBS.shape_trace
+        # knob step_timing: per-path host-issue vs GPU time of the forward
+        self._step_timing = KNOBS.step_timing
         self._pending_ev: list = []
+        # debug (knob nonfinite_check): per-layer non-finite flags, read with each sampling
+        self._nf = None
+        if KNOBS.nonfinite_check and self.device.type == "cuda" and hasattr(self.model, "nf_flags"):
+            self._nf = torch.zeros(self.mc.n_layers + 1, dtype=torch.int32, device=self.device)
+            self.model.nf_flags = self._nf
         self.stats = {"steps": 0, "decode_steps": 0, "graph_steps": 0, "prefill_tokens": 0, "decode_tokens": 0,
                       "forced_tokens": 0, "sampled_tokens": 0, "forward_s": 0.0, "sample_s": 0.0, "host_s": 0.0,
                       "evictions": 0, "requests": 0, "decode_ctx_tokens": 0, "prefill_ctx_tokens": 0,
@@ -295,7 +307,9 @@ class LLMEngine:
                       "wait_s": 0.0, "post_s": 0.0, "admit_s": 0.0, "captures": 0, "capture_s": 0.0,
                       "eager_issue_s": 0.0, "eager_gpu_s": 0.0, "graph_issue_s": 0.0, "graph_gpu_s": 0.0,
                       "prefix_hit_tokens": 0, "prefill_deferred_steps": 0, "preemptions": 0, "cancelled": 0,
-                      "nonfinite_rows": 0,
+                      "nonfinite_rows": 0, "nonfinite_flag_steps": 0, "nonfinite_first_layer": -1,
+                      # why requests ended: grammar (complete / budget), eos, no allowed token, length cap
+                      "end_grammar": 0, "end_eos": 0, "end_no_allowed": 0, "end_cap": 0,
                       "timeouts": 0,
                       "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
                       "tiny_chunk_tokens": 0}
@@ -411,7 +425,7 @@ class LLMEngine:
         # The engine thread shares the GIL with the callers' pipeline threads;
         # CPython's default 5 ms switch interval can leave the GPU idle while
         # the engine waits to reacquire it after each device sync.
-        si = float(os.environ.get("K8S_RCA_SWITCH_INTERVAL", self.cfg.gil_switch_interval or 0))
+        si = float(KNOBS.switch_interval or self.cfg.gil_switch_interval or 0)
         if si > 0:
             import sys
             sys.setswitchinterval(si)
@@ -428,7 +442,7 @@ class LLMEngine:
             self._thread = None
 
     def _loop(self) -> None:
-        prof_path = os.environ.get("K8S_RCA_PROFILE_ENGINE")
+        prof_path = KNOBS.profile_engine
         if prof_path:  # cProfile of the engine thread only (host turnaround analysis)
             import cProfile
             pr = cProfile.Profile()
@@ -543,10 +557,12 @@ class LLMEngine:
                 continue
             if act == "sample":
                 if len(r.generated) >= r.max_new * 4 + 64:
+                    self.stats["end_cap"] += 1
                     self._finish(r)
                     return
                 r.mask = arg
                 return
+            self.stats["end_grammar"] += 1
             self._finish(r)
             return
 
@@ -1023,10 +1039,9 @@ class LLMEngine:
                                ctx_lens_host=None if ctx_h is None else ctx_h.tolist(),
                                q_start_host=None if qs_h is None else qs_h.tolist())
             if n_parts > 1:
-                dmeta.part_o = torch.empty(n_dec * self.model.nq * n_parts * self.model.D, dtype=torch.float32,
-                                           device=self.device)
-                dmeta.part_ml = torch.empty(n_dec * self.model.nq * n_parts * 2, dtype=torch.float32,
-                                            device=self.device)
+                dmeta.part_o = scratch(n_dec * self.model.nq * n_parts * self.model.D, torch.float32,
+                                       self.device)
+                dmeta.part_ml = scratch(n_dec * self.model.nq * n_parts * 2, torch.float32, self.device)
         if n_pre:
             bt, _ = take(n_pre * maxb_p, (n_pre, maxb_p))
             ctx, ctx_h = take(n_pre)
@@ -1308,8 +1323,8 @@ class LLMEngine:
             "ctx": torch.ones(Bmax, dtype=torch.int32, device=dev),
             "qs": torch.arange(Bmax + 1, dtype=torch.int32, device=dev),
             "sidx": torch.arange(Bmax, dtype=torch.int64, device=dev),
-            "part_o": torch.empty(Bmax * self.model.nq * npmax * self.model.D, dtype=torch.float32, device=dev),
-            "part_ml": torch.empty(Bmax * self.model.nq * npmax * 2, dtype=torch.float32, device=dev),
+            "part_o": scratch(Bmax * self.model.nq * npmax * self.model.D, torch.float32, dev),
+            "part_ml": scratch(Bmax * self.model.nq * npmax * 2, torch.float32, dev),
             "items": torch.zeros(Bmax * npmax, 4, dtype=torch.int32, device=dev),
             "n_items": torch.zeros(2, dtype=torch.int32, device=dev),  # {item count, keys per item}
             # two pinned staging buffers, alternated per graph step; each is
@@ -1526,6 +1541,11 @@ class LLMEngine:
             # once the sampled tokens are (_process_tokens checks it first)
             status = torch.zeros(1, dtype=torch.int32, pin_memory=True)
             car.status_async(status)
+        nf = None
+        if self._nf is not None:  # the flags of every forward since the last sampling
+            nf = torch.empty(self._nf.numel(), dtype=torch.int32, pin_memory=True)
+            nf.copy_(self._nf, non_blocking=True)
+            self._nf.zero_()
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)
@@ -1534,7 +1554,7 @@ class LLMEngine:
         else:
             host, ev = tok, None
         self.stats["sample_s"] += time.perf_counter() - t0
-        return InFlight(seqs, tok, host, ev, t0, status)
+        return InFlight(seqs, tok, host, ev, t0, status, nf)
 
     def _process_tokens(self, fl: InFlight, placeholders: bool = False) -> List[int]:
         """Host side of a sampled step: wait for its tokens (not for later GPU
@@ -1548,6 +1568,13 @@ class LLMEngine:
             from ..parallel.xgmi import CommFault
             raise CommFault("xGMI collective timed out: a TP peer never arrived (allreduce STATUS set)")
         toks = fl.tok_host.tolist()
+        if fl.nf is not None and bool(fl.nf.any()):
+            layer = int(fl.nf.nonzero()[0, 0])
+            self.stats["nonfinite_flag_steps"] += 1
+            if self.stats["nonfinite_first_layer"] < 0:
+                self.stats["nonfinite_first_layer"] = layer
+                log.error("non-finite values in layer %d's normed input (knob nonfinite_check; step %d)", layer,
+                          self.stats["steps"])
         now = time.perf_counter()
         if self._pending_ev:
             self._collect_timing()
@@ -1571,6 +1598,7 @@ class LLMEngine:
                 self._fail_req(r, "non-finite logits (NaN / inf) in this request's row")
                 continue
             if t < 0:  # no allowed token left
+                self.stats["end_no_allowed"] += 1
                 self._finish(r)
                 continue
             r.n_sampled += 1
@@ -1579,6 +1607,7 @@ class LLMEngine:
             if t in self.eos_ids:
                 r.generated.pop()
                 r.gs.advance(t)
+                self.stats["end_eos"] += 1
                 self._finish(r)
                 continue
             s.tokens.append(t)

@@ -9,6 +9,7 @@ containers that never ran ``__graft_entry__.build()``).
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import importlib
 import os
 from typing import List, Optional, Sequence, Tuple
@@ -24,7 +25,7 @@ def core():
     global _core, _tried
     if not _tried:
         _tried = True
-        if os.environ.get("K8SRCA_NO_NATIVE") != "1":
+        if not KNOBS.no_native:
             try:
                 _core = importlib.import_module("k8s_llm_rca_amd._graphcore")
             except ImportError:

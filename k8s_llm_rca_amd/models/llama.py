@@ -28,6 +28,7 @@ import torch.nn.functional as F
 from ..ops import attention as A
 from ..ops import layer_exec as LX
 from ..ops import norm as N
+from ..ops.norm import nonfinite_flag
 from ..ops.linear import linear, linear_f32out, linear_silu, swiglu_gemm
 from ..parallel.groups import ParallelContext, single
 from .config import ModelConfig
@@ -62,6 +63,9 @@ class LlamaModel:
         self.vocab_local = (cfg.vocab_size + tp - 1) // tp
         self.scale = 1.0 / math.sqrt(self.D)
         self._exec = None  # native layer executor (ops/layer_exec.py), bound on first GPU forward
+        # debug (knob nonfinite_check): int32 [n_layers + 1] device flags, set by
+        # ops.norm.nonfinite_flag when a layer's normed input holds NaN / inf
+        self.nf_flags: Optional[torch.Tensor] = None
         self.cos_sin = A.rope_cos_sin(cfg.max_position, cfg.rope_theta, self.D, cfg.scaling_dict(), device=self.device)
         self.layers: List[Dict[str, torch.Tensor]] = []
         self.moe: Optional[MOE.MoELayerSet] = None
@@ -178,6 +182,8 @@ class LlamaModel:
                 N.rmsnorm(residual, L["in_norm"], cfg.rms_eps, out=y)
             else:
                 N.rmsnorm(prev, L["in_norm"], cfg.rms_eps, residual=residual, out=y)
+            if self.nf_flags is not None:
+                nonfinite_flag(y, self.nf_flags[li:li + 1])
             qkv = A.linear_rope_kv(y, L["wqkv"], inp.positions, self.cos_sin, inp.slots, k_cache[li], v_cache[li],
                                    self.nq, self.nkv)
             if inp.meta_decode is not None and nd > 0:
@@ -200,6 +206,8 @@ class LlamaModel:
                     prev = linear_silu(gu, L["w_down"])  # SwiGLU fused into the down GEMM's operand staging
                 else:
                     prev = self.pc.linear_all_reduce(N.silu_mul(gu), L["w_down"], linear_fn=linear)
+        if self.nf_flags is not None:
+            nonfinite_flag(prev, self.nf_flags[len(self.layers):])
         N.rmsnorm(prev, self.final_norm, cfg.rms_eps, residual=residual, out=y)
         sel = y.index_select(0, inp.logits_idx) if inp.logits_idx.numel() != T else y
         logits = self._lm_head(sel)

@@ -11,6 +11,7 @@ on ``E / ep`` ranks and tokens travel by all-to-all (:mod:`..parallel.ep`).
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import os
 
 from typing import List, Optional
@@ -81,8 +82,8 @@ class MoELayerSet:
     # at 64-250 rows (5.2-5.5 TB/s); the down projection measured equal to the
     # split-K grouped kernel and stays there; at 512 rows the grouped kernel wins
     # (tools/bench_kernels.py --what moe_glds, profiles/r2_moe_glds.txt)
-    GLDS_MAX_ROWS = int(os.environ.get("K8S_MOE_GLDS_MAX_ROWS", "384"))  # 0 disables (A/B)
-    BIG_PREFILL = os.environ.get("K8SRCA_MOE_BIG", "1") == "1"  # 0: per-expert hipBLASLt (A/B)
+    GLDS_MAX_ROWS = KNOBS.moe_glds_max_rows  # 0 disables (A/B)
+    BIG_PREFILL = KNOBS.moe_big  # 0: per-expert hipBLASLt (A/B)
     GLDS_UP = (13, 1)
 
     def experts(self, li: int, x_perm: torch.Tensor, offsets: torch.Tensor,

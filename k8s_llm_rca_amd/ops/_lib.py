@@ -15,6 +15,7 @@ import threading
 import torch
 
 from .. import _build
+from ..knobs import KNOBS, push_native
 
 _lib = None
 _lock = threading.Lock()
@@ -69,6 +70,9 @@ _SIGS = {
     "k8s_graph_expand2": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],
     "k8s_window_mark": [I, P],
+    "k8s_set_knob": [I, I],
+    "k8s_nonfinite_flag": [P, ctypes.c_long, P, P],
+    "k8s_get_knob": [I],
     "k8s_walks": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P],
 }
 
@@ -82,9 +86,9 @@ def lib():
         if _lib is None:
             # K8SRCA_HIP_LIB: an alternate build of the same sources (compile-time
             # A/Bs, e.g. tools/_nt_ab.sh); the in-tree library otherwise
-            path = os.environ.get("K8SRCA_HIP_LIB") or _build.hip_lib_path()
+            path = KNOBS.hip_lib or _build.hip_lib_path()
             if not os.path.exists(path):
-                if os.environ.get("K8SRCA_AUTOBUILD", "1") == "1":
+                if KNOBS.autobuild:
                     _build.build_hip()
                 else:
                     raise RuntimeError(f"{path} missing: run __graft_entry__.build()")
@@ -95,6 +99,7 @@ def lib():
                     continue
                 fn.argtypes = args
                 fn.restype = ctypes.c_int
+            push_native(L)
             _lib = L
     return _lib
 
@@ -125,11 +130,22 @@ def ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
 
 
-_SYNC_DEBUG = os.environ.get("K8S_RCA_SYNC_DEBUG") == "1"
+_SYNC_DEBUG = KNOBS.sync_debug
+
+
+def scratch(shape, dtype, device) -> torch.Tensor:
+    """An uninitialised device buffer that kernels must write before they read
+    (split-K / split-KV partials, activations).  Knob ``poison``: filled with
+    NaN instead, so a read of an unwritten element is loud, not stale data."""
+    if isinstance(shape, int):
+        shape = (shape,)
+    if KNOBS.poison and dtype.is_floating_point:
+        return torch.full(shape, float("nan"), dtype=dtype, device=device)
+    return torch.empty(shape, dtype=dtype, device=device)
 
 
 def check(rc: int, name: str) -> None:
-    """Raise on a launch error.  ``K8S_RCA_SYNC_DEBUG=1`` (SURVEY.md §5.2 debug
+    """Raise on a launch error.  ``K8SRCA_SYNC_DEBUG=1`` (SURVEY.md §5.2 debug
     mode) also synchronises after every kernel so an asynchronous fault is
     reported at the op that caused it, not at a later sync."""
     if rc != 0:

@@ -7,6 +7,7 @@ MFMA operand is a contiguous load; see ``csrc/kernels/attention.hip``).
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import math
 import os
 from dataclasses import dataclass
@@ -14,7 +15,7 @@ from typing import List, Optional
 
 import torch
 
-from ._lib import check, lib, ptr, stream_ptr, use_hip
+from ._lib import check, lib, ptr, scratch, stream_ptr, use_hip
 
 HEAD_DIM = 128
 
@@ -83,12 +84,12 @@ def rope_kv_write(qkv: torch.Tensor, positions: torch.Tensor, cos_sin: torch.Ten
     v_cache[blk, :, :, off] = v[ok]
 
 
-_fuse_qkv = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
+_fuse_qkv = KNOBS.fuse_splitk
 
 
 # RoPE / KV-write epilogue on the skinny qkv GEMM (decode at M <= 16 where the
 # dispatch picks the skinny kernel): one launch instead of GEMM + rope_kv.
-_skinny_rope = os.environ.get("K8SRCA_SKINNY_ROPE", "1") == "1"
+_skinny_rope = KNOBS.skinny_rope
 
 
 def skinny_rope_ok(M: int, N: int, K: int, nq: int, nkv: int) -> bool:
@@ -188,7 +189,7 @@ class AttnMeta:
 DECODE_PARTS = tuple(range(256, 1537, 64))  # candidate keys per decode work item (64-key aligned)
 DECODE_PARTS_V1 = (512, 768, 1024)
 # consecutive tokens of one sequence in a decode step share multi-token work items
-DECODE_GROUP_TOKENS = os.environ.get("K8S_DECODE_GROUP", "1") == "1"
+DECODE_GROUP_TOKENS = KNOBS.decode_group
 DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (<= 256 VGPRs)
 DECODE_ITEM_OVERHEAD = 256               # per-item start cost in key-equivalents (replay-calibrated)
 _DECODE_PLANNER = "makespan"
@@ -274,8 +275,8 @@ def attach_decode_plan(meta: "AttnMeta", ctx_host, nq: int, nkv: int, block_size
         n_parts = 1 << (n - 1).bit_length()
     meta.n_parts, meta.part_size = n_parts, P
     if n_parts > 1:
-        meta.part_o = torch.empty(S * nq * n_parts * HEAD_DIM, dtype=torch.float32, device=device)
-        meta.part_ml = torch.empty(S * nq * n_parts * 2, dtype=torch.float32, device=device)
+        meta.part_o = scratch(S * nq * n_parts * HEAD_DIM, torch.float32, device)
+        meta.part_ml = scratch(S * nq * n_parts * 2, torch.float32, device)
     return meta
 
 
@@ -334,9 +335,9 @@ def build_decode_items(ctx_lens, q_rows, part: int, chain=None, gmax: int = 1):
 
 def pf_wg_rows(G: int) -> int:
     """(token, q-head) rows per paged-64 prefill workgroup: 256 for the 8-wave
-    LDS-DMA kernel (``K8SRCA_PF_W8``, default on; the C launcher reads the
+    LDS-DMA kernel (knob ``pf_w8``, default on; the C launcher reads the
     same switch per launch), 128 for the 4-wave pg64 kernel."""
-    if os.environ.get("K8SRCA_PF_W8", "1") != "0" and PF8_ROWS % G == 0:
+    if KNOBS.pf_w8 != 0 and PF8_ROWS % G == 0:
         return PF8_ROWS
     return PF_ROWS
 
@@ -354,7 +355,7 @@ PF8_ROWS = 256              # rows per 8-wave (w8) prefill workgroup
 PF8_MAXP = 1024             # key pages per w8 work item (page ids staged in LDS; attention.hip)
 PF_MAX_SLOTS = 512          # partial-result slots of the prefill split-KV workspace
 # split long key ranges until a prefill launch has about this many workgroups
-PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
+PF_TARGET_WGS = KNOBS.pf_target_wgs
 # makespan planner (PF_OVERHEAD_PAGES > 0): where the fixed-target rule would split
 # (too few tiles to fill the chip), pick instead the split length that minimises
 # the launch's estimated makespan on the CU slots, pricing every work item at its
@@ -362,9 +363,9 @@ PF_TARGET_WGS = int(os.environ.get("K8S_PF_TARGET_WGS", "512"))
 # Replayed steady-state mix (profiles/r4/planner/): fixed target 635.5 -> 725.5
 # TFLOP/s at 8 pages (200-700-token extends -24 %, longer ones -7 %); applying it
 # to launches with enough tiles too (PF_MAKESPAN_ALL) 675-715; 0 = the fixed target.
-PF_OVERHEAD_PAGES = float(os.environ.get("K8S_PF_OVERHEAD_PAGES", "8"))
+PF_OVERHEAD_PAGES = KNOBS.pf_overhead_pages
 PF_CU_SLOTS = 256           # concurrent prefill workgroups: one 8-wave w8 workgroup per CU
-PF_MAKESPAN_ALL = os.environ.get("K8S_PF_MAKESPAN_ALL", "0") == "1"
+PF_MAKESPAN_ALL = KNOBS.pf_makespan_all
 _NO_END = 1 << 30
 
 
@@ -538,8 +539,8 @@ def attach_plan(meta: "AttnMeta", plan: PrefillPlan, device, workspace: Optional
 def prefill_workspace(nkv: int, device, slots: int = PF_MAX_SLOTS, D: int = HEAD_DIM) -> tuple:
     """fp32 partial-O / (max, sum) buffers for ``slots`` split-tile parts
     (sized for the larger, 256-row workgroup)."""
-    return (torch.empty(slots * nkv * PF8_ROWS * D, dtype=torch.float32, device=device),
-            torch.empty(slots * nkv * PF8_ROWS * 2, dtype=torch.float32, device=device))
+    return (scratch(slots * nkv * PF8_ROWS * D, torch.float32, device),
+            scratch(slots * nkv * PF8_ROWS * 2, torch.float32, device))
 
 
 def paged_attention(q: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor, meta: AttnMeta, nq: int,

@@ -7,12 +7,13 @@ engine's graph batch buckets -- and writes ``data/gemm_tuned_<model>.csv``.
 winner, every other shape the default heuristic, nothing is tuned online.
 Measured on MI355X (profiles/r1_gemm_tunableop_8b.txt): per-shape wins of up
 to ~35 % (down projection, M = 128-192) but losses elsewhere (3 % net over the
-decode buckets), so it is off by default (``K8S_RCA_GEMM_TUNING=1``); the
+decode buckets), so it is off by default (``K8SRCA_GEMM_TUNING=1``); the
 measured dispatch of :mod:`.linear` (hand-written gemm_mid / skinny kernels
 vs hipBLASLt per shape) is the default path.
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import logging
 import os
 import shutil
@@ -35,7 +36,7 @@ def load(model: str, tp: int = 1) -> bool:
     """Use the tuned GEMM table of ``model`` at TP degree ``tp`` if one exists
     for this build (TunableOp validators: torch / HIP / hipBLASLt / arch)."""
     global _loaded
-    if os.environ.get("K8S_RCA_GEMM_TUNING", "0") != "1" or not torch.cuda.is_available():
+    if not KNOBS.gemm_tuning or not torch.cuda.is_available():
         return False
     path = table_path(model, tp)
     if _loaded == path:

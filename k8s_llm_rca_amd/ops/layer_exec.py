@@ -10,6 +10,7 @@ results (``tests/test_model_gpu.py::test_layer_executor_bit_identical``).
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import ctypes
 import os
 from typing import List
@@ -18,7 +19,7 @@ import torch
 
 from . import attention as A
 from . import linear as LIN
-from ._lib import check, lib, ptr, stream_ptr
+from ._lib import check, lib, ptr, scratch, stream_ptr
 
 P = ctypes.c_void_p
 I = ctypes.c_int
@@ -42,25 +43,25 @@ class LlamaStep(ctypes.Structure):
         ("p_bt_stride", I), ("p_S", I), ("n_tiles", I), ("n_merge", I),
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
-        ("ar_id", I), ("ar_mode", I), ("ar_fuse", I), ("ar_push", I),
+        ("ar_id", I), ("ar_mode", I), ("ar_fuse", I), ("ar_push", I), ("nf_flags", P),
     ]
 
 
-_enabled = os.environ.get("K8SRCA_LAYER_EXEC", "1") == "1"
+_enabled = KNOBS.layer_exec
 # TP: all-reduce + residual add + RMSNorm of every row-parallel output in one launch
-_fuse_ar_norm = os.environ.get("K8SRCA_TP_FUSED_NORM", "1") == "1"
+_fuse_ar_norm = KNOBS.tp_fused_norm
 # TP: o / down projections on the stream GEMM store straight into the all-reduce's
 # slots (push epilogue, csrc/kernels/allreduce.hip "push epilogue").  Off by
 # default: on the tp-sim loopback the push GEMM's in-kernel publish (store acks +
 # release + flag per strip, +2.5-5.4 us) costs what the consumer saves (staging,
 # -2-2.5 us): 0.3-1.8 us slower per pair at 70B TP=8 decode shapes
 # (tools/push_ab.py, profiles/r4/push/).  1 = push wherever the shape allows.
-_tp_push = os.environ.get("K8SRCA_TP_PUSH", "0") == "1"
+_tp_push = KNOBS.tp_push
 # test hook: route o / down through the stream GEMM (LDS-DMA cfg 13; down split-K 2)
 # wherever its shape allows, so small test models exercise both push forms
-_tp_push_force = os.environ.get("K8SRCA_TP_PUSH_FORCE", "0") == "1"
+_tp_push_force = KNOBS.tp_push_force
 # split-K o / down projections reduced inside the following residual add + RMSNorm
-_fuse_splitk = os.environ.get("K8SRCA_FUSE_SPLITK", "1") == "1"
+_fuse_splitk = KNOBS.fuse_splitk
 # (Round 3 also carried a row-chunked o / down GEMM with each chunk's
 # all-reduce on a side stream, and the prefill attention on a side stream beside
 # the decode attention: both measured as losses -- profiles/r3/ab/tp_overlap_*,
@@ -155,14 +156,15 @@ class LlamaExecutor:
         T, H = residual.shape
         dev, dt = residual.device, residual.dtype
         ld_qkv = (m.nq + 2 * m.nkv) * m.D
-        y = torch.empty((T, H), dtype=dt, device=dev)
-        qkv = torch.empty((T, ld_qkv), dtype=dt, device=dev)
-        attn = torch.empty((T, m.nq * m.D), dtype=dt, device=dev)
-        obuf = torch.empty((T, H), dtype=dt, device=dev)
-        gu = torch.empty((T, 2 * m.inter), dtype=dt, device=dev)
-        act = torch.empty((T, m.inter), dtype=dt, device=dev)
-        prev = torch.empty((T, H), dtype=dt, device=dev)
+        y = scratch((T, H), dt, dev)
+        qkv = scratch((T, ld_qkv), dt, dev)
+        attn = scratch((T, m.nq * m.D), dt, dev)
+        obuf = scratch((T, H), dt, dev)
+        gu = scratch((T, 2 * m.inter), dt, dev)
+        act = scratch((T, m.inter), dt, dev)
+        prev = scratch((T, H), dt, dev)
         st.T, st.nd = T, inp.n_decode
+        st.nf_flags = ptr(m.nf_flags)
         if self._car is not None:
             from ..parallel.xgmi import ONE_SHOT_MAX
             st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2

@@ -8,14 +8,15 @@ from typing import Dict, List, Tuple
 import torch
 import torch.nn.functional as F
 
-from ._lib import check, lib, ptr, stream_ptr
+from ..knobs import KNOBS
+from ._lib import check, lib, ptr, scratch, stream_ptr
 
-SKINNY_MAX_M = int(os.environ.get("K8SRCA_SKINNY_MAX_M", "16"))
+SKINNY_MAX_M = KNOBS.skinny_max_m
 # measured on MI355X (tools/bench_kernels.py): the skinny kernel beats hipBLASLt
 # ~2x on the small-N decode projections (o_proj / QKV) for M <= 16 and ties or
 # loses on the wide ones; beyond M = 16 its L2-read X operand is the bottleneck.
 SKINNY_MAX_NK = 8192 * 4096
-_enabled = os.environ.get("K8SRCA_SKINNY", "1") == "1"
+_enabled = KNOBS.skinny
 
 
 def set_skinny(enabled: bool) -> None:
@@ -86,7 +87,7 @@ def linear(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.
 # hipblasLtMatmul instead of F.linear's ~28 us of host time.
 BLASLT_WS_BYTES = 64 << 20
 _blaslt_ws = {}
-_native_lib_gemm = os.environ.get("K8SRCA_NATIVE_BLASLT", "1") == "1"
+_native_lib_gemm = KNOBS.native_blaslt
 
 
 def lib_gemm(x: torch.Tensor, w: torch.Tensor, out: torch.Tensor = None) -> torch.Tensor:
@@ -138,7 +139,7 @@ def reserve_lib_workspace(dev: torch.device) -> None:
 
 
 _big_ws: Dict[torch.device, torch.Tensor] = {}
-_big_tail = os.environ.get("K8SRCA_BIG_TAIL", "1") == "1"
+_big_tail = KNOBS.big_tail
 
 
 def reserve_big_ws(dev: torch.device, enable: bool = None) -> None:
@@ -196,7 +197,7 @@ def load_lib_algos(path: str) -> int:
     them up to the next ladder point; it measured slower (profiles/r2_blaslt_ab/)
     and is still read for other models' files.  No-op without the native
     library GEMM."""
-    if not _native_lib_gemm or os.environ.get("K8S_BLASLT_ALGOS", "1") != "1" or not os.path.exists(path):
+    if not _native_lib_gemm or not KNOBS.blaslt_algos or not os.path.exists(path):
         return 0
     with open(path) as f:
         d = json.load(f)
@@ -234,7 +235,7 @@ DATA_DIR = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__
 
 
 def dispatch_path(model: str, tp: int = 1) -> str:
-    override = os.environ.get("K8SRCA_GEMM_DISPATCH_FILE")  # A/B of two measured tables
+    override = KNOBS.gemm_dispatch_file  # A/B of two measured tables
     if override:
         return override
     return os.path.join(DATA_DIR, f"gemm_dispatch_{model}" + (f"-tp{tp}" if tp > 1 else "") + ".json")
@@ -242,7 +243,7 @@ def dispatch_path(model: str, tp: int = 1) -> str:
 
 def load_dispatch(path: str) -> bool:
     global _dispatch
-    if not os.path.exists(path) or os.environ.get("K8SRCA_GEMM_DISPATCH", "1") != "1":
+    if not os.path.exists(path) or not KNOBS.gemm_dispatch:
         return False
     with open(path) as f:
         d = json.load(f)
@@ -343,14 +344,14 @@ def gemm_stream(x: torch.Tensor, w: torch.Tensor, cfg: int = 8, splits: int = 1,
     return out
 
 
-BIG_PIPE = int(os.environ.get("K8SRCA_BIG_VAR", "1"))  # schedule variant (gemm_big.hip: 1 = ping-pong)
+BIG_PIPE = KNOBS.big_var  # schedule variant (gemm_big.hip: 1 = ping-pong)
 # Prefill-size dispatch between gemm_big and hipBLASLt: per (N, K) the M ranges
 # where the hand-written kernel measured faster, each with its K split count
 # (data/gemm_big_<model>.json, tools/big_gemm_ab.py --emit), separately for the
 # SwiGLU-fused gate_up form (against hipBLASLt + silu_mul).
 # K8SRCA_BIG_GEMM=0 disables it; K8SRCA_BIG_GEMM=all uses gemm_big (no K split)
 # for every shape it accepts above DISPATCH_MAX_M (A/B runs).
-_big_mode = os.environ.get("K8SRCA_BIG_GEMM", "1")
+_big_mode = KNOBS.big_gemm
 _big_ranges: Dict[Tuple, List[Tuple[int, int, int]]] = {}
 
 
@@ -451,7 +452,7 @@ def _big_pick(M: int, N: int, K: int, silu: bool = False) -> int:
 # gemm_stream with one K split for gate_up, the SwiGLU form of the same strip
 # kernel (64-row W strips = 32 gate + 32 up rows) replaces gate_up + silu_mul --
 # the same weight bytes, no [M, 2I] write and re-read, one launch fewer.
-_stream_silu = os.environ.get("K8SRCA_STREAM_SILU", "1") == "1"
+_stream_silu = KNOBS.stream_silu
 
 
 def swiglu_choice(M: int, N2: int, K: int):
@@ -615,7 +616,7 @@ def _scratch(dev: torch.device, n: int) -> torch.Tensor:
         if t is not None:
             _retired_scratch.append(t)
             scratch_growths += 1
-        t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
+        t = scratch(max(n, 1 << 20), torch.float32, dev)
         _mid_scratch[dev] = t
     return t
 

@@ -5,7 +5,7 @@ from typing import Optional, Tuple
 
 import torch
 
-from ._lib import check, lib, ptr, stream_ptr, use_hip
+from ._lib import check, lib, ptr, scratch, stream_ptr, use_hip
 
 
 def route_topk(logits: torch.Tensor, k: int) -> Tuple[torch.Tensor, torch.Tensor]:
@@ -136,7 +136,7 @@ def _split_scratch(dev: torch.device, n: int) -> torch.Tensor:
         if t is not None:  # never freed: graphs captured earlier replay at its address (ops/linear.py _scratch)
             from . import linear as LIN
             LIN._retired_scratch.append(t)
-        t = torch.empty(max(n, 1 << 20), dtype=torch.float32, device=dev)
+        t = scratch(max(n, 1 << 20), torch.float32, dev)
         _scratch[dev] = t
     return t
 

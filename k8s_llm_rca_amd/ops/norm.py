@@ -65,3 +65,14 @@ def silu_mul(gu: torch.Tensor, out: Optional[torch.Tensor] = None) -> torch.Tens
     g, u = gu.float().split(inter, dim=-1)
     out.copy_((torch.nn.functional.silu(g) * u).to(out.dtype))
     return out
+
+
+def nonfinite_flag(x: torch.Tensor, flag: torch.Tensor) -> None:
+    """Debug: ``flag[0] = 1`` (int32, device) when ``x`` holds a NaN / inf;
+    never clears it.  CPU tensors: the same test in PyTorch."""
+    if use_hip(x):
+        xc = x.contiguous()
+        check(lib().k8s_nonfinite_flag(ptr(xc), xc.numel(), ptr(flag), stream_ptr(x)), "nonfinite_flag")
+        return
+    if not torch.isfinite(x).all():
+        flag[0] = 1

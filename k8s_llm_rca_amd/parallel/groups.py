@@ -8,6 +8,7 @@ moves tokens with all-to-all.  ``gloo`` runs the same code on CPU for tests.
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import os
 from dataclasses import dataclass
 from typing import Optional
@@ -150,16 +151,16 @@ def attach_custom_allreduce(pc: ParallelContext, same_gpu: bool = False) -> Para
     """Give a GPU TP context the xGMI communicator (``parallel/xgmi.py``):
     one-/two-shot all-reduce, fused all-reduce + add + RMSNorm, all-to-all and
     all-gather over hipIpc-mapped peer buffers, every data collective on it
-    (``xgmi_only``).  ``K8S_RCA_CUSTOM_AR=0`` keeps every collective on RCCL.
+    (``xgmi_only``).  Knob ``custom_ar=0`` (``K8SRCA_CUSTOM_AR``) keeps every collective on RCCL.
     ``same_gpu``: the ranks share one device over a gloo group (the one-GPU
     rehearsal of a TP deployment: RCCL refuses duplicate devices, so the xGMI
     kernels are the only data path and a failure to map them is fatal)."""
-    if pc.tp_size > 1 and torch.cuda.is_available() and os.environ.get("K8S_RCA_CUSTOM_AR", "1") != "0":
+    if pc.tp_size > 1 and torch.cuda.is_available() and KNOBS.custom_ar:
         from .xgmi import XgmiAllReduce
         # 64 MiB: every TP all-reduce up to 4,096 tokens of 70B (8,192 x bf16) in one xGMI
         # two-shot, which reads the N-1 peers over N-1 links at once; larger ones in
         # 64 MiB chunks (640 MiB of uncached HBM a rank)
-        mb = int(os.environ.get("K8S_RCA_AR_MAX_MB", "64"))
+        mb = KNOBS.ar_max_mb
         nccl = dist.get_backend(pc.tp_group) == "nccl"
         if not nccl and not same_gpu:
             return pc  # a gloo group on separate devices (CPU-side tests): the dist.* collectives

@@ -20,6 +20,7 @@ No exec, no GPU call: :func:`bind_rank` only reads sysfs and calls
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import glob
 import os
 import re
@@ -143,7 +144,7 @@ def rank_cpus(local_rank: int, local_world: int, allowed: Sequence[int], nodes: 
 def bind_rank(local_rank: int, local_world: int) -> Optional[dict]:
     """Bind this process to its rank's CPU slice (see the module docstring);
     returns ``{"cpus", "numa", "source"}`` or None when disabled / unsupported."""
-    if os.environ.get("K8SRCA_BIND", "1") != "1" or local_world <= 1 or not hasattr(os, "sched_setaffinity"):
+    if not KNOBS.bind or local_world <= 1 or not hasattr(os, "sched_setaffinity"):
         return None
     allowed = sorted(os.sched_getaffinity(0))
     gpus = gpu_numa_nodes()

@@ -7,6 +7,7 @@
 """
 from __future__ import annotations
 
+from ..knobs import KNOBS
 import contextlib
 import ctypes
 import os
@@ -24,7 +25,7 @@ def _get_roctx():
     global _roctx, _roctx_tried
     if not _roctx_tried:
         _roctx_tried = True
-        if os.environ.get("K8SRCA_ROCTX") == "1":
+        if KNOBS.roctx:
             for lib in ("librocprofiler-sdk-roctx.so", "/opt/rocm/lib/librocprofiler-sdk-roctx.so",
                         "libroctx64.so"):
                 try:

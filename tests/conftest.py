@@ -18,6 +18,27 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer CPU tests")
 
 
+@pytest.fixture
+def knob():
+    """``knob(name, value)``: set a k8s_llm_rca_amd.knobs switch for this test
+    (native ones pushed to the HIP library); restored at teardown."""
+    from k8s_llm_rca_amd import knobs as K
+    old = {}
+
+    def set_(name, value):
+        if name not in old:
+            old[name] = getattr(K.KNOBS, name)
+        setattr(K.KNOBS, name, value)
+        if name in K.NATIVE:
+            K.push_native()
+
+    yield set_
+    for name, v in old.items():
+        setattr(K.KNOBS, name, v)
+    if any(n in K.NATIVE for n in old):
+        K.push_native()
+
+
 @pytest.fixture(scope="session")
 def small_cluster():
     from k8s_llm_rca_amd.graph.synth import generate_cluster

@@ -55,11 +55,11 @@ def test_groups_break_on_partition_count_and_sequence():
     assert nt.tolist() == [1] * 6
 
 
-def test_prefill_plan_caps_w8_items_at_lds_page_table(monkeypatch):
+def test_prefill_plan_caps_w8_items_at_lds_page_table(monkeypatch, knob):
     """with the 8-wave prefill kernel every work item spans at
     most PF8_MAXP key pages (the kernel's LDS page table), whatever the block
     table width; each tile's items tile its key range exactly once."""
-    monkeypatch.setenv("K8SRCA_PF_W8", "2")
+    knob("pf_w8", 2)
     for ctx, qlen, known in (([70_000, 500], [96, 40], True), ([66_000, 300], [66_000, 300], False)):
         qs = [0]
         for n in qlen:
@@ -77,18 +77,18 @@ def test_prefill_plan_caps_w8_items_at_lds_page_table(monkeypatch):
                 assert sp[0][0] == 0 and all(a[1] == b[0] for a, b in zip(sp, sp[1:]))
                 assert sp[-1][1] >= min(end_pages, sp[-1][1])
     # the 4-wave kernel has no page table: no cap without a split plan
-    monkeypatch.setenv("K8SRCA_PF_W8", "0")
+    knob("pf_w8", 0)
     plan = A.plan_prefill([0, 66_000], 4, 64, None, nkv=8)
     assert plan.n_merge == 0
 
 
-def test_prefill_makespan_planner_covers_keys_and_balances(monkeypatch):
+def test_prefill_makespan_planner_covers_keys_and_balances(monkeypatch, knob):
     """The makespan split choice (K8S_PF_OVERHEAD_PAGES > 0): every tile's items
     still tile its key range exactly once, the slot budget holds, and on a
     200-700-token extend over a ~5k context (7 tiles x 8 heads of ~83 pages) it
     picks a split whose round count is full rather than a few items over a
     multiple of the CU slots."""
-    monkeypatch.setenv("K8SRCA_PF_W8", "1")
+    knob("pf_w8", 1)
     monkeypatch.setattr(A, "PF_OVERHEAD_PAGES", 3.0)
     monkeypatch.setattr(A, "PF_MAKESPAN_ALL", True)
     ctx, q = [5277], [437]

@@ -189,7 +189,7 @@ def _cpu_meta(meta):
 @pytest.mark.parametrize("BS", [64, 32])  # 64: persistent work-list kernel; 32: (seq, part) grid kernel
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 8)])
 @pytest.mark.parametrize("ctx", [[1], [17, 64, 65], [1000, 3, 2500, 128], [5000], [130] * 300])
-def test_paged_decode(nq, nkv, ctx, BS, monkeypatch):
+def test_paged_decode(nq, nkv, ctx, BS, monkeypatch, knob):
     _need_gpu()
     torch.manual_seed(1)
     NB = sum((c + BS - 1) // BS for c in ctx) + 4
@@ -203,7 +203,7 @@ def test_paged_decode(nq, nkv, ctx, BS, monkeypatch):
     # the split-KV reduce's register form (<= 16 partitions) == its LDS form, bit for bit
     outs = {}
     for pre in ("1", "0"):
-        monkeypatch.setenv("K8SRCA_DECODE_REDUCE_PRE", pre)
+        knob("decode_reduce_pre", pre != "0")
         outs[pre] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
     assert torch.equal(outs["1"], outs["0"])
 
@@ -601,7 +601,7 @@ def test_grouped_gemm_matches_per_expert(E, N, K, fuse, splits):
     torch.testing.assert_close(got, ref, atol=3e-2, rtol=3e-2)
 
 
-def test_blaslt_bucket_registration(monkeypatch):
+def test_blaslt_bucket_registration(monkeypatch, knob):
     """A solution registered for M in [lo, hi] (k8s_blaslt_set_algo_range: the
     heuristic's own pick at another M) serves that range only; results inside
     and outside the bucket match fp32; the shipped 8B table registers."""
@@ -621,7 +621,7 @@ def test_blaslt_bucket_registration(monkeypatch):
             x = torch.randn(M, K, device=dev).bfloat16()
             torch.testing.assert_close(LIN.lib_gemm(x, w).float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
         LIN.clear_lib_tuning()
-        monkeypatch.setenv("K8S_BLASLT_ALGOS", "1")
+        knob("blaslt_algos", True)
         assert LIN.load_lib_algos(LIN.lib_algos_path("llama3-8b")) > 0
     finally:
         LIN.clear_lib_tuning()
@@ -653,7 +653,7 @@ def test_gemm_stream_vs_fp32(M, N, K, splits, cfg):
 
 @pytest.mark.parametrize("M", [16, 64, 100, 128, 192])
 @pytest.mark.parametrize("cfg,splits", [(13, 1), (14, 4), (15, 2), (23, 4), (24, 8)])
-def test_glds_hand_reads_bit_identical(M, cfg, splits, monkeypatch):
+def test_glds_hand_reads_bit_identical(M, cfg, splits, monkeypatch, knob):
     """The LDS-DMA decode GEMM's hand-issued LDS reads with counted waits (the
     default, K8SRCA_GLDS_HAND) compute exactly what hipcc's own reads compute:
     the same MFMAs in the same order, only the waits differ."""
@@ -667,7 +667,7 @@ def test_glds_hand_reads_bit_identical(M, cfg, splits, monkeypatch):
     w = (torch.randn(N, K, device=dev) * 0.02).bfloat16()
     outs = {}
     for h in ("0", "1"):
-        monkeypatch.setenv("K8SRCA_GLDS_HAND", h)
+        knob("glds_hand", h != "0")
         outs[h] = LIN.gemm_stream(x, w, cfg, splits)
     assert torch.equal(outs["0"], outs["1"])
     torch.testing.assert_close(outs["1"].float(), x.float() @ w.float().t(), atol=2e-2, rtol=2e-2)
@@ -730,7 +730,7 @@ def test_grouped_big_matches_per_expert(E, N, K, silu, pad, var, monkeypatch):
 
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (8, 1), (64, 4)])
 @pytest.mark.parametrize("ctx,qlen", [([7], [7]), ([4100, 700], [900, 700]), ([8000], [1500]), ([130, 64, 3000], [66, 64, 700])])
-def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
+def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch, knob):
     """The 8-wave LDS-DMA prefill kernel (256-row workgroups; K8SRCA_PF_W8=2 the
     compiler-scheduled page loop, 4 the explicitly prefetched one with tree
     reductions) against the 4-wave pg64 kernel and the fp32 reference, with and
@@ -747,12 +747,12 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
     outs = {}
     for w8 in ("2", "4", "5", "6", "6m", "1", "0"):  # w8 compiler schedule, explicit schedule, + LDS epilogue
         # (1 = default), + hand-issued LDS reads with counted waits (6m: with the 2-dims-per-lane merge), pg64
-        monkeypatch.setenv("K8SRCA_PF_W8", w8.rstrip("m"))
-        monkeypatch.setenv("K8SRCA_PF_MERGE16", "0" if w8.endswith("m") else "1")
+        knob("pf_w8", int(w8.rstrip("m")))
+        knob("pf_merge16", not w8.endswith("m"))
         torch.manual_seed(7)  # the same block tables for both kernels
         meta = _meta(ctx, qlen, nq, nkv, BS, NB, dev, decode=False)
         outs[w8] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
-    monkeypatch.setenv("K8SRCA_PF_W8", "2")
+    knob("pf_w8", 2)
     ref = A.paged_attention(q.cpu(), kc.cpu(), vc.cpu(), _cpu_meta(meta), nq, nkv, scale)
     for k in ("2", "4", "5"):
         torch.testing.assert_close(outs[k].cpu().float(), ref.float(), atol=2e-2, rtol=2e-2)
@@ -767,7 +767,7 @@ def test_prefill_w8_matches_pg64(nq, nkv, ctx, qlen, monkeypatch):
 
 
 @pytest.mark.parametrize("split", [False, True])
-def test_prefill_w8_long_context_block_table(split, monkeypatch):
+def test_prefill_w8_long_context_block_table(split, monkeypatch, knob):
     """a block table wider than the 8-wave kernel's LDS page
     table (bt_stride > 1024 pages, ctx > 64k tokens) must still run the kernel
     the planner tiled for (256-row tiles), with every item's key range cut at
@@ -775,7 +775,7 @@ def test_prefill_w8_long_context_block_table(split, monkeypatch):
     prefix (ctx_lens known: split-KV plan) and without one."""
     _need_gpu()
     torch.manual_seed(11)
-    monkeypatch.setenv("K8SRCA_PF_W8", "2")
+    knob("pf_w8", 2)
     BS, nq, nkv = 64, 8, 1
     ctx = [70_000 if split else 66_000, 500]
     qlen = [96, 40] if split else [66_000, 500]

@@ -402,10 +402,12 @@ def _prefill_inputs(m, T, seed=5):
     return inp, kc, vc
 
 
-def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb):
+def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb, layers=(2, 32)):
     import torch.distributed as dist
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), K8S_RCA_AR_MAX_MB=str(max_mb))
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
+    from k8s_llm_rca_amd.knobs import set_knob
+    set_knob("ar_max_mb", max_mb)
     from k8s_llm_rca_amd.models.config import get_config
     from k8s_llm_rca_amd.models.llama import LlamaModel
     from k8s_llm_rca_amd.parallel.groups import ParallelContext, attach_custom_allreduce
@@ -416,11 +418,16 @@ def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb):
         assert pc.custom_ar is not None and pc.xgmi_only
     else:
         pc = None
-    m = LlamaModel(get_config("llama3-8b"), "cuda:0", torch.bfloat16, pc, seed=11, init_mode="full_slice")
     out = {}
-    for T in Ts:
-        inp, kc, vc = _prefill_inputs(m, T)
-        out[T] = {"logits": m.forward(inp, kc, vc).float().cpu(), "exec": m._exec is not None and m._exec.fits(T)}
+    for nl in layers:
+        m = LlamaModel(get_config("llama3-8b", n_layers=nl), "cuda:0", torch.bfloat16, pc, seed=11,
+                       init_mode="full_slice")
+        for T in Ts:
+            inp, kc, vc = _prefill_inputs(m, T)
+            out[f"{nl}/{T}"] = {"logits": m.forward(inp, kc, vc).float().cpu(),
+                                "exec": m._exec is not None and m._exec.fits(T)}
+        del m
+        torch.cuda.empty_cache()
     if world > 1:
         out["status"] = pc.custom_ar.status()
     if rank == 0:
@@ -436,7 +443,12 @@ def test_tp2_llama3_8b_logits_match_tp1_one_gpu():
     host group, every collective on the xGMI kernels) gives the TP=1 logits
     within bf16 tolerance on a fixed prompt -- at T=300 through the native
     executor's fused all-reduce + add + RMSNorm, and at T=1100 (past the 4 MiB
-    buffer) through the Python layer path's chunked all-reduce."""
+    buffer) through the Python layer path's chunked all-reduce.  The TP sum
+    rounds each rank's row-parallel partial to bf16, so the two differ by
+    rounding that compounds with depth through a random-init stack (measured,
+    tools/tp_check.py, profiles/r5/tp_check.txt: 0.7 / 1.1 / 2.3 / 5.8 % at
+    1 / 2 / 8 / 32 layers, the same on both paths); a wrong shard or
+    collective is O(1) after one layer."""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     Ts = (300, 1100)
@@ -446,12 +458,13 @@ def test_tp2_llama3_8b_logits_match_tp1_one_gpu():
         a = torch.load(os.path.join(d, "tp2.pt"), weights_only=True)
         b = torch.load(os.path.join(d, "tp1.pt"), weights_only=True)
     assert a["status"] == 0
-    assert a[300]["exec"] and not a[1100]["exec"]
-    for T in Ts:
-        x, y = a[T]["logits"][:, :128256], b[T]["logits"][:, :128256]
-        assert torch.isfinite(x).all()
-        rel = ((x - y).norm() / y.norm()).item()
-        assert rel < 0.02, (T, rel)
-        # the top tokens agree (bf16 reduction order differs between TP=1 and TP=2)
-        top = set(y.topk(5, -1).indices.view(-1).tolist())
-        assert int(x.argmax(-1)) in top, T
+    assert a["2/300"]["exec"] and not a["2/1100"]["exec"]
+    for nl, bound in ((2, 0.02), (32, 0.1)):
+        for T in Ts:
+            x, y = a[f"{nl}/{T}"]["logits"][:, :128256], b[f"{nl}/{T}"]["logits"][:, :128256]
+            assert torch.isfinite(x).all()
+            rel = ((x - y).norm() / y.norm()).item()
+            assert rel < bound, (nl, T, rel)
+            # the top tokens agree (bf16 reduction order differs between TP=1 and TP=2)
+            top = set(y.topk(5, -1).indices.view(-1).tolist())
+            assert int(x.argmax(-1)) in top, (nl, T)

@@ -16,6 +16,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
+from k8s_llm_rca_amd.knobs import KNOBS, set_knob  # noqa: E402
 
 from k8s_llm_rca_amd.parallel.tpsim import LoopbackAR  # noqa: E402
 
@@ -38,7 +39,7 @@ def main():
         res = {"0": [], "1": [], "d": []}
         for _ in range(a.rounds):
             for fa in ("0", "1", "d"):
-                os.environ["K8SRCA_AR_FENCE_ALL"] = "1" if fa == "1" else "0"
+                set_knob("ar_fence_all", fa == "1")
                 for _ in range(3):
                     car(t, mode)
                 torch.cuda.synchronize()
@@ -61,7 +62,7 @@ def main():
                 res[fa].append(e0.elapsed_time(e1) * 1e3 / a.reps)
         med = {k: statistics.median(v) for k, v in res.items()}
         print(f"{nb:>9} {mode:>4} {med['0']:>8.1f} {med['1']:>9.1f} {med['d']:>12.1f}", flush=True)
-    os.environ.pop("K8SRCA_AR_FENCE_ALL", None)
+    set_knob("ar_fence_all", False)
     car.close()
 
 

@@ -13,6 +13,7 @@ import time
 import torch
 
 sys.path.insert(0, ".")
+from k8s_llm_rca_amd.knobs import KNOBS, set_knob  # noqa: E402
 from k8s_llm_rca_amd.ops import attention as A  # noqa: E402
 from k8s_llm_rca_amd.ops import norm as N  # noqa: E402
 
@@ -163,7 +164,7 @@ def main():
                     res[f"replay decode {name} B{b[0]}-{b[1]}"] = f"n={n} {u / n:.1f}us/step {by / u / 1e6:.2f} TB/s"
         # prefill: the 8-wave LDS-DMA kernel (K8SRCA_PF_W8=1) and the 4-wave pg64
         # kernel interleaved per recorded step (same process, same data)
-        kinds0 = tuple(args.pf_kinds.split(",")) if args.pf_ab else (os.environ.get("K8SRCA_PF_W8", "1"),)
+        kinds0 = tuple(args.pf_kinds.split(",")) if args.pf_ab else (str(KNOBS.pf_w8),)
         pf_ovh0, pf_all0 = A.PF_OVERHEAD_PAGES, A.PF_MAKESPAN_ALL  # the planner defaults (arms without "@")
         targets = [int(t) for t in args.pf_targets.split(",")] if args.pf_targets else [A.PF_TARGET_WGS]
         # arms: (kernel kind, planner split target in workgroups); the label keeps the old form for one target
@@ -179,9 +180,9 @@ def main():
             ql = [q for c, q in pre[i]]
             T = sum(ql)
             for k in kinds:
-                os.environ["K8SRCA_PF_W8"] = k.split("@")[0].rstrip("m")
+                set_knob("pf_w8", k.split("@")[0].rstrip("m"))
                 # "<kind>m": the 2-dims-per-lane merge kernel (K8SRCA_PF_MERGE16=0)
-                os.environ["K8SRCA_PF_MERGE16"] = "0" if k.split("@")[0].endswith("m") else "1"
+                set_knob("pf_merge16", not k.split("@")[0].endswith("m"))
                 arm = k.split("@")[1] if "@" in k else None
                 # "@o<pages>": makespan split choice everywhere; "@h<pages>": only where the
                 # fixed-target rule would split; "@<n>": fixed target of n workgroups
@@ -204,7 +205,7 @@ def main():
         for k in kinds:
             res[f"replay prefill {len(idx)} steps PF_W8={k}"] = (f"{tot[k] / len(idx):.1f}us/step "
                                                                f"{fl / tot[k] / 1e6:.1f} TFLOP/s")
-        os.environ["K8SRCA_PF_W8"] = kinds0[0]
+        set_knob("pf_w8", kinds0[0])
         A.PF_TARGET_WGS = targets[0]
         A.PF_OVERHEAD_PAGES, A.PF_MAKESPAN_ALL = pf_ovh0, pf_all0
         if args.pf_steps_out:

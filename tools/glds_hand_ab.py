@@ -18,6 +18,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
+from k8s_llm_rca_amd.knobs import KNOBS, set_knob  # noqa: E402
 
 from k8s_llm_rca_amd.ops import linear as LIN  # noqa: E402
 
@@ -55,7 +56,7 @@ def main():
             x = torch.randn(M, K, device=dev).bfloat16()
             outs = {}
             for h in ("0", "1"):
-                os.environ["K8SRCA_GLDS_HAND"] = h
+                set_knob("glds_hand", h)
                 outs[h] = LIN.gemm_stream(x, ws[0], cfg, splits).clone()
             torch.cuda.synchronize()
             same = bool(torch.equal(outs["0"], outs["1"]))
@@ -67,7 +68,7 @@ def main():
                 it[0] += 1
             for _ in range(a.rounds):
                 for h in ("0", "1"):
-                    os.environ["K8SRCA_GLDS_HAND"] = h
+                    set_knob("glds_hand", h)
                     res[h].append(timed(run, a.iters))
             line = {"shape": name, "M": M, "cfg": cfg, "splits": splits, "bit_identical": same,
                     "us_hipcc_reads": round(statistics.median(res["0"]), 2),
@@ -75,7 +76,7 @@ def main():
             line["tbps_hand"] = round(N * K * 2 / line["us_hand_reads"] / 1e6, 2)
             rows.append(line)
             print(json.dumps(line), flush=True)
-    os.environ.pop("K8SRCA_GLDS_HAND", None)
+    set_knob("glds_hand", True)
     out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out", "glds_hand_ab.jsonl")
     os.makedirs(os.path.dirname(out), exist_ok=True)
     with open(out, "w") as f:

@@ -8,6 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests"))
 
 import torch  # noqa: E402
+from k8s_llm_rca_amd.knobs import KNOBS, set_knob  # noqa: E402
 
 import test_kernels_gpu as T  # noqa: E402
 from k8s_llm_rca_amd.ops import attention as A  # noqa: E402
@@ -20,7 +21,7 @@ for ctx, BS, (nq, nkv) in (([1000, 3, 2500, 128], 64, (32, 8)), ([5000], 64, (32
     q = torch.randn(len(ctx), (nq + 2 * nkv) * 128, device=T.dev).bfloat16()
     outs = []
     for pre in ("0", "0", "1", "1", "0"):
-        os.environ["K8SRCA_DECODE_REDUCE_PRE"] = pre
+        set_knob("decode_reduce_pre", pre)
         outs.append(A.paged_attention(q, kc, vc, meta, nq, nkv, 1 / math.sqrt(128)).clone())
     torch.cuda.synchronize()
     eq = [[bool(torch.equal(a, b)) for b in outs] for a in outs]

@@ -548,6 +548,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                   "kernel_batches": int(sum(b["launches"] for b in bstats)),
                   "max_batch": int(max([b["max_batch"] for b in bstats] or [0]))},
     }
+    if getattr(eng, "tp_tune", None):
+        res["tp_collectives"] = eng.tp_tune  # the per-bucket epilogue plan measured on this fabric at init
     res["sanity"] = sanity(res)
     if world > 1 and not tp_mode:
         import torch.distributed as dist

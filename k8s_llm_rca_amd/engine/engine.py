@@ -146,6 +146,7 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         if self.pc.tp_size > 1 and not self._sim:
             from ..parallel.channel import make_channel
             self._chan = make_channel(self.pc)  # host-side step metadata (parallel/channel.py)
+        self.tp_tune = self._tune_collectives()
         self._last_tok = None  # TP workers: device tokens of the last sampling (decode inputs of the next step)
         # TP: exact vocab-parallel sampling (B10) instead of all-gathering logits
         self._dist_sample = (self.pc.tp_size > 1 and not self._sim and hasattr(self.model, "vocab_local")
@@ -184,6 +185,26 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         self._test_stall = False  # tests: a TP worker that receives steps but never executes them
         self._test_host_stall_s = 0.0  # tests: rank 0 sleeps between a step's message and its own launch
         self.comm_dead = False  # a TP worker whose own collective timed out: it stops executing steps
+
+    def _tune_collectives(self) -> Optional[dict]:
+        """TP on the xGMI communicator: time the row-parallel epilogue's forms
+        (one-/two-shot x staged/push) per decode bucket on this fabric, with
+        layer 0's real o / down weights, before any graph is captured
+        (``XgmiAllReduce.tune``; knob ``tp_autotune``).  Every rank runs it in
+        lockstep and gets the same plan; the report goes into the bench line."""
+        car = self.pc.custom_ar if self.pc.tp_size > 1 and not self._sim else None
+        if car is None or not hasattr(car, "tune") or not KNOBS.tp_autotune or self.device.type != "cuda":
+            return None
+        layers = getattr(self.model, "layers", None)
+        if not layers or getattr(self.model, "moe", None) is not None:
+            return None
+        L0 = layers[0]
+        buckets = sorted(set(self.cfg.graph_batch_sizes) | {384, 512, 1024, 2048, 4096})
+        t0 = time.perf_counter()
+        rep = car.tune([("o", L0["wo"]), ("down", L0["w_down"])], L0["post_norm"], float(self.mc.rms_eps), buckets)
+        log.info("xGMI epilogue plan tuned in %.1f s: %s", time.perf_counter() - t0,
+                 {T: r["pick"] for T, r in rep.items()})
+        return {"tune_s": round(time.perf_counter() - t0, 2), "buckets": rep}
 
     def _workspace_bytes(self) -> int:
         mc = self.mc

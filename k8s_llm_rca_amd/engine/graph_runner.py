@@ -196,7 +196,7 @@ class GraphRunnerMixin:
             n += n_sel
         dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
         dev_flat.copy_(host[:n], non_blocking=True)
-        ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event()
+        ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event(blocking=KNOBS.blocking_sync)
         ev.record()
         # the upload scattered into the graph's static inputs in one launch (csrc/kernels/norm_act.hip),
         # the speculative decode ids (spec) taken from the device tokens in the same launch; before a

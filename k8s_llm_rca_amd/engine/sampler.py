@@ -247,7 +247,7 @@ class SamplerMixin:
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)
-            ev = torch.cuda.Event()
+            ev = torch.cuda.Event(blocking=KNOBS.blocking_sync)
             ev.record()
         else:
             host, ev = tok, None

@@ -23,6 +23,7 @@ from typing import List, Optional, Sequence
 import numpy as np
 import torch
 
+from ..knobs import KNOBS
 from ..ops._lib import check, lib, ptr, stream_ptr
 
 
@@ -72,7 +73,7 @@ class DeviceGraph:
         hs = [torch.empty(t.shape, dtype=t.dtype, pin_memory=True) for t in ts]
         for h, t in zip(hs, ts):
             h.copy_(t, non_blocking=True)
-        ev = torch.cuda.Event()
+        ev = torch.cuda.Event(blocking=KNOBS.blocking_sync)
         ev.record(self.stream)
         ev.synchronize()
         return [h.numpy() for h in hs]

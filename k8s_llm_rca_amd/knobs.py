@@ -72,7 +72,9 @@ class Knobs:
     # ---------------------------------------------------------------- native layer executor / TP
     layer_exec: bool = _f(True, "whole dense layer stack issued by one C call (ops/layer_exec.py)")
     tp_fused_norm: bool = _f(True, "TP all-reduce + residual add + RMSNorm in one launch")
-    tp_push: bool = _f(False, "TP o/down GEMM epilogue stores into the all-reduce slots (push)")
+    tp_push: bool = _f(False, "TP o/down GEMM epilogue stores into the all-reduce slots (push) wherever it fits "
+                              "(default: where the init-time fabric tuning measured it faster)")
+    tp_autotune: bool = _f(True, "time one-/two-shot x staged/push per decode bucket at communicator init")
     tp_push_force: bool = _f(False, "test hook: route o/down through the stream GEMM wherever it fits")
     custom_ar: bool = _f(True, "xGMI communicator for TP/EP collectives (0: RCCL)", legacy="K8S_RCA_CUSTOM_AR")
     ar_max_mb: int = _f(64, "xGMI buffer per rank in MiB (larger messages run in chunks of it)",
@@ -96,6 +98,8 @@ class Knobs:
                                           legacy="K8S_RCA_SWITCH_INTERVAL")
     profile_engine: Optional[str] = _f(None, "cProfile of the engine thread dumped to this path",
                                        legacy="K8S_RCA_PROFILE_ENGINE")
+    blocking_sync: bool = _f(False, "host waits on the engine's token / staging / graph-mirror events block in the "
+                                    "driver (hipEventBlockingSync) instead of spinning")
     nonfinite_check: bool = _f(False, "device-side non-finite flag on every layer's normed input (no host sync)")
     poison: bool = _f(False, "fill scratch / partial / KV buffers with NaN at allocation: a read of memory no "
                              "kernel wrote shows up as NaN (sampler NON_FINITE) instead of stale finite data")

@@ -167,10 +167,12 @@ class LlamaExecutor:
         st.nf_flags = ptr(m.nf_flags)
         if self._car is not None:
             from ..parallel.xgmi import ONE_SHOT_MAX
-            st.ar_mode = 1 if T * H * 2 <= ONE_SHOT_MAX else 2
+            plan_for = getattr(self._car, "plan_for", None)  # the fabric-tuned plan (XgmiAllReduce.tune)
+            mode, push = plan_for(T, H) if plan_for else ((1 if T * H * 2 <= ONE_SHOT_MAX else 2), False)
+            st.ar_mode = mode
             # the two-shot epilogue splits each row's 16-B chunks evenly over the ranks
             st.ar_fuse = int(_fuse_ar_norm and (st.ar_mode == 1 or (H // 8) % self._car.world == 0))
-            st.ar_push = int(bool(st.ar_fuse) and _tp_push and self._car.push_ok(H, T, st.ar_mode))
+            st.ar_push = int(bool(st.ar_fuse) and (_tp_push or push) and self._car.push_ok(H, T, st.ar_mode))
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
         st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)

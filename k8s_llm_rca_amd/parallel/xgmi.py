@@ -214,6 +214,92 @@ class XgmiAllReduce:
         out = out.view(torch.uint8)[:, :nb].contiguous()
         return out.view(x.dtype).view(self.world, *x.shape)
 
+    # ------------------------------------------------------------ fabric tuning
+    plan: Optional[dict] = None  # {T bucket: (mode, push)} from :meth:`tune`; None = the size rule
+
+    def tune(self, shapes, nw: torch.Tensor, eps: float, buckets, iters: int = 10, rounds: int = 3) -> dict:
+        """Pick, per decode row-count bucket T, the collective form of the TP
+        row-parallel epilogue (GEMM + all-reduce + residual add + RMSNorm) by
+        timing every candidate ON THIS FABRIC at communicator init: one-shot
+        vs two-shot, staged (the GEMM writes y, the fused epilogue stages it)
+        vs push (the stream GEMM stores into the peers' slots,
+        csrc/kernels/allreduce.hip "push epilogue").  ``shapes``: the real
+        row-parallel weights [(name, w [H, K_local])] (o and down).  Every
+        rank runs the same sequence of collectives, and each timing is
+        max-reduced over the group, so every rank gets the same plan.  The
+        round-4 defaults (one-shot <= 512 KiB, push off) came from a
+        loopback on one GPU, which cannot show xGMI behaviour; this replaces
+        them with what the deployment's own links measure."""
+        from ..ops import linear as LIN
+        H = int(shapes[0][1].shape[0])
+        dev = shapes[0][1].device
+        report = {}
+        plan = {}
+        for T in sorted(set(int(b) for b in buckets)):
+            if T * H * 2 + 4 * T > self.max_bytes:
+                continue
+            cands = [(1, False)]
+            if (H // 8) % self.world == 0:
+                cands.append((2, False))
+            for m in (1, 2):
+                if (m, False) not in cands:
+                    continue
+                ok = True
+                for _, w in shapes:
+                    kind, cfg, splits = LIN.select_gemm(T, H, int(w.shape[1]))
+                    ok &= kind == LIN.KIND_STREAM and (cfg >= 13 or splits > 1) and self.push_ok(H, T, m)
+                if ok:
+                    cands.append((m, True))
+            x = {name: torch.randn(T, int(w.shape[1]), device=dev).bfloat16() for name, w in shapes}
+            res = torch.zeros(T, H, device=dev, dtype=torch.bfloat16)
+            y = torch.empty(T, H, device=dev, dtype=torch.bfloat16)
+            out = torch.empty(T, H, device=dev, dtype=torch.bfloat16)
+
+            def pair(m, push):
+                for name, w in shapes:
+                    if push:
+                        kind, cfg, splits = LIN.select_gemm(T, H, int(w.shape[1]))
+                        self.linear_push_addnorm(x[name], w, res, nw, y, eps, cfg, splits, m)
+                    else:
+                        LIN.linear(x[name], w, out)
+                        self.addnorm(out, res, nw, y, eps, m)
+                    res.zero_()
+
+            us = {c: [] for c in cands}
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            for _ in range(rounds):
+                for c in cands:
+                    pair(*c)  # warm (also aligns the ranks on this candidate)
+                    e0.record()
+                    for _ in range(iters):
+                        pair(*c)
+                    e1.record()
+                    e1.synchronize()
+                    us[c].append(e0.elapsed_time(e1) * 1e3 / iters)
+            med = torch.tensor([sorted(v)[len(v) // 2] for v in us.values()], dtype=torch.float64)
+            on_dev = dist.get_backend(self.group) == "nccl"
+            t = med.to(dev) if on_dev else med
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.group)  # the slowest rank's view
+            med = t.cpu().tolist()
+            best = min(range(len(cands)), key=lambda i: med[i])
+            plan[T] = cands[best]
+            report[T] = {f"{'two' if m == 2 else 'one'}_shot{'_push' if p else ''}": round(v, 2)
+                         for (m, p), v in zip(cands, med)}
+            report[T]["pick"] = list(cands[best])
+        torch.cuda.synchronize()
+        self.plan = plan
+        self.tune_report = report
+        return report
+
+    def plan_for(self, T: int, H: int):
+        """(mode, push) of a [T, H] row-parallel epilogue: the tuned bucket at or
+        above T, else the size rule (one-shot <= 512 KiB, no push)."""
+        if self.plan:
+            for b in sorted(self.plan):
+                if b >= T:
+                    return self.plan[b]
+        return (1 if T * H * 2 <= ONE_SHOT_MAX else 2), False
+
     def status_async(self, host: torch.Tensor) -> None:
         """Copy this rank's STATUS word into ``host`` (pinned int32[1]) on the
         current stream, ordered after the collectives issued before it."""

@@ -468,3 +468,45 @@ def test_tp2_llama3_8b_logits_match_tp1_one_gpu():
             # the top tokens agree (bf16 reduction order differs between TP=1 and TP=2)
             top = set(y.topk(5, -1).indices.view(-1).tolist())
             assert int(x.argmax(-1)) in top, (nl, T)
+
+
+def _tune_worker(rank, world, port, out_dir):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.parallel.groups import SHARED_GPU_AR_BLOCKS as CAP
+    from k8s_llm_rca_amd.parallel.xgmi import XgmiAllReduce
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    car = XgmiAllReduce(dist.group.WORLD, max_bytes=16 << 20, timeout_s=60.0, max_blocks=CAP)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    H = 4096
+    wo = (torch.randn(H, 2048, device="cuda", generator=g) * 0.02).bfloat16()
+    wd = (torch.randn(H, 7168, device="cuda", generator=g) * 0.02).bfloat16()
+    nw = torch.ones(H, device="cuda").bfloat16()
+    rep = car.tune([("o", wo), ("down", wd)], nw, 1e-5, (16, 64, 256, 4096), iters=3, rounds=2)
+    res = {"plan": {int(k): list(v) for k, v in car.plan.items()}, "rep": {int(k): v for k, v in rep.items()},
+           "for_40": list(car.plan_for(40, H)), "for_5000": list(car.plan_for(5000, H)), "status": car.status()}
+    car.close()
+    torch.save(res, os.path.join(out_dir, f"tune{rank}.pt"))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_xgmi_epilogue_tuning_same_plan_on_every_rank():
+    """the init-time fabric tuning times one-/two-shot (and
+    push where the GEMM allows it) per bucket and every rank gets the SAME plan
+    (a rank-dependent mode would deadlock the collective); buckets past the
+    buffer are skipped and T above the largest bucket falls back to the size
+    rule."""
+    if not torch.cuda.is_available():
+        pytest.skip("needs a GPU")
+    with tempfile.TemporaryDirectory() as d:
+        mp.spawn(_tune_worker, args=(2, _free_port(), d), nprocs=2, join=True)
+        a = torch.load(os.path.join(d, "tune0.pt"), weights_only=True)
+        b = torch.load(os.path.join(d, "tune1.pt"), weights_only=True)
+    assert a["status"] == 0 and b["status"] == 0
+    assert a["plan"] == b["plan"] and set(a["plan"]) == {16, 64, 256}   # 4096 x 4096 x 2 B > 16 MiB
+    assert a["for_40"] == a["plan"][64]
+    assert a["for_5000"] == [2, False]
+    for T, r in a["rep"].items():
+        assert "one_shot" in r and "two_shot" in r and all(v > 0 for k, v in r.items() if k != "pick")

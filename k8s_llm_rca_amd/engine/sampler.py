@@ -174,12 +174,12 @@ class SamplerMixin:
     # ------------------------------------------------------------ sampling
     def _mask_table(self) -> Optional[torch.Tensor]:
         if self._mask_ver != self.grt.masks.version:
-            arr = self.grt.masks.array()
+            ver, arr = self.grt.masks.snapshot()  # version and rows together (MaskTable.snapshot)
             host = torch.from_numpy(arr)
             if self.device.type == "cuda":  # pinned + non-blocking: a pageable copy would wait for the GPU
                 host = host.pin_memory()
             self._mask_dev = host.to(self.device, non_blocking=True)
-            self._mask_ver = self.grt.masks.version
+            self._mask_ver = ver
         return self._mask_dev
 
     def _launch_sample(self, logits: torch.Tensor, seqs: List[Sequence], rows: Optional[List[int]] = None) -> InFlight:
@@ -221,6 +221,10 @@ class SamplerMixin:
                                   seeds, steps, temps, topk, topp, rows)
         else:
             table = self._mask_table()
+            if table is not None and int(mask_id.max(initial=-1)) >= table.shape[0]:
+                # a bitmap row the device mirror does not hold: sampling would read past
+                # the table (garbage bits, silently ended runs) -- fail loudly instead
+                raise RuntimeError(f"grammar mask row {int(mask_id.max())} >= device table rows {table.shape[0]}")
             arrays = [mask_id, list_off, list_len, np.asarray(lists, np.int32), seeds, steps, temps.view(np.int32)]
             if filt:
                 arrays += [topk, topp.view(np.int32)]

@@ -50,10 +50,17 @@ class MaskTable:
             return r
 
     def array(self) -> np.ndarray:
+        return self.snapshot()[1]
+
+    def snapshot(self):
+        """(version, [rows, words] array) taken together: a version read apart
+        from the rows can name a row the array does not hold yet (a mask
+        registered by another thread in between), and the device mirror would
+        then never be refreshed for it."""
         with self.lock:
             if not self.rows:
-                return np.zeros((1, self.words), dtype=np.int32)
-            return np.stack(self.rows)
+                return self.version, np.zeros((1, self.words), dtype=np.int32)
+            return self.version, np.stack(self.rows)
 
 
 class GrammarRuntime:

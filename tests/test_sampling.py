@@ -172,3 +172,44 @@ def test_sampler_flags_nonfinite_rows_kernel():
                          a["list_len"], a["lists"], V)
         assert got.cpu().tolist()[:3] == [SMP.NON_FINITE] * 3
         assert torch.equal(got.cpu()[3:], ref[3:])
+
+
+def test_mask_mirror_never_skips_a_row_registered_during_upload():
+    """The device mirror of the grammar bitmaps (SamplerMixin._mask_table) used
+    to read the table's rows and THEN its version: a row registered by another
+    thread in between was counted as uploaded, so the mirror was never
+    refreshed for it and sampling read past the table (garbage bits: runs that
+    end at once with no error).  Rows and version are now taken together."""
+    import numpy as np
+    import torch
+    from k8s_llm_rca_amd.engine.sampler import SamplerMixin
+    from k8s_llm_rca_amd.engine.structured import MaskTable
+
+    mt = MaskTable(64)
+    mt.get(("a",), lambda: np.ones(64, bool))
+
+    class Racy(MaskTable):
+        fired = False
+
+        def snapshot(self):
+            out = super().snapshot()
+            if not Racy.fired:  # another thread registers a mask right after the rows were stacked
+                Racy.fired = True
+                self.get(("b",), lambda: np.zeros(64, bool))
+            return out
+
+    racy = Racy(64)
+    racy.get(("a",), lambda: np.ones(64, bool))
+
+    class G:
+        masks = racy
+
+    class Eng(SamplerMixin):
+        def __init__(self):
+            self.grt, self.device, self._mask_ver, self._mask_dev = G(), torch.device("cpu"), -1, None
+
+    e = Eng()
+    t1 = e._mask_table()
+    assert t1.shape[0] == 1 and racy.version == 2
+    t2 = e._mask_table()  # the version it recorded is the rows', so the new row is picked up now
+    assert t2.shape[0] == 2

@@ -95,6 +95,11 @@ __device__ __forceinline__ float block_max(float v, float* scratch) {
 // "rewrites" the fragments it covers so the MFMA cannot be hoisted above it
 // (cdna_hip_programming.md §5.7: an asm statement's memory traffic is not modelled).
 template <int OFF>
+// Hand-issued ds_read_b128 for counted lgkmcnt waits (lgkm_wait<N>): the
+// caller must keep scalar memory loads out of the window between its reads and
+// their waits (lgkmcnt counts them too, out of order) -- a sched_barrier(0)
+// before the read block and after the consuming MFMAs (gemm_stream.hip
+// glds_strip, attention.hip's page loop).
 __device__ __forceinline__ bf16x8 lds_rd16(uint32_t addr) {
   bf16x8 v;
   asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(v) : "v"(addr), "i"(OFF) : "memory");

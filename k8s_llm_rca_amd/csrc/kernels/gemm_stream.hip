@@ -298,6 +298,14 @@ __device__ __forceinline__ void glds_strip(const uint16_t* __restrict__ x, int l
       const uint32_t wb = lds0 + 2u * (uint32_t)(stage * STG), xb = wb + 2u * WST;
 #pragma unroll
       for (int s = 0; s < 2; ++s) {
+        // the counted lgkmcnt waits of glds_mm assume every lgkm operation
+        // between these reads and their waits is one of these ds_reads: a scalar
+        // load scheduled into the window (it also counts on lgkmcnt, and returns
+        // out of order) would let a wait pass before its fragment landed.  No
+        // instruction from before the block may move into it (this barrier), and
+        // none from after it (glds_mm's barrier behind each column's MFMAs);
+        // the reads' own addresses are VALU / SALU arithmetic.
+        __builtin_amdgcn_sched_barrier(0);
         bf16x8 xf[MTW], wf[NF];
 #pragma unroll
         for (int mt = 0; mt < MTW; ++mt) {

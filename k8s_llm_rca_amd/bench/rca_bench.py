@@ -276,6 +276,7 @@ def run(args) -> Optional[Dict[str, Any]]:
     eng = LLMEngine(EngineConfig(model=args.model, device=str(device),
                                  dtype=torch.bfloat16 if cuda else torch.float32,
                                  kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,
+                                 max_context=args.max_context,
                                  use_graphs=cuda and not args.no_graphs, prefix_sharing=not args.no_prefix_sharing,
                                  seed=args.seed + (0 if tp_mode else rank),
                                  num_blocks=None if cuda else 512), pc)
@@ -589,6 +590,9 @@ def parser() -> argparse.ArgumentParser:
                    help="keep the graphs on the host (default on GPU: HBM mirror + batched HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
+    p.add_argument("--max-context", type=int, default=None,
+                   help="serving window (tokens) a thread is cut at (default: the model's own window); "
+                        "reported in config.truncation")
     p.add_argument("--max-batch-tokens", type=int,
                    default=KNOBS.max_batch_tokens)
     p.add_argument("--temperature", type=float, default=0.7)

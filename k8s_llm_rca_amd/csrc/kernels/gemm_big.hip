@@ -704,18 +704,19 @@ static void tail_plan(int T, int nt, int& r, int& S) {
 
 // Stream-K instead of waves + split tail, when it is shorter: time in tile
 // units -- waves: the full waves plus the tail's 1/S of a tile; stream-K: T ku
-// units spread over the CUs plus the fixup (the last contributor of a split
-// tile reads the other partials: ~1/20 of a tile each, at most 3 contributors,
-// i.e. each CU's share is at least half a tile).  Measured per shape with
+// units spread over the CUs plus the fixup: the last contributor of a split
+// tile reads the other partials (a 256 KB slab, ~3 us against a ~97 us tile at
+// K = 4096, so ~128 / K tiles) and at most 3 contribute (each CU's share is at
+// least half a tile).  Measured per shape with
 // tools/big_gemm_ab.py (profiles/r5/stream_k/); knob big_stream_k = 0 disables
 // it (A/B, read per launch).
 static long g_sk_launches = 0;
-static bool sk_better(int T, int ku, int tr, int ts) {
+static bool sk_better(int T, int ku, int tr, int ts, int K) {
   if (T % kCUs == 0 || T > kTickets || ku < 2) return false;
   const long units = (long)T * ku;
   if (units < (long)kCUs * ku / 2) return false;  // > 3 contributors per tile: the fixup would dominate
   const double waves = (double)((T - tr) / kCUs) + ((T - tr) % kCUs ? 1.0 : 0.0) + (tr ? 1.0 / ts : 0.0);
-  const double sk = (double)units / kCUs / ku + 0.1;
+  const double sk = (double)units / kCUs / ku + 0.05 + 128.0 / K;
   return sk < 0.97 * waves;
 }
 
@@ -748,7 +749,7 @@ static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M
     }
   }
   const int ku = K / BK / 2;  // 128-deep K units per tile
-  if (tws && knob(kKnobBigStreamK) && sk_better(T, ku, tr, ts)) {
+  if (tws && knob(kKnobBigStreamK) && sk_better(T, ku, tr, ts, K)) {
     hipLaunchKernelGGL((gemm_big_kernel<MODE, VAR, true>), dim3(kCUs), dim3(512), 0, s, (const uint16_t*)x, ldx,
                        (const uint16_t*)w, (uint16_t*)y, ldy, M, N, K, n_mt, n_nt, 1, (float*)nullptr, 0, 1, tws,
                        tick, (const int*)nullptr, 0, g_rope, T * ku, ku);

@@ -1052,17 +1052,22 @@ def test_gemm_big_split_tail_owned_by_one_stream():
 
 @pytest.mark.parametrize("pipe", [1, 5])
 @pytest.mark.parametrize("M,I,K", [(5, 128, 128), (300, 384, 512), (1500, 1024, 4096), (4100, 14336, 256)])
-def test_gemm_big_silu_epilogue(M, I, K, pipe):
+def test_gemm_big_silu_epilogue(M, I, K, pipe, knob):
     """SwiGLU epilogue of gemm_big (gate_up never written) == the unfused
-    gemm_big + silu_mul bit for bit, and fp32 silu(x Wg^T) * (x Wu^T)."""
+    gemm_big + silu_mul bit for bit on whole tiles (stream-K off: the two forms
+    tile the columns differently, so their split points differ), and fp32
+    silu(x Wg^T) * (x Wu^T) with the default schedule."""
     _need_gpu()
     from k8s_llm_rca_amd.ops import linear as LIN
     torch.manual_seed(M + I)
     x = torch.randn(M, K, device=dev).bfloat16()
     w = (torch.randn(2 * I, K, device=dev) * 0.05).bfloat16()
+    act_sk = LIN.gemm_big(x, w, silu=True, pipe=pipe)
+    knob("big_stream_k", False)
     act = LIN.gemm_big(x, w, silu=True, pipe=pipe)
     gu = LIN.gemm_big(x, w, pipe=pipe)
     assert torch.equal(act, N.silu_mul(gu))
+    torch.testing.assert_close(act_sk.float(), act.float(), atol=2e-2, rtol=2e-2)
     g, u = (x.float() @ w.float().t()).split(I, dim=1)
     torch.testing.assert_close(act.float(), torch.nn.functional.silu(g) * u, atol=3e-2, rtol=3e-2)
 

@@ -76,7 +76,6 @@
 #include <type_traits>
 
 #include "common.h"
-#include "knobs.h"
 
 namespace k8s {
 namespace big {
@@ -190,14 +189,13 @@ struct RopeArgs {
 // VAR bit 0: ping-pong stagger of waves
 // 4-7; bit 1: s_setprio(1) around the MFMA clusters; bit 2: the 32x32x16 MFMA
 // (1 = the default).
-template <int MODE, int VAR, bool SK = false>
+template <int MODE, int VAR>
 __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __restrict__ x, int ldx,
                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                           int ldy, int M, int N, int K, int n_mt, int n_nt, int splits,
                                                           float* __restrict__ part, int tail_tiles, int tail_split,
                                                           float* __restrict__ tws, int* __restrict__ tick,
-                                                          const int* __restrict__ goffs, int G, RopeArgs ra,
-                                                          int sk_units = 0, int sk_ku = 1) {
+                                                          const int* __restrict__ goffs, int G, RopeArgs ra) {
   constexpr int SH = (VAR & 4) ? 32 : 16;
   using GG = Geo<SH>;
   using acc_t = typename GG::acc_t;
@@ -206,51 +204,19 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __rest
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wr = wv >> 2, wc = wv & 3;
-  // bijective XCD remap of id b within [0, n): blocks b, b+8, ... (one XCD under
-  // round-robin placement) get a contiguous id range
-  auto remap = [](int b, int n) {
-    const int xcd = b & 7, q = n >> 3, r = n & 7;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
-  };
-
-  // ---- stream-K (SK): the grid (one workgroup per CU) splits the T tiles x
-  // sk_ku 128-deep K units evenly; workgroup p (XCD-contiguous logical id) owns
-  // units [p U / P, (p+1) U / P) -- a partial first tile, whole tiles, a
-  // partial last tile.  A whole tile runs the normal epilogue; a partial one
-  // publishes its fp32 partial to slot 2p (its first tile) / 2p+1 (its last)
-  // and the tile's last contributor sums every contributor's partial in
-  // workgroup order (deterministic) before the epilogue.
-  [[maybe_unused]] int sk_p = 0, sk_u = 0, sk_end = 0, sk_t0 = 0;
-  if constexpr (SK) {
-    sk_p = remap(blockIdx.x, gridDim.x);
-    sk_u = (int)((long)sk_p * sk_units / gridDim.x);
-    sk_end = (int)((long)(sk_p + 1) * sk_units / gridDim.x);
-    sk_t0 = sk_u / sk_ku;
-  }
-  for (;;) {
-  [[maybe_unused]] int seg_t = 0, seg_k0 = 0, seg_nk = 0;
-  [[maybe_unused]] bool seg_full = true;
-  if constexpr (SK) {
-    if (sk_u >= sk_end) return;
-    seg_t = sk_u / sk_ku;
-    const int s1 = min(sk_end, (seg_t + 1) * sk_ku);
-    seg_k0 = 2 * (sk_u - seg_t * sk_ku);
-    seg_nk = 2 * (s1 - sk_u);
-    seg_full = sk_u == seg_t * sk_ku && s1 == (seg_t + 1) * sk_ku;
-    sk_u = s1;
-    __syncthreads();  // every wave is done with the previous segment's LDS (the flag word included)
-  }
 
   // ---- tile of this workgroup: XCD-contiguous remap, then grouped order
   int tm, tn, slice, nsl = splits, tt = -1;  // tt: tail tile index (split tail), else -1
   {
+    // bijective XCD remap of id b within [0, n): blocks b, b+8, ... (one XCD under
+    // round-robin placement) get a contiguous id range
+    auto remap = [](int b, int n) {
+      const int xcd = b & 7, q = n >> 3, r = n & 7;
+      return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (b >> 3);
+    };
     const int T = n_mt * n_nt, F = T - tail_tiles, b = blockIdx.x;
     int t;
-    if constexpr (SK) {
-      t = seg_t;
-      slice = 0;
-      nsl = 1;
-    } else if (splits > 1) {  // uniform split-K: units of one tile consecutive
+    if (splits > 1) {  // uniform split-K: units of one tile consecutive
       const int t0 = remap(b, T * splits);
       slice = t0 % splits;
       t = t0 / splits;
@@ -305,7 +271,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __rest
       wsrc[h][i] = w + (size_t)w_row<MODE, SH>(tn, h, R >> 5, R & 31, N) * K + 8 * lch;
     }
   }
-  const int nt = SK ? seg_nk : K / BK / nsl, kt0 = SK ? seg_k0 : slice * nt;  // this workgroup's K tiles
+  const int nt = K / BK / nsl, kt0 = slice * nt;  // this workgroup's K tiles
   auto issue = [&](const uint16_t* const* src, int lds_off, int kt) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) glds16(src[i] + (kt0 + kt) * BK, sm + lds_off + (2 * wv + i) * 1024);
@@ -419,66 +385,6 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __rest
         }
   };
 
-  if constexpr (SK) {
-    if (!seg_full) {
-      const int P = gridDim.x, U = sk_units;
-      auto owner = [&](int u) { return (int)(((long)(u + 1) * P + U - 1) / U) - 1; };
-      auto slot_of = [&](int c) { return 2 * c + (seg_t == (int)((long)c * U / P) / sk_ku ? 0 : 1); };
-      const int c0 = owner(seg_t * sk_ku), c1 = owner((seg_t + 1) * sk_ku - 1);
-      const size_t lane_off = (size_t)(wv * 32 * 64 + lane) * 4;
-      float* mine = tws + (size_t)(2 * sk_p + (seg_t == sk_t0 ? 0 : 1)) * (BM * BN) + lane_off;
-      for_chunks([&](acc_t& a, int k0) {
-        *reinterpret_cast<f32x4*>(mine + (k0 + 0) * 256) = chunk<0>(a);
-        if constexpr (NC == 4) {
-          *reinterpret_cast<f32x4*>(mine + (k0 + 1) * 256) = chunk<1>(a);
-          *reinterpret_cast<f32x4*>(mine + (k0 + 2) * 256) = chunk<2>(a);
-          *reinterpret_cast<f32x4*>(mine + (k0 + 3) * 256) = chunk<3>(a);
-        }
-      });
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      int* flag = reinterpret_cast<int*>(sm);
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        const int old = __hip_atomic_fetch_add(tick + seg_t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        const int last = old == c1 - c0;
-        if (last) {
-          __hip_atomic_store(tick + seg_t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // ready for the next launch
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-        flag[0] = last;
-      }
-      __syncthreads();
-      if (!flag[0]) continue;  // another contributor finishes this tile
-      // every contributor's partial (this one's too, from memory) in workgroup order
-#pragma unroll
-      for (int hk = 0; hk < 2; ++hk) {
-        f32x4 s[16];
-#pragma unroll
-        for (int c = 0; c < 16; ++c) s[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-        for (int cc = c0; cc <= c1; ++cc) {
-          const float* src = tws + (size_t)slot_of(cc) * (BM * BN) + lane_off;
-          f32x4 t[16];
-#pragma unroll
-          for (int c = 0; c < 16; ++c) t[c] = *reinterpret_cast<const f32x4*>(src + (16 * hk + c) * 256);
-#pragma unroll
-          for (int c = 0; c < 16; ++c) s[c] += t[c];
-        }
-        for_chunks([&](acc_t& a, int k0) {
-          if (k0 >= 16 * hk && k0 < 16 * hk + 16) {
-            set_chunk<0>(a, s[k0 - 16 * hk]);
-            if constexpr (NC == 4) {
-              set_chunk<1>(a, s[k0 - 16 * hk + 1]);
-              set_chunk<2>(a, s[k0 - 16 * hk + 2]);
-              set_chunk<3>(a, s[k0 - 16 * hk + 3]);
-            }
-          }
-        });
-      }
-    }
-  }
   if (tt >= 0) {
     // split tail: publish this unit's partial; the last of the tile's units sums them
     float* mine = tws + ((size_t)tt * nsl + slice) * (BM * BN) + (size_t)(wv * 32 * 64 + lane) * 4;
@@ -644,8 +550,6 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(const uint16_t* __rest
       }
     }
   }
-  if constexpr (!SK) return;
-  }  // segment loop (one trip unless SK)
 }
 
 // Y[m][n] = bf16(sum_s part[s][m][n]) (slice order); 8 outputs per thread.
@@ -679,10 +583,7 @@ __global__ void __launch_bounds__(256) big_reduce_kernel(const float* __restrict
 // stream runs without the split tail (whole-tile last wave: slower, never
 // wrong).  k8s_gemm_big_set_ws releases the claim.  
 constexpr int kTailUnits = 256;
-// partial slots: the split tail's r x S units (<= 256), or stream-K's two per
-// workgroup (the grid is one workgroup per CU: 2 x 256); tickets: one per tile
-constexpr int kSlots = 512, kTickets = 4096, kCUs = 256;
-constexpr size_t kTailWsBytes = (size_t)kSlots * BM * BN * 4 + kTickets * 4;
+constexpr size_t kTailWsBytes = (size_t)kTailUnits * BM * BN * 4 + kTailUnits * 4;
 static void* g_tail_ws[16] = {};
 static hipStream_t g_tail_owner[16] = {};
 static bool g_tail_claimed[16] = {};
@@ -700,24 +601,6 @@ static void tail_plan(int T, int nt, int& r, int& S) {
       break;
     }
   if (S == 1) r = 0;
-}
-
-// Stream-K instead of waves + split tail, when it is shorter: time in tile
-// units -- waves: the full waves plus the tail's 1/S of a tile; stream-K: T ku
-// units spread over the CUs plus the fixup: the last contributor of a split
-// tile reads the other partials (a 256 KB slab, ~3 us against a ~97 us tile at
-// K = 4096, so ~128 / K tiles) and at most 3 contribute (each CU's share is at
-// least half a tile).  Measured per shape with
-// tools/big_gemm_ab.py (profiles/r5/stream_k/); knob big_stream_k = 0 disables
-// it (A/B, read per launch).
-static long g_sk_launches = 0;
-static bool sk_better(int T, int ku, int tr, int ts, int K) {
-  if (T % kCUs == 0 || T > kTickets || ku < 2) return false;
-  const long units = (long)T * ku;
-  if (units < (long)kCUs * ku / 2) return false;  // > 3 contributors per tile: the fixup would dominate
-  const double waves = (double)((T - tr) / kCUs) + ((T - tr) % kCUs ? 1.0 : 0.0) + (tr ? 1.0 / ts : 0.0);
-  const double sk = (double)units / kCUs / ku + 0.05 + 128.0 / K;
-  return sk < 0.97 * waves;
 }
 
 // MODE 2's epilogue arguments for the next launch (set by k8s_gemm_big_rope;
@@ -744,17 +627,9 @@ static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M
       } else {
         tail_plan(T, K / BK, tr, ts);
         tws = (float*)g_tail_ws[dev];
-        tick = (int*)((char*)g_tail_ws[dev] + (size_t)kSlots * BM * BN * 4);
+        tick = (int*)((char*)g_tail_ws[dev] + (size_t)kTailUnits * BM * BN * 4);
       }
     }
-  }
-  const int ku = K / BK / 2;  // 128-deep K units per tile
-  if (tws && knob(kKnobBigStreamK) && sk_better(T, ku, tr, ts, K)) {
-    hipLaunchKernelGGL((gemm_big_kernel<MODE, VAR, true>), dim3(kCUs), dim3(512), 0, s, (const uint16_t*)x, ldx,
-                       (const uint16_t*)w, (uint16_t*)y, ldy, M, N, K, n_mt, n_nt, 1, (float*)nullptr, 0, 1, tws,
-                       tick, (const int*)nullptr, 0, g_rope, T * ku, ku);
-    ++g_sk_launches;
-    return (int)hipGetLastError();
   }
   const int grid = splits > 1 ? T * splits : T - tr + tr * ts;
   hipLaunchKernelGGL((gemm_big_kernel<MODE, VAR>), dim3(grid), dim3(512), 0, s, (const uint16_t*)x, ldx,
@@ -838,8 +713,6 @@ K8S_API int k8s_gemm_big_set_ws(void* ws) {
   k8s::big::g_tail_claimed[dev] = false;  // the next launch that uses it claims it for its stream
   return 0;
 }
-// launches that took the stream-K form (tests / diagnostics)
-K8S_API long k8s_gemm_big_sk_launches() { return k8s::big::g_sk_launches; }
 // launches on this device that ran without the split tail because another
 // stream owns the workspace (test / diagnostics)
 K8S_API long k8s_gemm_big_tail_foreign() {

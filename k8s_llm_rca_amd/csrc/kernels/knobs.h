@@ -10,7 +10,6 @@ enum Knob : int {
   kKnobPfW8 = 2,            // attention.hip: prefill kernel variant (6; 1 = the default, 0 = pg64)
   kKnobPfMerge16 = 3,       // attention.hip: 16-B merge for bf16 partials (1)
   kKnobArFenceAll = 4,      // allreduce.hip: system fence in every wave (0)
-  kKnobBigStreamK = 5,      // gemm_big.hip: stream-K where it beats waves + split tail (1)
   kKnobCount = 8
 };
 int knob(int id);

@@ -4,7 +4,7 @@
 #include "knobs.h"
 
 namespace k8s {
-static int g_knobs[kKnobCount] = {1, 1, 6, 1, 0, 1, 0, 0};
+static int g_knobs[kKnobCount] = {1, 1, 6, 1, 0, 0, 0, 0};
 int knob(int id) { return (id >= 0 && id < kKnobCount) ? g_knobs[id] : 0; }
 }  // namespace k8s
 

@@ -53,7 +53,6 @@ class Knobs:
     big_gemm: str = _f("1", "prefill GEMMs on gemm_big where measured faster; 0 off, 'all' everywhere it fits")
     big_var: int = _f(1, "gemm_big schedule variant (1 ping-pong, 3 + setprio, 5/7 32x32 MFMA)")
     big_tail: bool = _f(True, "gemm_big split-tail (stream-K last wave) workspace")
-    big_stream_k: bool = _f(True, "gemm_big: whole-grid stream-K where it beats waves + split tail", native=5)
     stream_silu: bool = _f(True, "SwiGLU epilogue on the decode stream GEMM's gate_up")
     glds_hand: bool = _f(True, "hand-issued LDS reads in the LDS-DMA decode GEMM", native=0)
     # ---------------------------------------------------------------- attention (ops/attention.py)

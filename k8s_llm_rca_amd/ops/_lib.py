@@ -73,7 +73,6 @@ _SIGS = {
     "k8s_set_knob": [I, I],
     "k8s_nonfinite_flag": [P, ctypes.c_long, P, P],
     "k8s_get_knob": [I],
-    "k8s_gemm_big_sk_launches": [],
     "k8s_walks": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P],
 }
 

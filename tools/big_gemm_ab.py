@@ -25,7 +25,6 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 
 import torch  # noqa: E402
 
-from k8s_llm_rca_amd.knobs import set_knob  # noqa: E402
 from k8s_llm_rca_amd.ops import linear as LIN  # noqa: E402
 from k8s_llm_rca_amd.ops import norm as NRM  # noqa: E402
 
@@ -54,7 +53,6 @@ def main():
     ap.add_argument("--margin", type=float, default=-0.03)
     ap.add_argument("--model", default="llama3-8b", help="projection shapes of this preset (per TP rank)")
     ap.add_argument("--tp", type=int, default=1)
-    ap.add_argument("--nosk", action="store_true", help="also time gemm_big with stream-K off (A/B arm 'nosk')")
     a = ap.parse_args()
     dev = torch.device("cuda")
     from k8s_llm_rca_amd.models.config import get_config
@@ -73,12 +71,6 @@ def main():
             arms = {"blaslt": lambda i: LIN.lib_gemm(x, ws[i % a.layers], y)}
             for p in pipes:
                 arms[f"big{p}"] = lambda i, p=p: LIN.gemm_big(x, ws[i % a.layers], y, pipe=p)
-            if a.nosk:  # the same kernel with stream-K off (waves + split tail), for the A/B only
-                def nosk(i, p=pipes[0]):
-                    set_knob("big_stream_k", False)
-                    LIN.gemm_big(x, ws[i % a.layers], y, pipe=p)
-                    set_knob("big_stream_k", True)
-                arms["nosk"] = nosk
             for sp in (int(v) for v in a.splits.split(",") if v):
                 tiles = -(-M // 256) * (N // 256)
                 if LIN.big_shape_ok(M, N, K, splits=sp) and tiles < 256:
@@ -103,12 +95,6 @@ def main():
                 arms["blaslt+silu"] = lambda i: NRM.silu_mul(LIN.lib_gemm(x, ws[i % a.layers], y), out=act)
                 for p in pipes:
                     arms[f"big{p}_silu"] = lambda i, p=p: LIN.gemm_big(x, ws[i % a.layers], act, silu=True, pipe=p)
-                if a.nosk:
-                    def nosk_silu(i, p=pipes[0]):
-                        set_knob("big_stream_k", False)
-                        LIN.gemm_big(x, ws[i % a.layers], act, silu=True, pipe=p)
-                        set_knob("big_stream_k", True)
-                    arms["nosk_silu"] = nosk_silu
             for fn in arms.values():  # warm-up (heuristics, code objects)
                 fn(0)
             torch.cuda.synchronize()

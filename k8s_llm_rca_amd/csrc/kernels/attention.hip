@@ -85,6 +85,16 @@ struct RowState {
 };
 
 __device__ __forceinline__ bf16x8 load16(const uint16_t* p) { return *reinterpret_cast<const bf16x8*>(p); }
+// the decode KV stream's loads: default policy, or non-temporal (NT, knob
+// decode_kv_nt) -- MI355X_MICROARCH.md measures nt weight streams at 6.5-6.8
+// TB/s against 6.4 with the default policy
+template <bool NT>
+__device__ __forceinline__ bf16x8 load16k(const uint16_t* p) {
+  if constexpr (NT)
+    return __builtin_nontemporal_load(reinterpret_cast<const bf16x8*>(p));
+  else
+    return *reinterpret_cast<const bf16x8*>(p);
+}
 
 __device__ __forceinline__ bf16x8 zero8() {
   bf16x8 z;
@@ -188,6 +198,7 @@ __device__ __forceinline__ void init_state(RowState& st, const AttnArgs& a, int 
 // always has the next chunk's 16-32 KB in flight while it computes (a plain
 // load -> wait -> compute loop leaves the wave's memory pipe idle during
 // compute and decode is bound by bytes in flight per CU).
+template <bool NT>
 __device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs& a, int blk, int kvh, int kb,
                                            int lane) {
   const int r = lane & 15, h = lane >> 4;
@@ -200,10 +211,11 @@ __device__ __forceinline__ void dec_load_k(bf16x8 (&kf)[2][2][4], const AttnArgs
     for (int t = 0; t < 2; ++t) {
       const int key = off + 32 * u + 8 * (r >> 2) + 4 * t + (r & 3);
 #pragma unroll
-      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16(kp + (size_t)key * D + 32 * c + 8 * h);
+      for (int c = 0; c < 4; ++c) kf[u][t][c] = load16k<NT>(kp + (size_t)key * D + 32 * c + 8 * h);
     }
 }
 
+template <bool NT>
 __device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a, int blk, int kvh, int kb,
                                            int lane) {
   const int r = lane & 15, h = lane >> 4;
@@ -213,7 +225,7 @@ __device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a
 #pragma unroll
   for (int u = 0; u < 2; ++u)
 #pragma unroll
-    for (int dt = 0; dt < 8; ++dt) vf[u][dt] = load16(vp + (size_t)(16 * dt + r) * a.BS + off + 32 * u + 8 * h);
+    for (int dt = 0; dt < 8; ++dt) vf[u][dt] = load16k<NT>(vp + (size_t)(16 * dt + r) * a.BS + off + 32 * u + 8 * h);
 }
 
 // `blkv`: lane j holds the block id of the partition's j-th page (fetched
@@ -222,6 +234,7 @@ __device__ __forceinline__ void dec_load_v(bf16x8 (&vf)[2][8], const AttnArgs& a
 // `k1`: end key of the item (wave-uniform); `lim`: this lane's row sees keys
 // < lim (== k1 except for the earlier tokens of a multi-token item);
 // `kmin`: the smallest row limit of the wave (tail masking starts there).
+template <bool NT>
 __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a, int blkv, int kvh, int k0,
                                                 int k1, int kmin, int lim, int lane) {
   const int h = lane >> 4;
@@ -230,8 +243,8 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
   bf16x8 kf[2][2][4], vf[2][8];
   {
     const int b0 = __builtin_amdgcn_readfirstlane(blkv);
-    dec_load_k(kf, a, b0, kvh, k0, lane);
-    dec_load_v(vf, a, b0, kvh, k0, lane);
+    dec_load_k<NT>(kf, a, b0, kvh, k0, lane);
+    dec_load_v<NT>(vf, a, b0, kvh, k0, lane);
   }
   for (int c = 0; c < nch; ++c) {
     const int kb = k0 + 64 * c;
@@ -247,7 +260,7 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
         for (int q = 0; q < 4; ++q) acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf[u][t][q], st.qf[q], acc, 0, 0, 0);
         sc[u][t] = acc;
       }
-    dec_load_k(kf, a, bn, kvh, kbn, lane);
+    dec_load_k<NT>(kf, a, bn, kvh, kbn, lane);
     float cmax = -INFINITY;
     if (kb + 64 > kmin) {  // tail chunk: keys >= the row's limit are not visible to it
 #pragma unroll
@@ -299,7 +312,7 @@ __device__ __forceinline__ void decode_stream64(RowState& st, const AttnArgs& a,
     for (int dt = 0; dt < 8; ++dt)
 #pragma unroll
       for (int u = 0; u < 2; ++u) st.o[dt] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(pf[u], vf[u][dt], st.o[dt], 0, 0, 0);
-    dec_load_v(vf, a, bn, kvh, kbn, lane);
+    dec_load_v<NT>(vf, a, bn, kvh, kbn, lane);
   }
 }
 
@@ -412,6 +425,7 @@ __device__ __forceinline__ void decode_epilogue(const RowState& st, const AttnAr
 // each (row group, kv head), K8SRCA_DECODE_MERGE=1: its per-item ticket cost
 // what the separate reduce launch saves -- profiles/r2_decode_merge/ -- and it
 // was retired in round 4; attn_reduce_kernel merges.)
+template <bool NT>
 __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
   const int lane = threadIdx.x;
   const int r = lane & 15;
@@ -442,7 +456,7 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
     }
     RowState st;
     init_state(st, a, qrow + (valid ? qi : 0), kvh * a.G + (valid ? r - qi * a.G : 0), valid, lane);
-    decode_stream64(st, a, blkv, kvh, k0, k1, kmin, lim, lane);
+    decode_stream64<NT>(st, a, blkv, kvh, k0, k1, kmin, lim, lane);
     decode_epilogue(st, a, seq, part, qrow, kvh, whole, nt, lane);
   }
 }
@@ -1325,7 +1339,10 @@ K8S_API int k8s_attn_decode(const void* q, int q_stride, const void* kc, const v
     a.items = reinterpret_cast<const int4*>(items);
     a.n_items = n_items;
     a.d_n_items = d_n_items;
-    hipLaunchKernelGGL(attn_decode_items_kernel, dim3(grid_waves), dim3(64), 0, stream, a);
+    if (knob(kKnobDecodeKvNt))
+      hipLaunchKernelGGL(attn_decode_items_kernel<true>, dim3(grid_waves), dim3(64), 0, stream, a);
+    else
+      hipLaunchKernelGGL(attn_decode_items_kernel<false>, dim3(grid_waves), dim3(64), 0, stream, a);
   } else {
     const long nw = (long)S * nkv * n_parts;
     hipLaunchKernelGGL(attn_decode_kernel, dim3((unsigned)nw), dim3(64), 0, stream, a, S);

@@ -10,6 +10,7 @@ enum Knob : int {
   kKnobPfW8 = 2,            // attention.hip: prefill kernel variant (6; 1 = the default, 0 = pg64)
   kKnobPfMerge16 = 3,       // attention.hip: 16-B merge for bf16 partials (1)
   kKnobArFenceAll = 4,      // allreduce.hip: system fence in every wave (0)
+  kKnobDecodeKvNt = 5,      // attention.hip: non-temporal K/V loads in the decode stream (0)
   kKnobCount = 8
 };
 int knob(int id);

@@ -206,6 +206,9 @@ def test_paged_decode(nq, nkv, ctx, BS, monkeypatch, knob):
         knob("decode_reduce_pre", pre != "0")
         outs[pre] = A.paged_attention(q, kc, vc, meta, nq, nkv, scale)
     assert torch.equal(outs["1"], outs["0"])
+    # the non-temporal K/V stream (knob decode_kv_nt) only changes the cache policy
+    knob("decode_kv_nt", True)
+    assert torch.equal(A.paged_attention(q, kc, vc, meta, nq, nkv, scale), outs["0"])
 
 
 @pytest.mark.parametrize("nq,nkv", [(32, 8), (64, 8), (8, 1)])

@@ -61,7 +61,8 @@ class Knobs:
                             legacy="K8S_DECODE_GROUP")
     decode_reduce_pre: bool = _f(True, "decode split-KV reduce: register-prefetch form for <= 16 partitions",
                                  native=1)
-    decode_kv_nt: bool = _f(False, "non-temporal K/V loads in the decode attention stream (A/B)", native=5)
+    decode_kv_nt: bool = _f(False, "non-temporal K/V loads in the decode attention stream (A/B: 5.6 % slower on "
+                                   "the contract run's decode steps, profiles/r5/decode_nt/)", native=5)
     pf_w8: int = _f(6, "prefill attention kernel: 6 (default) / 5 / 4 / 2 8-wave variants, 0 the 4-wave pg64",
                     native=2)
     pf_merge16: bool = _f(True, "prefill split-KV merge at 16 B per lane for bf16 partials", native=3)

@@ -49,7 +49,7 @@ def main():
             ls = a.shared // BS
             bt = meta.block_tables.cpu()
             for s0 in range(0, B, 42):
-                bt[s0:s0 + 42, :ls] = bt[s0, :ls]
+                bt[s0:s0 + 42, :ls] = bt[s0, :ls].clone()
             meta.block_tables = bt.to(dev)
         kc = torch.empty(nb, nkv, BS, 128, device=dev, dtype=torch.bfloat16).normal_()
         vc = torch.empty(nb, nkv, 128, BS, device=dev, dtype=torch.bfloat16).normal_()

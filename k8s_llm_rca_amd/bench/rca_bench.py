@@ -635,6 +635,10 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # (1.34 M tokens): 754 preemptions, 36k prefill tokens per analysis, 0.77 /s
     # (profiles/r3/presets/mixtral_128.json) -- 48 concurrent analyses fit
     "mixtral-10k": dict(model="mixtral-8x7b", graph_nodes=10_000, thread_age=4, incidents=48, quantum=6),
+    # the same model served with an 8k window (config.truncation.max_context): threads are cut
+    # where Llama-3's are, the steady state is reachable (12 pre-aged incidents) and 64 pipelines'
+    # KV fits beside the experts -- 1.74 /s at p50 30.5 s, 0 preemptions (profiles/r5/mixtral_8k/)
+    "mixtral-10k-8k": dict(model="mixtral-8x7b", graph_nodes=10_000, max_context=8192, incidents=64, quantum=8),
 }
 
 

@@ -117,8 +117,11 @@ def _engine_worker(rank, world, port, out_dir):
     from k8s_llm_rca_amd.ops import layer_exec as LE
     from k8s_llm_rca_amd.parallel import xgmi
     from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    from k8s_llm_rca_amd.knobs import set_knob
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
+    # this test forces each (mode, push) form itself: no init-time fabric tuning
+    set_knob("tp_autotune", False)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD)
     pc.custom_ar = xgmi.XgmiAllReduce(dist.group.WORLD, max_bytes=8 << 20, timeout_s=60.0,

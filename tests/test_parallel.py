@@ -267,3 +267,21 @@ def test_step_channel_roundtrip():
         out = os.path.join(d, "ch")
         mp.spawn(_run_channel, args=(world, _free_port(), out), nprocs=world, join=True)
         assert all(open(f"{out}.{r}").read() == "ok" for r in range(1, world))
+
+
+def test_xgmi_plan_for_buckets_and_size_rule():
+    """XgmiAllReduce.plan_for: the tuned bucket at or above T, else the size
+    rule (one-shot up to ONE_SHOT_MAX bytes, never push) -- the executor's
+    per-step (mode, push) choice (ops/layer_exec.py)."""
+    import types
+    from k8s_llm_rca_amd.parallel.xgmi import ONE_SHOT_MAX, XgmiAllReduce
+    tuned = types.SimpleNamespace(plan={16: (1, False), 64: (2, True), 256: (1, True)})
+    assert XgmiAllReduce.plan_for(tuned, 1, 8192) == (1, False)
+    assert XgmiAllReduce.plan_for(tuned, 17, 8192) == (2, True)
+    assert XgmiAllReduce.plan_for(tuned, 256, 8192) == (1, True)
+    big = 300                                                          # > the largest bucket, > ONE_SHOT_MAX bytes
+    assert big * 8192 * 2 > ONE_SHOT_MAX
+    assert XgmiAllReduce.plan_for(tuned, big, 8192) == (2, False)       # past the largest bucket: size rule
+    untuned = types.SimpleNamespace(plan=None)
+    assert XgmiAllReduce.plan_for(untuned, 4, 8192) == (1, False)
+    assert XgmiAllReduce.plan_for(untuned, big, 8192) == (2, False)

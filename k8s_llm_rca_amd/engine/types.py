@@ -97,7 +97,13 @@ class EngineConfig:
     # step n+1 (decode inputs taken from the device-side sampled tokens)
     async_steps: bool = True
     prefix_sharing: bool = True  # attach other threads' published prompt pages (kv_cache.py)
-    gil_switch_interval: Optional[float] = None  # seconds; None keeps the interpreter default
+    # sys.setswitchinterval while the engine thread runs (seconds; None keeps the
+    # interpreter's 5 ms): the engine thread re-takes the GIL from the pipeline
+    # threads after every device wait, and a step boundary it reaches late is GPU
+    # idle.  0.5 ms, interleaved A/B at the 104-concurrency operating point
+    # (profiles/r5/ab_gil104/): 4.703 / 4.655 -> 4.716 / 4.763 analyses/s, p50
+    # 19.47 / 19.48 -> 19.15 / 19.19 s
+    gil_switch_interval: Optional[float] = 0.0005
     graph_batch_sizes: Tuple[int, ...] = (1, 2, 4, 8, 16, 24, 32, 48, 64, 96, 128, 160, 192, 224, 256)
     seed: int = 0
     # a request running longer than this is cancelled by the engine (its run

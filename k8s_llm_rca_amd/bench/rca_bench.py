@@ -587,10 +587,10 @@ def parser() -> argparse.ArgumentParser:
     # The operating point is chosen by the latency half of the metric: the
     # throughput plateau spans 96-128 concurrent analyses within ~2 % (4.67-4.77 /s,
     # profiles/r5/curve/, profiles/r5/ab_defer96/) while p50 grows with concurrency
-    # (Little's law: 17.6 s at 96, 19.3 s at 104, 20.2 s at 112, 26.9 s at 128), so
-    # the default is the largest measured point with p50 under the reference's
-    # 20 s latency floor.
-    p.add_argument("--incidents", type=int, default=104,
+    # (Little's law: 17.6 s at 96, 18.7 s at 100, 19.2-19.9 s at 104, 20.2 s at 112,
+    # 26.9 s at 128), so the default is the point with p50 a clear second under the
+    # reference's 20 s latency floor at the plateau's throughput.
+    p.add_argument("--incidents", type=int, default=100,
                    help="concurrent RCA analyses (pipelines) per GPU (default: the p50 < 20 s operating point)")
     p.add_argument("--graph-nodes", type=int, default=10_000)
     p.add_argument("--no-graph-device", action="store_true",

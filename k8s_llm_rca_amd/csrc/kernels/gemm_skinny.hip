@@ -10,6 +10,7 @@
 // feeds MT MFMAs (MT = ceil(M/16) m-tiles).  The 4 K-quarters are summed through
 // LDS and written as bf16.  Grid = N/16 workgroups (256 for N = 4096: one per CU).
 #include "common.h"
+#include "norm_prologue.h"
 
 namespace k8s {
 
@@ -33,17 +34,23 @@ __device__ __forceinline__ int rope_row(int n, int b) {  // W / output row of st
   return (b >> 3) * 128 + (b & 7) * 8 + (n & 7) + (n >= 8 ? 64 : 0);
 }
 
-template <int MT, int U, int NW, bool ROPE>
+// NORM: X = rmsnorm(nin) computed by the block itself into LDS (norm_prologue.h;
+// M <= kNormMaxRows, K == nin.H), after the first U weight loads are issued.
+template <int MT, int U, int NW, bool ROPE, bool NORM = false>
 __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __restrict__ x, int ldx,
                                                               const uint16_t* __restrict__ w,
                                                               uint16_t* __restrict__ y, int ldy, int M, int N, int K,
-                                                              SkinnyRope rp) {
+                                                              SkinnyRope rp, NormIn nin = {}) {
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   const int r = lane & 15, h = lane >> 4;
   const int n0 = blockIdx.x * 16;
   const int kq = K / NW;                 // K slice per wave (multiple of 32)
   const int kbeg = wv * kq;
   const uint16_t* wrow = w + (size_t)(ROPE ? rope_row(r, blockIdx.x) : n0 + r) * K + kbeg + 8 * h;
+  if constexpr (NORM) {
+    x = k8s_norm_lds;
+    ldx = K;
+  }
   const uint16_t* xrow[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) {
@@ -73,8 +80,22 @@ __global__ void __launch_bounds__(NW * 64) gemm_skinny_kernel(const uint16_t* __
   };
   const int nblk = nsteps / U;
   int s = 0;
+  if constexpr (NORM) {  // the first weight block in flight while the rows are normalised
+    __shared__ float nscr[16];
+    if (nblk > 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u) wa[u] = ldw_nt<bf16x8>(wrow + u * 32);
+    }
+    norm_rows_to_lds(k8s_norm_lds, M, nin, blockIdx.x == 0, nscr);
+    if (nblk > 0) {
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) xa[u][mt] = *reinterpret_cast<const bf16x8*>(xrow[mt] + u * 32);
+    }
+  }
   if (nblk > 0) {
-    load(wa, xa, 0);
+    if constexpr (!NORM) load(wa, xa, 0);
     int b = 0;
     for (; b + 2 <= nblk; b += 2) {
       if (b + 1 < nblk) load(wb, xb, (b + 1) * U);
@@ -184,5 +205,25 @@ K8S_API int k8s_gemm_skinny_rope(const void* x, int ldx, const void* w, void* qk
   const SkinnyRope rp{pos, cos_sin, slots, (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS};
   hipLaunchKernelGGL((gemm_skinny_kernel<1, 4, 8, true>), dim3(N / 16), dim3(512), 0, s, (const uint16_t*)x, ldx,
                      (const uint16_t*)w, (uint16_t*)qkv, ldq, M, N, K, rp);
+  return (int)hipGetLastError();
+}
+
+// k8s_gemm_skinny_rope on X = rmsnorm(x [or the split-K partials `part`] + res_in) * norm_w,
+// computed by every workgroup into LDS (norm_prologue.h): bit-identical to
+// k8s_rmsnorm / k8s_splitk_addnorm + k8s_gemm_skinny_rope, one launch fewer.  res_in
+// null: the plain norm of x (first layer).  Otherwise res_out (!= res_in) <- x + res_in.
+K8S_API int k8s_gemm_skinny_rope_norm(const void* x, int x_stride, const float* part, int splits, const void* res_in,
+                                      void* res_out, const void* norm_w, float eps, const void* w, void* qkv, int ldq,
+                                      int M, int N, int K, const int* pos, const float* cos_sin, const int* slots,
+                                      void* kc, void* vc, int nq, int nkv, int BS, hipStream_t s) {
+  if (M <= 0 || M > kNormMaxRows || K % 256 || K / 8 > 256 * kNormMaxChunks || N != (nq + 2 * nkv) * 128 ||
+      ldq < N || !pos || !cos_sin || BS <= 0 || !norm_w || (!x && !part) || (part && (splits < 1 || !res_in)) ||
+      (res_in && (!res_out || res_out == res_in)))
+    return (int)hipErrorInvalidValue;
+  const SkinnyRope rp{pos, cos_sin, slots, (uint16_t*)kc, (uint16_t*)vc, nq, nkv, BS};
+  const NormIn nin{(const uint16_t*)x, part, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)norm_w,
+                   x_stride, splits, K, eps};
+  hipLaunchKernelGGL((gemm_skinny_kernel<1, 4, 8, true, true>), dim3(N / 16), dim3(512), (size_t)M * K * 2, s,
+                     nullptr, 0, (const uint16_t*)w, (uint16_t*)qkv, ldq, M, N, K, rp, nin);
   return (int)hipGetLastError();
 }

@@ -27,6 +27,7 @@
 
 #include "common.h"
 #include "knobs.h"
+#include "norm_prologue.h"
 
 namespace k8s {
 
@@ -50,11 +51,14 @@ __device__ __forceinline__ int strip_row(int n, int silu_i) {
 
 __device__ __forceinline__ float silu_f(float g) { return g / (1.f + __expf(-g)); }
 
-template <int MTW, int U>
+// NORM: X = rmsnorm(nin) computed by the workgroup into LDS (norm_prologue.h;
+// M <= kNormMaxRows, one K split, K == nin.H) while its first U chunks of W
+// are in flight; the X fragments are then read from LDS.
+template <int MTW, int U, bool NORM = false>
 __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __restrict__ x, int ldx,
                                                           const uint16_t* __restrict__ w, uint16_t* __restrict__ y,
                                                           int ldy, float* __restrict__ part, int M, int N, int K,
-                                                          int kslice, int silu_i) {
+                                                          int kslice, int silu_i, NormIn nin = {}) {
   __shared__ __attribute__((aligned(16))) uint16_t ws[2][kSBN * kSC];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int r = lane & 15, g = lane >> 4;
@@ -76,6 +80,10 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
     wdst[i] = n * kSC + 8 * jl;
   }
   // ---- X fragments: row of frag mt for this lane (clamped; masked at the store)
+  if constexpr (NORM) {
+    x = k8s_norm_lds;
+    ldx = K;
+  }
   const uint16_t* xrow[MTW];
 #pragma unroll
   for (int mt = 0; mt < MTW; ++mt) {
@@ -100,14 +108,20 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
   // while one is computed.
   u16x8 ring[U][2];
   bf16x8 xq[U][2][MTW];
-  auto load_chunk = [&](int slot, int c) {
+  auto load_w = [&](int slot, int c) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) ring[slot][i] = ldw_nt<u16x8>(wsrc[i] + c * kSC);
+  };
+  auto load_x = [&](int slot, int c) {
 #pragma unroll
     for (int s = 0; s < 2; ++s)
 #pragma unroll
       for (int mt = 0; mt < MTW; ++mt)
         xq[slot][s][mt] = *reinterpret_cast<const bf16x8*>(xrow[mt] + c * kSC + 32 * s);
+  };
+  auto load_chunk = [&](int slot, int c) {
+    load_w(slot, c);
+    load_x(slot, c);
   };
   auto store_w = [&](int slot, int buf) {
 #pragma unroll
@@ -128,8 +142,17 @@ __global__ void __launch_bounds__(256) gemm_stream_kernel(const uint16_t* __rest
 
   // ---- prologue: chunks 0..U-1 in flight, chunk 0's W -> LDS
   // (nch % U == 0 and nch >= U: checked at launch)
+  if constexpr (NORM) {
+    __shared__ float nscr[16];
 #pragma unroll
-  for (int u = 0; u < U; ++u) load_chunk(u, u);
+    for (int u = 0; u < U; ++u) load_w(u, u);
+    norm_rows_to_lds(k8s_norm_lds, M, nin, blockIdx.x == 0 && blockIdx.y == 0, nscr);
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_x(u, u);
+  } else {
+#pragma unroll
+    for (int u = 0; u < U; ++u) load_chunk(u, u);
+  }
   store_w(0, 0);
   __syncthreads();
 
@@ -696,6 +719,30 @@ K8S_API int k8s_gemm_stream_push(const void* x, int ldx, const void* w, int M, i
 K8S_API int k8s_gemm_stream_silu(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K,
                                  int cfg, hipStream_t s) {
   return stream_launch(x, ldx, w, y, ldy, M, N, K, cfg, 1, nullptr, true, s, true);
+}
+
+// k8s_gemm_stream_silu (register-ring cfg 4 / 8) on X = rmsnorm(x [or the split-K
+// partials `part`] + res_in) * norm_w computed by every workgroup into LDS
+// (norm_prologue.h): bit-identical to k8s_rmsnorm / k8s_splitk_addnorm +
+// k8s_gemm_stream_silu, one launch fewer.  res_out (!= res_in) <- x + res_in.
+K8S_API int k8s_gemm_stream_silu_norm(const void* x, int x_stride, const float* part, int splits, const void* res_in,
+                                      void* res_out, const void* norm_w, float eps, const void* w, void* y, int ldy,
+                                      int M, int N, int K, int cfg, hipStream_t s) {
+  if (M <= 0 || M > kNormMaxRows || K % kSC || K / 8 > 256 * kNormMaxChunks || (cfg != 4 && cfg != 8) ||
+      (K / kSC) % cfg || N % (kSBN / 2) || ldy < N || !norm_w || (!x && !part) || (part && (splits < 1 || !res_in)) ||
+      (res_in && (!res_out || res_out == res_in)))
+    return (int)hipErrorInvalidValue;
+  const NormIn nin{(const uint16_t*)x, part, (const uint16_t*)res_in, (uint16_t*)res_out, (const uint16_t*)norm_w,
+                   x_stride, splits, K, eps};
+  const dim3 grid(N / (kSBN / 2), 1);
+  const size_t lds = (size_t)M * K * 2;
+  if (cfg == 4)
+    hipLaunchKernelGGL((gemm_stream_kernel<1, 4, true>), grid, dim3(256), lds, s, nullptr, 0, (const uint16_t*)w,
+                       (uint16_t*)y, ldy, nullptr, M, N, K, K, N, nin);
+  else
+    hipLaunchKernelGGL((gemm_stream_kernel<1, 8, true>), grid, dim3(256), lds, s, nullptr, 0, (const uint16_t*)w,
+                       (uint16_t*)y, ldy, nullptr, M, N, K, K, N, nin);
+  return (int)hipGetLastError();
 }
 
 K8S_API int k8s_gemm_stream_part(const void* x, int ldx, const void* w, void* y, int ldy, int M, int N, int K, int cfg,

@@ -82,6 +82,13 @@ int k8s_gemm_stream_push(const void* x, int ldx, const void* w, int M, int N, in
 int k8s_ar_push_addnorm_bf16(int id, void* res, const void* w, void* y, int T, int H, float eps, int mode, int S,
                              hipStream_t s);
 int k8s_nonfinite_flag(const void* x, long n, int* flag, hipStream_t s);
+int k8s_gemm_skinny_rope_norm(const void* x, int x_stride, const float* part, int splits, const void* res_in,
+                              void* res_out, const void* norm_w, float eps, const void* w, void* qkv, int ldq, int M,
+                              int N, int K, const int* pos, const float* cos_sin, const int* slots, void* kc, void* vc,
+                              int nq, int nkv, int BS, hipStream_t s);
+int k8s_gemm_stream_silu_norm(const void* x, int x_stride, const float* part, int splits, const void* res_in,
+                              void* res_out, const void* norm_w, float eps, const void* w, void* y, int ldy, int M,
+                              int N, int K, int cfg, hipStream_t s);
 }
 
 // kind: 0 hipBLASLt, 1 skinny, 2 gemm_mid (cfg, splits), 3 single-expert grouped (splits),
@@ -157,6 +164,13 @@ struct K8sLlamaStep {
   // debug (knob nonfinite_check): nf_flags[l] = 1 when layer l's normed input
   // holds a NaN / inf, nf_flags[L] for the last down output; nullptr = off
   int* nf_flags;
+  // norm_fuse (TP = 1, T <= 4; ops/layer_exec.py decides): bit 0 -- the input norm
+  // rides in the skinny RoPE qkv GEMM's prologue, bit 1 -- the post-attention norm
+  // in the SwiGLU stream gate_up GEMM's (norm_prologue.h).  A fused add-norm
+  // writes the new residual to the OTHER of {residual, res2} (its workgroups are
+  // still reading the current one), so the current residual alternates.
+  void* res2;
+  int norm_fuse;
 };
 
 namespace {
@@ -229,20 +243,38 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
   const bool push_o = fuse_an && s.ar_push && push_kind(s.sel[1]);
   const bool push_d = fuse_an && s.ar_push && push_kind(s.sel[3]);
   const long n_out = (long)T * H;
+  // current / other residual buffer (norm_fuse ping-pong, see K8sLlamaStep)
+  void* rc = s.residual;
+  void* ro = s.res2;
+  const bool nf_qkv = !tp && (s.norm_fuse & 1) && s.sel[0].kind == 1 && s.sel[0].fuse == 3;
+  const bool nf_gu = !tp && (s.norm_fuse & 2) && s.sel[2].kind == 4 && s.sel[2].fuse == 2;
   for (int l = 0; l < s.L; ++l) {
-    if (l == 0)
-      K8S_TRY(k8s_rmsnorm(s.residual, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    if (nf_qkv) {  // input norm + qkv GEMM + RoPE / KV write in one launch
+      const bool first = l == 0;
+      const float* part = pend ? (const float*)part_of(s, s.sel[3]) : nullptr;
+      K8S_TRY(k8s_gemm_skinny_rope_norm(first ? rc : (pend ? nullptr : s.prev), H, part, s.sel[3].splits,
+                                        first ? nullptr : rc, first ? nullptr : ro, s.in_norm[l], s.eps, s.wqkv[l],
+                                        qkv, ld_qkv, T, ld_qkv, H, s.pos, s.cos_sin, s.slots, s.kc[l], s.vc[l], s.nq,
+                                        s.nkv, s.BS, st));
+      if (!first) {
+        void* t = rc;
+        rc = ro;
+        ro = t;
+      }
+    } else if (l == 0)
+      K8S_TRY(k8s_rmsnorm(rc, nullptr, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
     else if (fuse_an) {
       // y = rmsnorm(all-reduced down_proj + residual): done by the previous layer's fused epilogue
     } else if (pend)
-      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[3]), s.sel[3].splits, s.residual, s.in_norm[l], s.y, T, H, H,
-                                 s.eps, st));
+      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[3]), s.sel[3].splits, rc, s.in_norm[l], s.y, T, H, H, s.eps, st));
     else
-      K8S_TRY(k8s_rmsnorm(s.prev, s.residual, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
-    if (s.nf_flags) K8S_TRY(k8s_nonfinite_flag(s.y, n_out, s.nf_flags + l, st));
+      K8S_TRY(k8s_rmsnorm(s.prev, rc, s.in_norm[l], s.y, T, H, H, H, s.eps, st));
+    if (s.nf_flags && !nf_qkv) K8S_TRY(k8s_nonfinite_flag(s.y, n_out, s.nf_flags + l, st));
     // a split-K qkv projection leaves its partials to the RoPE / KV-write kernel,
     // which reduces them first (k8s_splitk_rope_kv: bit-identical, one launch fewer)
-    if (deferred(s.sel[0], true)) {
+    if (nf_qkv) {
+      // done above
+    } else if (deferred(s.sel[0], true)) {
       K8S_TRY(gemm(s, s.sel[0], s.y, H, s.wqkv[l], qkv, ld_qkv, T, ld_qkv, H, st, true));
       K8S_TRY(k8s_splitk_rope_kv(part_of(s, s.sel[0]), s.sel[0].splits, qkv, ld_qkv, s.pos, s.cos_sin, s.slots,
                                  s.kc[l], s.vc[l], T, s.nq, s.nkv, s.BS, st));
@@ -280,14 +312,23 @@ K8S_API int k8s_llama_layers(const K8sLlamaStep* sp, hipStream_t st) {
       K8S_TRY(k8s_ar_addnorm_bf16(s.ar_id, s.obuf, s.residual, s.post_norm[l], s.y, T, H, s.eps, s.ar_mode, st));
     else if (tp)
       K8S_TRY(k8s_ar_allreduce_bf16(s.ar_id, s.obuf, s.obuf, n_out, s.ar_mode, st));
-    if (fuse_an) {
+    if (nf_gu) {  // post-attention norm + gate_up + SwiGLU in one launch
+      const bool dp = deferred(s.sel[1], true);
+      K8S_TRY(k8s_gemm_stream_silu_norm(dp ? nullptr : s.obuf, H, dp ? (const float*)part_of(s, s.sel[1]) : nullptr,
+                                        s.sel[1].splits, rc, ro, s.post_norm[l], s.eps, s.wgu[l], s.act, s.I, T, s.I,
+                                        H, s.sel[2].cfg, st));
+      void* t = rc;
+      rc = ro;
+      ro = t;
+    } else if (fuse_an) {
       // residual add + post-attention norm done above
     } else if (!tp && deferred(s.sel[1], true))
-      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[1]), s.sel[1].splits, s.residual, s.post_norm[l], s.y, T, H, H,
-                                 s.eps, st));
+      K8S_TRY(k8s_splitk_addnorm(part_of(s, s.sel[1]), s.sel[1].splits, rc, s.post_norm[l], s.y, T, H, H, s.eps, st));
     else
-      K8S_TRY(k8s_rmsnorm(s.obuf, s.residual, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
-    if (s.sel[2].fuse == 2 && s.sel[2].kind == 5) {  // gate_up + SwiGLU in one launch: gu is never written
+      K8S_TRY(k8s_rmsnorm(s.obuf, rc, s.post_norm[l], s.y, T, H, H, H, s.eps, st));
+    if (nf_gu) {
+      // gate_up done above
+    } else if (s.sel[2].fuse == 2 && s.sel[2].kind == 5) {  // gate_up + SwiGLU in one launch: gu is never written
       K8S_TRY(k8s_gemm_big(s.y, H, s.wgu[l], s.act, s.I, T, s.I, H, 1, s.sel[2].cfg, st));
     } else if (s.sel[2].fuse == 2 && s.sel[2].kind == 4) {
       K8S_TRY(k8s_gemm_stream_silu(s.y, H, s.wgu[l], s.act, s.I, T, s.I, H, s.sel[2].cfg, st));

@@ -149,7 +149,8 @@ class GraphRunnerMixin:
         # plan on the real rows; padded rows (ctx 1) still get a one-key item
         # (sorted last) so every output row the graph produces is finite
         chain = self._decode_chain(decode)
-        _, part = A.plan_decode_split(self._plan_ctx(ctx[:B], chain), self.model.nkv)
+        _, part = A.plan_decode_split(self._plan_ctx(ctx[:B], chain), self.model.nkv,
+                                      max_parts=self._n_parts(self.max_context))
         if self.stats["graph_steps"] % 32 == 0:  # how often decode attention re-reads a shared KV block
             used = np.concatenate([s.blocks[: (s.n_cached + j + BS) // BS] for s, j in decode])
             self.stats["kv_read_blocks_sampled"] += used.size

@@ -181,7 +181,8 @@ class StepExecMixin:
             bt_d, ctx_d, qs_d = self._decode_meta(decode)
             maxb_d = bt_d.shape[1]
             chain = self._decode_chain(decode)
-            n_parts, part = A.plan_decode_split(self._plan_ctx(ctx_d, chain), self.model.nkv)
+            n_parts, part = A.plan_decode_split(self._plan_ctx(ctx_d, chain), self.model.nkv,
+                                                max_parts=self._n_parts(self.max_context))
             n_parts = max(n_parts, -(-int(ctx_d.max()) // part))
             arrays += [bt_d, ctx_d, qs_d]
             if self.kv.block_size % 64 == 0:

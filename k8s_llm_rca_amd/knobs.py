@@ -59,6 +59,8 @@ class Knobs:
     fuse_splitk: bool = _f(True, "split-K partials reduced inside the next RoPE/KV-write or add+RMSNorm")
     decode_group: bool = _f(True, "consecutive tokens of one sequence share multi-token decode items",
                             legacy="K8S_DECODE_GROUP")
+    decode_low_units: int = _f(512, "low-batch decode split: fewest keys per item keeping <= this many waves "
+                                    "(ops/attention.py DECODE_LOW_UNITS; 0 = the makespan planner everywhere)")
     decode_reduce_pre: bool = _f(True, "decode split-KV reduce: register-prefetch form for <= 16 partitions",
                                  native=1)
     decode_kv_nt: bool = _f(False, "non-temporal K/V loads in the decode attention stream (A/B: 5.6 % slower on "
@@ -73,6 +75,8 @@ class Knobs:
                                legacy="K8S_PF_MAKESPAN_ALL")
     # ---------------------------------------------------------------- native layer executor / TP
     layer_exec: bool = _f(True, "whole dense layer stack issued by one C call (ops/layer_exec.py)")
+    norm_fuse: bool = _f(True, "steps of <= 4 rows: the RMSNorms ride in the qkv / gate_up GEMMs' prologues "
+                               "(csrc/kernels/norm_prologue.h)")
     tp_fused_norm: bool = _f(True, "TP all-reduce + residual add + RMSNorm in one launch")
     tp_push: bool = _f(False, "TP o/down GEMM epilogue stores into the all-reduce slots (push) wherever it fits "
                               "(default: where the init-time fabric tuning measured it faster)")

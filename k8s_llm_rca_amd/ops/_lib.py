@@ -47,6 +47,8 @@ _SIGS = {
     "k8s_gemm_big_ws_bytes": [],
     "k8s_gemm_big_set_ws": [P],
     "k8s_gemm_stream_silu": [P, I, P, P, I, I, I, I, I, P],
+    "k8s_gemm_stream_silu_norm": [P, I, P, I, P, P, P, F, P, P, I, I, I, I, I, P],
+    "k8s_gemm_skinny_rope_norm": [P, I, P, I, P, P, P, F, P, P, I, I, I, I, P, P, P, P, P, I, I, I, P],
     "k8s_gemm_stream_part": [P, I, P, P, I, I, I, I, I, I, P, P],
     "k8s_grouped_glds": [P, I, P, P, I, P, I, I, I, I, I, I, P, I, P],
     "k8s_splitk_addnorm": [P, I, P, P, P, I, I, I, F, P],

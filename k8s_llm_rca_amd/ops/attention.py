@@ -193,9 +193,20 @@ DECODE_GROUP_TOKENS = KNOBS.decode_group
 DECODE_WAVE_SLOTS = 2048                 # resident decode waves: 256 CUs x 4 SIMDs x 2 (<= 256 VGPRs)
 DECODE_ITEM_OVERHEAD = 256               # per-item start cost in key-equivalents (replay-calibrated)
 _DECODE_PLANNER = "makespan"
+# Low batch (the whole step is one round of waves at 256 keys per item): the
+# fewest keys per item that keep the launch at <= this many (item, kv head)
+# waves, from 64 keys up.  Measured over cold K/V, 1-8 rows x 2k-8k keys
+# (tools/decode_part_sweep.py, profiles/r5/decode_parts/): the best part size
+# puts ~256-512 waves on the 256 CUs -- fewer, longer items at 4-8 rows (512
+# keys: 30.7 vs 34.4 us at 4 x 8k), shorter ones at one row (192: 13.7 vs
+# 15.4 us at 5k) -- where the makespan model's fixed item cost took 256 keys
+# everywhere.  0 = off.
+DECODE_LOW_UNITS = KNOBS.decode_low_units
+DECODE_LOW_PARTS = tuple(range(64, 1537, 64))
 
 
-def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=None) -> tuple:
+def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=None,
+                      max_parts: Optional[int] = None) -> tuple:
     """Keys per decode work item for one step -> (max items per sequence, part_size).
 
     The persistent decode kernel runs ``slots`` waves over a longest-first
@@ -212,6 +223,13 @@ def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candid
     import numpy as np
     c = np.asarray(ctx_lens, dtype=np.int64)
     mx = int(c.max()) if c.size else 1
+    if DECODE_LOW_UNITS and candidates is None and c.size:
+        P0 = min(DECODE_PARTS)
+        if nkv * int(((c + P0 - 1) // P0).sum()) <= slots:  # one round: the low-batch rule
+            for P in DECODE_LOW_PARTS:
+                n = -(-mx // P)
+                if (max_parts is None or n <= max_parts) and nkv * int(((c + P - 1) // P).sum()) <= DECODE_LOW_UNITS:
+                    return max(1, n), P
     if _DECODE_PLANNER == "v1":
         return _plan_decode_split_v1(c, nkv, slots, candidates or DECODE_PARTS_V1)
     Ps = np.asarray(candidates or DECODE_PARTS, dtype=np.int64)[:, None]      # [nc, 1]

@@ -44,6 +44,7 @@ class LlamaStep(ctypes.Structure):
         ("sel", GemmSel * 4),
         ("blaslt_ws", P), ("blaslt_ws_bytes", ctypes.c_size_t), ("mid_part", P), ("grp_part", P), ("grp_offs", P),
         ("ar_id", I), ("ar_mode", I), ("ar_fuse", I), ("ar_push", I), ("nf_flags", P),
+        ("res2", P), ("norm_fuse", I),
     ]
 
 
@@ -62,6 +63,11 @@ _tp_push = KNOBS.tp_push
 _tp_push_force = KNOBS.tp_push_force
 # split-K o / down projections reduced inside the following residual add + RMSNorm
 _fuse_splitk = KNOBS.fuse_splitk
+# steps of <= NORM_FUSE_MAX_T rows: the input / post-attention RMSNorms computed in
+# the prologue of the skinny RoPE qkv GEMM / the SwiGLU stream gate_up GEMM
+# (csrc/kernels/norm_prologue.h; bit-identical, two launches fewer per layer)
+_norm_fuse = KNOBS.norm_fuse
+NORM_FUSE_MAX_T = 4
 # (Round 3 also carried a row-chunked o / down GEMM with each chunk's
 # all-reduce on a side stream, and the prefill attention on a side stream beside
 # the decode attention: both measured as losses -- profiles/r3/ab/tp_overlap_*,
@@ -231,8 +237,20 @@ class LlamaExecutor:
             from . import moe as MO
             st.grp_part = MO._split_scratch(dev, need_grp).data_ptr()
             st.grp_offs = LIN.grp_offsets(dev, T).data_ptr()
+        # fused norms (TP = 1): mirrors llama_exec.hip's nf_qkv / nf_gu conditions
+        nf = 0
+        if _norm_fuse and self._car is None and m.nf_flags is None and T <= NORM_FUSE_MAX_T:
+            if st.sel[0].kind == LIN.KIND_SKINNY and st.sel[0].fuse == 3:
+                nf |= 1
+            if st.sel[2].kind == LIN.KIND_STREAM and st.sel[2].fuse == 2 and st.sel[2].cfg in (4, 8):
+                nf |= 2
+        st.norm_fuse = nf
+        res2 = scratch((T, H), dt, dev) if nf else None
+        st.res2 = ptr(res2)
         check(lib().k8s_llama_layers(ctypes.byref(st), stream_ptr(residual)), "llama_layers")
-        return prev, residual
+        # every fused add-norm moves the residual to the other buffer
+        swaps = (st.L - 1) * (nf & 1) + st.L * ((nf >> 1) & 1)
+        return prev, (res2 if swaps % 2 else residual)
 
 
 def _silu_fused_in_table(model) -> bool:

@@ -128,3 +128,28 @@ def test_fit_slots_clamps_non_power_of_two_part():
     assert A._fit_slots(pages, 256, None, 12) == 1024
     with pytest.raises(ValueError):
         A._fit_slots(pages, 768, 1024, 11)   # max_part itself overflows
+
+
+@pytest.mark.parametrize("rows,ctx,want", [(1, 2048, 64), (1, 5000, 128), (2, 5000, 192), (2, 8000, 256),
+                                           (4, 2048, 128), (4, 8000, 512), (8, 2048, 256)])
+def test_low_batch_decode_split_targets_wave_count(rows, ctx, want):
+    """One-round decode steps take the fewest keys per item that keep the
+    launch at <= DECODE_LOW_UNITS (item, kv head) waves -- the measured best of
+    tools/decode_part_sweep.py at these shapes -- capped by the graph buffers'
+    partition count; big batches keep the makespan planner (>= 256 keys)."""
+    nkv = 8
+    n, P = A.plan_decode_split([ctx] * rows, nkv)
+    assert P == want and n == -(-ctx // P)
+    assert nkv * rows * n <= A.DECODE_LOW_UNITS
+    # the buffer cap: at most 32 partitions (an 8k window at 256 keys) -> P >= ctx / 32
+    n2, P2 = A.plan_decode_split([ctx] * rows, nkv, max_parts=32)
+    assert n2 <= 32 and P2 >= P
+    # a headline-size step: many rows, several rounds -> the makespan planner's part sizes
+    _, Pb = A.plan_decode_split([5000] * 100, nkv)
+    assert Pb in A.DECODE_PARTS
+
+
+def test_low_batch_rule_off(monkeypatch):
+    monkeypatch.setattr(A, "DECODE_LOW_UNITS", 0)
+    _, P = A.plan_decode_split([5000], 8)
+    assert P == min(A.DECODE_PARTS)

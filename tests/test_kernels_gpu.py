@@ -1073,6 +1073,130 @@ def test_gemm_skinny_rope_epilogue_bit_identical(M, nq, nkv):
     torch.testing.assert_close(out.cpu().float(), r32.float(), atol=3e-2, rtol=3e-2)
 
 
+def _norm_inputs(M, H, mode, splits=4, seed=0):
+    """(x, part, res) for a fused-norm case: ``first`` the plain norm of x,
+    ``add`` x + res, ``part`` split-K fp32 partials [splits][M][H] + res."""
+    g = torch.Generator(device=dev).manual_seed(seed)
+    res = torch.randn(M, H, device=dev, generator=g).bfloat16()
+    x = torch.randn(M, H, device=dev, generator=g).bfloat16()
+    part = torch.randn(splits, M, H, device=dev, generator=g) * 0.5 if mode == "part" else None
+    return x, part, res
+
+
+def _norm_ref(x, part, res, w, eps, mode):
+    """The unfused kernels: k8s_rmsnorm / k8s_splitk_addnorm -> (y, new residual)."""
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    M, H = res.shape
+    y = torch.empty(M, H, device=dev).bfloat16()
+    r = res.clone()
+    if mode == "first":
+        assert lib().k8s_rmsnorm(ptr(x), None, ptr(w), ptr(y), M, H, H, H, eps, stream_ptr(x)) == 0
+    elif mode == "add":
+        assert lib().k8s_rmsnorm(ptr(x), ptr(r), ptr(w), ptr(y), M, H, H, H, eps, stream_ptr(x)) == 0
+    else:
+        assert lib().k8s_splitk_addnorm(ptr(part), part.shape[0], ptr(r), ptr(w), ptr(y), M, H, H, eps,
+                                        stream_ptr(x)) == 0
+    return y, r
+
+
+@pytest.mark.parametrize("M", [1, 2, 3, 4])
+@pytest.mark.parametrize("mode", ["first", "add", "part"])
+@pytest.mark.parametrize("H", [512, 4096])
+def test_gemm_skinny_rope_norm_bit_identical(M, mode, H):
+    """RMSNorm in the skinny RoPE qkv GEMM's prologue (norm_prologue.h) ==
+    rmsnorm / split-K add-norm + k8s_gemm_skinny_rope bit for bit: qkv, the K / V
+    pages and the new residual (written to the other buffer; the input
+    residual untouched); and the normed GEMM against fp32."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    nq, nkv, BS, NB, eps = 8, 2, 64, 8, 1e-5
+    N = (nq + 2 * nkv) * 128
+    x, part, res = _norm_inputs(M, H, mode, seed=M + H)
+    nw = (torch.rand(H, device=dev) + 0.5).bfloat16()
+    w = (torch.randn(N, H, device=dev) * 0.05).bfloat16()
+    cs = A.rope_cos_sin(4096, 500000.0, device=dev)
+    pos = torch.randint(0, 4000, (M,), device=dev, dtype=torch.int32)
+    slots = torch.randperm(NB * BS, device=dev)[:M].int()
+    kc, vc = torch.zeros(NB, nkv, BS, 128, device=dev).bfloat16(), torch.zeros(NB, nkv, 128, BS, device=dev).bfloat16()
+    kc2, vc2 = kc.clone(), vc.clone()
+    y, r_ref = _norm_ref(x, part, res, nw, eps, mode)
+    ref = torch.empty(M, N, device=dev).bfloat16()
+    assert lib().k8s_gemm_skinny_rope(ptr(y), H, ptr(w), ptr(ref), N, M, N, H, ptr(pos), ptr(cs), ptr(slots),
+                                      ptr(kc), ptr(vc), nq, nkv, BS, stream_ptr(x)) == 0
+    out = torch.empty(M, N, device=dev).bfloat16()
+    res_in = res.clone()
+    res_out = torch.full_like(res, float("nan"))
+    first = mode == "first"
+    rc = lib().k8s_gemm_skinny_rope_norm(ptr(x if mode != "part" else None), H, ptr(part),
+                                         part.shape[0] if part is not None else 1,
+                                         None if first else ptr(res_in), None if first else ptr(res_out), ptr(nw),
+                                         eps, ptr(w), ptr(out), N, M, N, H, ptr(pos), ptr(cs), ptr(slots), ptr(kc2),
+                                         ptr(vc2), nq, nkv, BS, stream_ptr(x))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(out, ref) and torch.equal(kc2, kc) and torch.equal(vc2, vc)
+    assert torch.equal(res_in, res)
+    if not first:
+        assert torch.equal(res_out, r_ref)
+    # fp32: normalise and project in fp32, then RoPE (the bf16 reference path rounds y)
+    s = (part.sum(0) if mode == "part" else x.float()) + (0 if first else res.float())
+    y32 = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + eps) * nw.float()
+    r32 = (y32 @ w.float().t()).bfloat16().cpu()
+    A.rope_kv_write(r32, pos.cpu(), cs.cpu(), None, kc.cpu(), vc.cpu(), nq, nkv)
+    torch.testing.assert_close(out.cpu().float(), r32.float(), atol=6e-2, rtol=5e-2)
+
+
+@pytest.mark.parametrize("M", [1, 2, 4])
+@pytest.mark.parametrize("mode", ["add", "part"])
+@pytest.mark.parametrize("cfg", [4, 8])
+def test_gemm_stream_silu_norm_bit_identical(M, mode, cfg):
+    """RMSNorm in the SwiGLU stream gate_up GEMM's prologue == rmsnorm /
+    split-K add-norm + k8s_gemm_stream_silu bit for bit (act and the new
+    residual), and fp32."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    H, I, eps = 4096, 1024, 1e-5
+    x, part, res = _norm_inputs(M, H, mode, seed=7 * M + cfg)
+    nw = (torch.rand(H, device=dev) + 0.5).bfloat16()
+    w = (torch.randn(2 * I, H, device=dev) * 0.02).bfloat16()
+    y, r_ref = _norm_ref(x, part, res, nw, eps, mode)
+    ref = LIN.gemm_stream_silu(y, w, cfg)
+    act = torch.empty(M, I, device=dev).bfloat16()
+    res_in = res.clone()
+    res_out = torch.full_like(res, float("nan"))
+    rc = lib().k8s_gemm_stream_silu_norm(ptr(x if mode == "add" else None), H, ptr(part),
+                                         part.shape[0] if part is not None else 1, ptr(res_in), ptr(res_out),
+                                         ptr(nw), eps, ptr(w), ptr(act), I, M, I, H, cfg, stream_ptr(x))
+    assert rc == 0
+    torch.cuda.synchronize()
+    assert torch.equal(act, ref) and torch.equal(res_out, r_ref) and torch.equal(res_in, res)
+    s = (part.sum(0) if mode == "part" else x.float()) + res.float()
+    y32 = s * torch.rsqrt(s.pow(2).mean(-1, keepdim=True) + eps) * nw.float()
+    g, u = (y32 @ w.float().t()).split(I, dim=1)
+    torch.testing.assert_close(act.float(), torch.nn.functional.silu(g) * u, atol=5e-2, rtol=5e-2)
+
+
+def test_fused_norm_launch_contract():
+    """Shapes the fused-norm launchers refuse (they fail loudly, never run)."""
+    _need_gpu()
+    from k8s_llm_rca_amd.ops._lib import lib, ptr, stream_ptr
+    H, I = 4096, 1024
+    x = torch.zeros(5, H, device=dev).bfloat16()
+    w = torch.zeros(2 * I, H, device=dev).bfloat16()
+    act = torch.empty(5, I, device=dev).bfloat16()
+    r0, r1 = x.clone(), x.clone()
+    nw = torch.ones(H, device=dev).bfloat16()
+    s = stream_ptr(x)
+    # 5 rows > kNormMaxRows; res_out aliasing res_in; H = 8192 > the prologue's 4096
+    assert lib().k8s_gemm_stream_silu_norm(ptr(x), H, None, 1, ptr(r0), ptr(r1), ptr(nw), 1e-5, ptr(w), ptr(act), I,
+                                           5, I, H, 4, s) != 0
+    assert lib().k8s_gemm_stream_silu_norm(ptr(x), H, None, 1, ptr(r0), ptr(r0), ptr(nw), 1e-5, ptr(w), ptr(act), I,
+                                           1, I, H, 4, s) != 0
+    assert lib().k8s_gemm_stream_silu_norm(ptr(x), 8192, None, 1, ptr(r0), ptr(r1), ptr(nw), 1e-5, ptr(w), ptr(act),
+                                           I, 1, I, 8192, 4, s) != 0
+
+
 @pytest.mark.parametrize("Bb,mb,n_items", [(1, 4, 1), (24, 130, 37), (256, 130, 0)])
 def test_unpack_step_matches_slices(Bb, mb, n_items):
     """k8s_unpack_step (one launch before each graph decode step) scatters the

@@ -201,10 +201,19 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         L0 = layers[0]
         buckets = sorted(set(self.cfg.graph_batch_sizes) | {384, 512, 1024, 2048, 4096})
         t0 = time.perf_counter()
-        rep = car.tune([("o", L0["wo"]), ("down", L0["w_down"])], L0["post_norm"], float(self.mc.rms_eps), buckets)
+        shapes = [("o", L0["wo"]), ("down", L0["w_down"])]
+        rep = car.tune(shapes, L0["post_norm"], float(self.mc.rms_eps), buckets)
         log.info("xGMI epilogue plan tuned in %.1f s: %s", time.perf_counter() - t0,
                  {T: r["pick"] for T, r in rep.items()})
-        return {"tune_s": round(time.perf_counter() - t0, 2), "buckets": rep}
+        # steps whose all-reduce does not fit the executor's buffer take the Python
+        # path's row-chunked GEMM / all-reduce overlap: its depth per bucket, timed here
+        H = int(L0["wo"].shape[0])
+        big = [T for T in (1024, 2048, 4096, 8192, 16384)
+               if T <= self.cfg.max_batch_tokens and T * H * 2 + 4 * T > car.max_bytes]
+        ov = self.pc.tune_overlap(shapes, big) if big else {}
+        if ov:
+            log.info("GEMM / all-reduce overlap depth tuned: %s", {T: r["pick"] for T, r in ov.items()})
+        return {"tune_s": round(time.perf_counter() - t0, 2), "buckets": rep, "overlap": ov}
 
     def _workspace_bytes(self) -> int:
         mc = self.mc

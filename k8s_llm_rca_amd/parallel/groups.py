@@ -34,6 +34,66 @@ class ParallelContext:
     # when ranks share one GPU (RCCL refuses duplicate devices), and the mode a
     # TP group runs in whenever its communicator is up (attach_custom_allreduce)
     xgmi_only: bool = False
+    # pipeline depth per row-count bucket, timed on this fabric at init
+    # (tune_overlap): the bucket at or above M, else ar_chunks
+    chunk_plan: Optional[dict] = None
+
+    def chunks_for(self, M: int) -> int:
+        if self.chunk_plan:
+            for b in sorted(self.chunk_plan):
+                if b >= M:
+                    return self.chunk_plan[b]
+        return self.ar_chunks
+
+    def tune_overlap(self, shapes, buckets, depths=(1, 2, 4), iters: int = 4, rounds: int = 3) -> dict:
+        """Per row-count bucket T, the GEMM / all-reduce pipeline depth of
+        :meth:`linear_all_reduce` (1 = no overlap: GEMM, then one all-reduce;
+        k = k row chunks, chunk i's all-reduce on the comm stream beside chunk
+        i+1's GEMM), timed ON THIS FABRIC with the real row-parallel weights
+        [(name, w [H, K_local])].  Every rank runs the same collectives in
+        lockstep and each timing is max-reduced over the TP group, so all
+        ranks hold the same plan (``chunk_plan``); the report goes into the
+        bench line.  Round 4's default (4 chunks everywhere) and its loopback
+        A/B (a row-chunked decode-size overlap measured slower) could not show
+        what xGMI links do at prefill sizes."""
+        import time
+        if self.tp_size == 1:
+            return {}
+        dev = shapes[0][1].device
+        cuda = dev.type == "cuda"
+        report, plan = {}, {}
+        saved = self.chunk_plan
+        for T in sorted(set(int(b) for b in buckets)):
+            x = {name: torch.randn(T, int(w.shape[1]), device=dev).to(w.dtype) for name, w in shapes}
+            us = {k: [] for k in depths}
+            try:
+                for _ in range(rounds):
+                    for k in depths:
+                        self.chunk_plan = {1 << 30: k}
+                        for name, w in shapes:  # warm, and every rank enters this candidate together
+                            self.linear_all_reduce(x[name], w)
+                        if cuda:
+                            torch.cuda.synchronize(dev)
+                        t0 = time.perf_counter()
+                        for _ in range(iters):
+                            for name, w in shapes:
+                                self.linear_all_reduce(x[name], w)
+                        if cuda:
+                            torch.cuda.synchronize(dev)
+                        us[k].append((time.perf_counter() - t0) * 1e6 / iters)
+            finally:
+                self.chunk_plan = saved
+            med = torch.tensor([sorted(v)[len(v) // 2] for v in us.values()], dtype=torch.float64)
+            on_dev = cuda and dist.get_backend(self.tp_group) == "nccl"
+            t = med.to(dev) if on_dev else med
+            dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.tp_group)  # the slowest rank's view
+            med = t.cpu().tolist()
+            best = min(range(len(depths)), key=lambda i: med[i])
+            plan[T] = depths[best]
+            report[T] = {f"k{k}": round(v, 1) for k, v in zip(depths, med)}
+            report[T]["pick"] = depths[best]
+        self.chunk_plan = plan
+        return report
 
     @property
     def is_tp(self) -> bool:
@@ -86,7 +146,7 @@ class ParallelContext:
         if self.tp_size == 1:
             return lin(x, w)
         M, N = x.shape[0], w.shape[0]
-        k = self.ar_chunks
+        k = self.chunks_for(M)
         if k <= 1 or M * N * x.element_size() < self.overlap_min_bytes * k:
             return self.all_reduce(lin(x, w))
         works, parts = [], []

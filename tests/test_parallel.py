@@ -192,6 +192,44 @@ def test_linear_all_reduce_overlap_chunks_exact():
     assert all(v < 1e-4 for v in res.values()), res
 
 
+def _run_tune_overlap(rank, world, port, out_path):
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, overlap_min_bytes=64)
+    g = torch.Generator().manual_seed(7 + rank)
+    shapes = [("o", torch.randn(96, 48, generator=g)), ("down", torch.randn(96, 80, generator=g))]
+    rep = pc.tune_overlap(shapes, [300, 600], iters=2, rounds=2)
+    picks = torch.tensor([rep[300]["pick"], rep[600]["pick"]])
+    allp = [torch.zeros_like(picks) for _ in range(world)]
+    dist.all_gather(allp, picks)
+    # the tuned depth is what linear_all_reduce then runs, and it is still exact
+    x = torch.randn(450, 48, generator=g)
+    got = pc.linear_all_reduce(x, shapes[0][1])
+    want = x @ shapes[0][1].t()
+    dist.all_reduce(want)
+    if rank == 0:
+        torch.save({"plan": pc.chunk_plan, "picks": [p.tolist() for p in allp], "k450": pc.chunks_for(450),
+                    "err": (got - want).abs().max().item(), "keys": sorted(rep[300])}, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tune_overlap_same_plan_on_every_rank():
+    """The GEMM / all-reduce pipeline depth timed per bucket at init
+    (ParallelContext.tune_overlap): max-reduced timings give every rank the
+    same plan, linear_all_reduce takes the bucket at or above M, exactly."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_run_tune_overlap, args=(2, _free_port(), out), nprocs=2, join=True)
+        r = torch.load(out, weights_only=True)
+    assert r["picks"][0] == r["picks"][1]
+    assert set(r["plan"]) == {300, 600} and r["k450"] == r["plan"][600]
+    assert r["keys"] == ["k1", "k2", "k4", "pick"]
+    assert r["err"] < 1e-4
+
+
 def _run_moe(rank, world, port, out_path):
     import torch.distributed as dist
     from k8s_llm_rca_amd.models.config import get_config

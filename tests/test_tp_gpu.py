@@ -484,8 +484,14 @@ def _tune_worker(rank, world, port, out_dir):
     wd = (torch.randn(H, 7168, device="cuda", generator=g) * 0.02).bfloat16()
     nw = torch.ones(H, device="cuda").bfloat16()
     rep = car.tune([("o", wo), ("down", wd)], nw, 1e-5, (16, 64, 256, 4096), iters=3, rounds=2)
+    # the prefill-size GEMM / all-reduce overlap depth (steps past the executor's buffer:
+    # row chunks, each chunk's xGMI all-reduce on the comm stream beside the next GEMM)
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, custom_ar=car, xgmi_only=True)
+    ov = pc.tune_overlap([("o", wo), ("down", wd)], [4096], iters=2, rounds=1)
     res = {"plan": {int(k): list(v) for k, v in car.plan.items()}, "rep": {int(k): v for k, v in rep.items()},
-           "for_40": list(car.plan_for(40, H)), "for_5000": list(car.plan_for(5000, H)), "status": car.status()}
+           "for_40": list(car.plan_for(40, H)), "for_5000": list(car.plan_for(5000, H)), "status": car.status(),
+           "ov": {int(k): v["pick"] for k, v in ov.items()}}
     car.close()
     torch.save(res, os.path.join(out_dir, f"tune{rank}.pt"))
     dist.barrier()
@@ -508,5 +514,6 @@ def test_xgmi_epilogue_tuning_same_plan_on_every_rank():
     assert a["plan"] == b["plan"] and set(a["plan"]) == {16, 64, 256}   # 4096 x 4096 x 2 B > 16 MiB
     assert a["for_40"] == a["plan"][64]
     assert a["for_5000"] == [2, False]
+    assert a["ov"] == b["ov"] and set(a["ov"]) == {4096} and a["ov"][4096] in (1, 2, 4)
     for T, r in a["rep"].items():
         assert "one_shot" in r and "two_shot" in r and all(v > 0 for k, v in r.items() if k != "pick")

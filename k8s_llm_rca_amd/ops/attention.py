@@ -203,6 +203,7 @@ _DECODE_PLANNER = "makespan"
 # everywhere.  0 = off.
 DECODE_LOW_UNITS = KNOBS.decode_low_units
 DECODE_LOW_PARTS = tuple(range(64, 1537, 64))
+DECODE_LOW_ROWS = 8  # the measured range of the rule (1-8 rows); larger steps keep the makespan planner
 
 
 def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candidates=None,
@@ -223,7 +224,7 @@ def plan_decode_split(ctx_lens, nkv: int, slots: int = DECODE_WAVE_SLOTS, candid
     import numpy as np
     c = np.asarray(ctx_lens, dtype=np.int64)
     mx = int(c.max()) if c.size else 1
-    if DECODE_LOW_UNITS and candidates is None and c.size:
+    if DECODE_LOW_UNITS and candidates is None and 0 < c.size <= DECODE_LOW_ROWS:
         P0 = min(DECODE_PARTS)
         if nkv * int(((c + P0 - 1) // P0).sum()) <= slots:  # one round: the low-batch rule
             for P in DECODE_LOW_PARTS:

@@ -53,6 +53,40 @@ __device__ __forceinline__ void rope_pair(float a, float b, float co, float si, 
   hi = fmaf(b, co, __fmul_rn(a, si));
 }
 
+// Sum of the `splits` fp32 partials of 8 consecutive outputs, p[s * stride ..
+// + 8) for s < splits, in split order (p0 + p1 + p2 ...).  For splits <= 4 every
+// load is issued before the first add (unconditional: past the last split the
+// address is clamped to it -- an L2 hit that is not added), so a row of a
+// split-K consumer pays one memory latency instead of `splits` dependent ones;
+// the arithmetic, and hence every bit, is the plain loop's.
+__device__ __forceinline__ void sum_splits8(const float* p, size_t stride, int splits, f32x4& a0, f32x4& a1) {
+  constexpr int kPre = 4;
+  if (splits <= kPre) {
+    f32x4 b0[kPre], b1[kPre];
+#pragma unroll
+    for (int sp = 0; sp < kPre; ++sp) {
+      const float* q = p + (size_t)(sp < splits ? sp : splits - 1) * stride;
+      b0[sp] = *reinterpret_cast<const f32x4*>(q);
+      b1[sp] = *reinterpret_cast<const f32x4*>(q + 4);
+    }
+    a0 = b0[0];
+    a1 = b1[0];
+#pragma unroll
+    for (int sp = 1; sp < kPre; ++sp)
+      if (sp < splits) {
+        a0 += b0[sp];
+        a1 += b1[sp];
+      }
+    return;
+  }
+  a0 = *reinterpret_cast<const f32x4*>(p);
+  a1 = *reinterpret_cast<const f32x4*>(p + 4);
+  for (int sp = 1; sp < splits; ++sp) {
+    a0 += *reinterpret_cast<const f32x4*>(p + sp * stride);
+    a1 += *reinterpret_cast<const f32x4*>(p + sp * stride + 4);
+  }
+}
+
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

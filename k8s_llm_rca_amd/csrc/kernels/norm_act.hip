@@ -43,14 +43,8 @@ __global__ void __launch_bounds__(256) rmsnorm_kernel(const uint16_t* __restrict
     if (i < nv) {
       u16x8 a;
       if constexpr (PART) {
-        const float* pr = part + (size_t)row * H + i * 8;
-        const size_t TH = (size_t)T * H;
-        f32x4 a0 = *reinterpret_cast<const f32x4*>(pr);
-        f32x4 a1 = *reinterpret_cast<const f32x4*>(pr + 4);
-        for (int sp = 1; sp < splits; ++sp) {
-          a0 += *reinterpret_cast<const f32x4*>(pr + sp * TH);
-          a1 += *reinterpret_cast<const f32x4*>(pr + sp * TH + 4);
-        }
+        f32x4 a0, a1;
+        sum_splits8(part + (size_t)row * H + i * 8, (size_t)T * H, splits, a0, a1);
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           a[j] = f2bf(a0[j]);
@@ -131,12 +125,8 @@ __device__ __forceinline__ u16x8 qkv_piece(const uint16_t* row, const float* pro
   if constexpr (!PART) {
     return *reinterpret_cast<const u16x8*>(row + col);
   } else {
-    f32x4 a0 = *reinterpret_cast<const f32x4*>(prow + col);
-    f32x4 a1 = *reinterpret_cast<const f32x4*>(prow + col + 4);
-    for (int s = 1; s < splits; ++s) {
-      a0 += *reinterpret_cast<const f32x4*>(prow + s * MN + col);
-      a1 += *reinterpret_cast<const f32x4*>(prow + s * MN + col + 4);
-    }
+    f32x4 a0, a1;
+    sum_splits8(prow + col, MN, splits, a0, a1);
     u16x8 o;
 #pragma unroll
     for (int v = 0; v < 4; ++v) {

@@ -62,14 +62,8 @@ __device__ __forceinline__ void norm_rows_to_lds(uint16_t* xs, int M, const Norm
       if (tid < 256 && i < nv) {
         u16x8 xa;
         if (a.part) {
-          const float* pr = a.part + (size_t)m * a.H + i * 8;
-          const size_t TH = (size_t)M * a.H;
-          f32x4 a0 = *reinterpret_cast<const f32x4*>(pr);
-          f32x4 a1 = *reinterpret_cast<const f32x4*>(pr + 4);
-          for (int sp = 1; sp < a.splits; ++sp) {
-            a0 += *reinterpret_cast<const f32x4*>(pr + sp * TH);
-            a1 += *reinterpret_cast<const f32x4*>(pr + sp * TH + 4);
-          }
+          f32x4 a0, a1;
+          sum_splits8(a.part + (size_t)m * a.H + i * 8, (size_t)M * a.H, a.splits, a0, a1);
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
             xa[j] = f2bf(a0[j]);

@@ -145,7 +145,13 @@ _big_tail = KNOBS.big_tail
 def reserve_big_ws(dev: torch.device, enable: bool = None) -> None:
     """gemm_big's split-tail workspace on ``dev`` (csrc/kernels/gemm_big.hip:
     256 fp32 partial tiles + tickets, zeroed once): without it the kernel runs
-    a partial last wave of whole tiles.  ``enable=False`` unregisters it (A/B)."""
+    a partial last wave of whole tiles.  ``enable=False`` unregisters it (A/B).
+
+    One workspace per device, so gemm_big launches must not overlap in time on
+    that device: two in flight would mix their partial tiles and tickets.  The
+    engine issues every projection on its one compute stream (the TP overlap's
+    side stream carries only collectives, ``parallel/groups.py``); a second
+    stream issuing gemm_big needs its own workspace or an event between them."""
     dev = torch.device(dev)
     if dev.type != "cuda":
         return

@@ -44,6 +44,14 @@ TRUNCATION_CONTRACT = {"trunc_low": 0.5, "keep_seed": 2, "policy": "sticky"}
 REF_MAX_ANALYSES_PER_S = 0.033  # 1/(20 s + 10 s) best case of the sequential driver
 
 
+def _tail_foreign(eng) -> int:
+    try:
+        from ..ops import linear as LIN
+        return LIN.big_tail_foreign(eng.device)
+    except Exception:  # noqa: BLE001 -- a CPU engine / no library
+        return 0
+
+
 def _native_cpu() -> Dict[int, tuple]:
     """(user, system) CPU seconds per native (non-Python) thread of this
     process, by thread id."""
@@ -411,7 +419,8 @@ def run(args) -> Optional[Dict[str, Any]]:
     gq = {k: 1e3 * v["total_s"] for k, v in tracing.snapshot().items()}
     bstats = [dict(b.stats) for b in batchers]
     lat = stream.window(t0, t_end + 1e-9)
-    err_timed = sum(1 for t, _, ok in list(stream.done) if not ok and t0 <= t <= t_end)
+    err_timed = sum(1 for t, _, ok, *_ in list(stream.done) if not ok and t0 <= t <= t_end)
+    stage3 = stream.stage3(t0, t_end + 1e-9)
     # ---- optional no-hints window (disclosure): the same engine and stream with the
     # oracle hints off, timed after one full turnover of the in-flight analyses
     nh = None
@@ -475,6 +484,10 @@ def run(args) -> Optional[Dict[str, Any]]:
         "analyses_timed": total,
         "errors": err_timed,
         "errors_total": stream.n_err,
+        # timed analyses whose pipeline reached stage 3 (a statepath was analyzed); cni_failure
+        # incidents never do: the message names the pod, not the Node the metapath ends at, so
+        # message_compatible filters every record (the reference's own filter, generate_query.py:104-129)
+        "stage3_reached": stage3,
         "abandoned_at_shutdown": stream.n_abandoned,
         "truncated_by_time_budget": truncated,
         "tokens": {"sampled": d["sampled_tokens"], "forced": d["forced_tokens"], "prefill": d["prefill_tokens"],
@@ -517,6 +530,8 @@ def run(args) -> Optional[Dict[str, Any]]:
                    # measured GEMM tables in use (decode dispatch; hipBLASLt solution buckets registered)
                    "gemm_dispatch": bool(getattr(eng, "gemm_dispatch", False)),
                    "blaslt_buckets": int(getattr(eng, "lib_algos", 0) or 0),
+                   # gemm_big launches that ran without the split tail (a stream other than the engine's)
+                   "big_tail_foreign": _tail_foreign(eng),
                    # K8SRCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
                    **({k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}
                       if d["eager_gpu_s"] or d["graph_gpu_s"] else {})},

@@ -73,6 +73,7 @@
 // Reference parity: replaces the hipBLASLt call on the prefill path of
 // models/llama.py (the reference's GPT-4 prompt processing of the whole thread
 // history, /root/reference/common/openai_generic_assistant.py:45-51).
+#include <mutex>
 #include <type_traits>
 
 #include "common.h"
@@ -581,13 +582,18 @@ __global__ void __launch_bounds__(256) big_reduce_kernel(const float* __restrict
 // sum the wrong slices.  So the workspace belongs to ONE stream: the first
 // launch that uses it claims it (g_tail_owner), and a launch on any other
 // stream runs without the split tail (whole-tile last wave: slower, never
-// wrong).  k8s_gemm_big_set_ws releases the claim.  
+// wrong).  k8s_gemm_big_set_ws releases the claim.    The engine
+// claims it explicitly for its compute stream at init (k8s_gemm_big_claim_ws,
+// ADVICE r5), so a short-lived stream that happens to launch first (a capture's
+// warm-up, a tuning side stream) can no longer take it; claims are serialised
+// by g_tail_mu, so two host threads never both own it.
 constexpr int kTailUnits = 256;
 constexpr size_t kTailWsBytes = (size_t)kTailUnits * BM * BN * 4 + kTailUnits * 4;
 static void* g_tail_ws[16] = {};
 static hipStream_t g_tail_owner[16] = {};
 static bool g_tail_claimed[16] = {};
 static long g_tail_foreign[16] = {};  // launches that skipped the tail (another stream owns it)
+static std::mutex g_tail_mu;
 
 // (tail tiles r, split S) for T tiles of nt K-tiles on 256 CUs: the last partial
 // wave's r tiles in r x S units (S in {4, 2}: r S <= 256, nt % (2 S) == 0, >= 8 K-tiles each).
@@ -618,11 +624,16 @@ static int launch(const void* x, int ldx, const void* w, void* y, int ldy, int M
   if (splits == 1) {
     int dev = 0;
     if (hipGetDevice(&dev) == hipSuccess && dev >= 0 && dev < 16 && g_tail_ws[dev]) {
-      if (!g_tail_claimed[dev]) {
-        g_tail_claimed[dev] = true;
-        g_tail_owner[dev] = s;
+      bool mine;
+      {
+        std::lock_guard<std::mutex> g(g_tail_mu);
+        if (!g_tail_claimed[dev]) {
+          g_tail_claimed[dev] = true;
+          g_tail_owner[dev] = s;
+        }
+        mine = g_tail_owner[dev] == s;
       }
-      if (g_tail_owner[dev] != s) {
+      if (!mine) {
         ++g_tail_foreign[dev];
       } else {
         tail_plan(T, K / BK, tr, ts);
@@ -709,8 +720,20 @@ K8S_API long k8s_gemm_big_ws_bytes() { return (long)k8s::big::kTailWsBytes; }
 K8S_API int k8s_gemm_big_set_ws(void* ws) {
   int dev = 0;
   if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return (int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(k8s::big::g_tail_mu);
   k8s::big::g_tail_ws[dev] = ws;
   k8s::big::g_tail_claimed[dev] = false;  // the next launch that uses it claims it for its stream
+  return 0;
+}
+// Give the current device's split-tail workspace to stream `s` (the engine's
+// compute stream); launches on every other stream run without the tail.
+K8S_API int k8s_gemm_big_claim_ws(hipStream_t s) {
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 16) return (int)hipErrorInvalidValue;
+  std::lock_guard<std::mutex> g(k8s::big::g_tail_mu);
+  if (!k8s::big::g_tail_ws[dev]) return (int)hipErrorInvalidValue;
+  k8s::big::g_tail_claimed[dev] = true;
+  k8s::big::g_tail_owner[dev] = s;
   return 0;
 }
 // launches on this device that ran without the split tail because another

@@ -87,7 +87,9 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
             from ..ops import gemm_tuning
             from ..ops import linear as LIN
             gemm_tuning.load(self.mc.name, self.pc.tp_size)
-            LIN.reserve_lib_workspace(self.device)
+            from ..ops._lib import stream_ptr
+            with torch.cuda.device(self.device):  # the engine's compute stream owns gemm_big's split tail
+                LIN.reserve_lib_workspace(self.device, claim_stream=stream_ptr())
             self.lib_algos = LIN.load_lib_algos(LIN.lib_algos_path(self.mc.name, self.pc.tp_size))
             self.gemm_dispatch = LIN.load_dispatch(LIN.dispatch_path(self.mc.name, self.pc.tp_size))
             # prefill-size M ranges where the hand-written gemm_big beats hipBLASLt
@@ -206,13 +208,20 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         log.info("xGMI epilogue plan tuned in %.1f s: %s", time.perf_counter() - t0,
                  {T: r["pick"] for T, r in rep.items()})
         # steps whose all-reduce does not fit the executor's buffer take the Python
-        # path's row-chunked GEMM / all-reduce overlap: its depth per bucket, timed here
+        # path's row-chunked GEMM / all-reduce overlap: its depth AND transport (the
+        # xGMI kernels vs RCCL) per bucket, timed here.  On a "nccl" group the
+        # prefill-size buckets the executor carries are timed too, for the report
+        # (RCCL measured against the xGMI kernels on the fabric);
+        # the executor keeps its fused xGMI epilogue for them.
         H = int(L0["wo"].shape[0])
         big = [T for T in (1024, 2048, 4096, 8192, 16384)
-               if T <= self.cfg.max_batch_tokens and T * H * 2 + 4 * T > car.max_bytes]
+               if T <= self.cfg.max_batch_tokens and (T * H * 2 + 4 * T > car.max_bytes or self.pc.rccl_ok())]
         ov = self.pc.tune_overlap(shapes, big) if big else {}
+        for T, r in ov.items():
+            r["executor"] = T * H * 2 + 4 * T <= car.max_bytes
         if ov:
-            log.info("GEMM / all-reduce overlap depth tuned: %s", {T: r["pick"] for T, r in ov.items()})
+            log.info("GEMM / all-reduce overlap tuned (depth, transport): %s",
+                     {T: (r["pick"], r["transport"]) for T, r in ov.items()})
         return {"tune_s": round(time.perf_counter() - t0, 2), "buckets": rep, "overlap": ov}
 
     def _workspace_bytes(self) -> int:

@@ -46,6 +46,8 @@ _SIGS = {
     "k8s_gemm_big_rope": [P, I, P, P, I, I, I, I, P, P, P, P, P, I, I, I, I, P],
     "k8s_gemm_big_ws_bytes": [],
     "k8s_gemm_big_set_ws": [P],
+    "k8s_gemm_big_claim_ws": [P],
+    "k8s_gemm_big_tail_foreign": [],
     "k8s_gemm_stream_silu": [P, I, P, P, I, I, I, I, I, P],
     "k8s_gemm_stream_silu_norm": [P, I, P, I, P, P, P, F, P, P, I, I, I, I, I, P],
     "k8s_gemm_skinny_rope_norm": [P, I, P, I, P, P, P, F, P, P, I, I, I, I, P, P, P, P, P, I, I, I, P],
@@ -77,6 +79,8 @@ _SIGS = {
     "k8s_get_knob": [I],
     "k8s_walks": [P, P, P, P, P, P, P, P, P, P, P, I, I, I, I, I, I, P, P, P, P],
 }
+# entry points whose C return type is not int
+_RESTYPES = {"k8s_gemm_big_ws_bytes": ctypes.c_long, "k8s_gemm_big_tail_foreign": ctypes.c_long}
 
 
 def lib():
@@ -100,7 +104,7 @@ def lib():
                 if fn is None:
                     continue
                 fn.argtypes = args
-                fn.restype = ctypes.c_int
+                fn.restype = _RESTYPES.get(name, ctypes.c_int)
             push_native(L)
             _lib = L
     return _lib

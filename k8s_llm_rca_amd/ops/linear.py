@@ -130,12 +130,25 @@ def linear_f32out(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return x.float() @ w.float().t()
 
 
-def reserve_lib_workspace(dev: torch.device) -> None:
+def reserve_lib_workspace(dev: torch.device, claim_stream: int = None) -> None:
     """Allocate the hipBLASLt workspace (and gemm_big's split-tail workspace)
-    before any HIP-graph capture."""
+    before any HIP-graph capture.  ``claim_stream`` (a raw hipStream_t): the
+    stream that owns the split tail (the engine's compute stream)."""
     if dev not in _blaslt_ws:
         _blaslt_ws[dev] = torch.empty(BLASLT_WS_BYTES, dtype=torch.uint8, device=dev)
     reserve_big_ws(dev)
+    if claim_stream is not None and dev in _big_ws and _big_tail:
+        with torch.cuda.device(dev):
+            check(lib().k8s_gemm_big_claim_ws(claim_stream), "gemm_big_claim_ws")
+
+
+def big_tail_foreign(dev: torch.device) -> int:
+    """gemm_big launches on ``dev`` that ran without the split tail because
+    another stream owns its workspace (reported in the bench line)."""
+    if torch.device(dev).type != "cuda":
+        return 0
+    with torch.cuda.device(dev):
+        return int(lib().k8s_gemm_big_tail_foreign())
 
 
 _big_ws: Dict[torch.device, torch.Tensor] = {}

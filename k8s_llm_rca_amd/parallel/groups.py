@@ -37,87 +37,127 @@ class ParallelContext:
     # pipeline depth per row-count bucket, timed on this fabric at init
     # (tune_overlap): the bucket at or above M, else ar_chunks
     chunk_plan: Optional[dict] = None
+    # transport per row-count bucket (tune_overlap, same lookup): True = RCCL
+    # (torch.distributed "nccl") for that step's all-reduces, False = the xGMI
+    # kernels.  None: xGMI whenever the communicator takes the message.
+    rccl_plan: Optional[dict] = None
+
+    @staticmethod
+    def _bucket(plan: Optional[dict], M: int, default):
+        if plan:
+            for b in sorted(plan):
+                if b >= M:
+                    return plan[b]
+        return default
 
     def chunks_for(self, M: int) -> int:
-        if self.chunk_plan:
-            for b in sorted(self.chunk_plan):
-                if b >= M:
-                    return self.chunk_plan[b]
-        return self.ar_chunks
+        return self._bucket(self.chunk_plan, M, self.ar_chunks)
 
-    def tune_overlap(self, shapes, buckets, depths=(1, 2, 4), iters: int = 4, rounds: int = 3) -> dict:
+    def rccl_for(self, M: int) -> bool:
+        """This M-row step's all-reduces go to RCCL (the tuned plan's pick)."""
+        return bool(self._bucket(self.rccl_plan, M, False))
+
+    def rccl_ok(self) -> bool:
+        """RCCL can carry this group's data: a "nccl" group (one device per rank;
+        RCCL refuses ranks that share a GPU, so a loopback rehearsal is gloo)."""
+        return self.tp_size > 1 and self.tp_group is not None and dist.get_backend(self.tp_group) == "nccl"
+
+    def _time_candidate(self, shapes, x, k: int, rccl: bool, iters: int) -> float:
+        """us per (o, down) pair of :meth:`linear_all_reduce` with depth ``k``
+        on one transport (every rank runs the same calls in lockstep)."""
+        import time
+        dev = shapes[0][1].device
+        cuda = dev.type == "cuda"
+        self.chunk_plan, self.rccl_plan = {1 << 30: k}, {1 << 30: rccl}
+        for name, w in shapes:  # warm, and every rank enters this candidate together
+            self.linear_all_reduce(x[name], w)
+        if cuda:
+            torch.cuda.synchronize(dev)
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            for name, w in shapes:
+                self.linear_all_reduce(x[name], w)
+        if cuda:
+            torch.cuda.synchronize(dev)
+        return (time.perf_counter() - t0) * 1e6 / iters
+
+    def tune_overlap(self, shapes, buckets, depths=(1, 2, 4), iters: int = 4, rounds: int = 3,
+                     transports=None) -> dict:
         """Per row-count bucket T, the GEMM / all-reduce pipeline depth of
         :meth:`linear_all_reduce` (1 = no overlap: GEMM, then one all-reduce;
         k = k row chunks, chunk i's all-reduce on the comm stream beside chunk
-        i+1's GEMM), timed ON THIS FABRIC with the real row-parallel weights
-        [(name, w [H, K_local])].  Every rank runs the same collectives in
-        lockstep and each timing is max-reduced over the TP group, so all
-        ranks hold the same plan (``chunk_plan``); the report goes into the
-        bench line.  Round 4's default (4 chunks everywhere) and its loopback
-        A/B (a row-chunked decode-size overlap measured slower) could not show
-        what xGMI links do at prefill sizes."""
-        import time
+        i+1's GEMM) AND its transport -- the xGMI kernels (two-shot over the
+        hipIpc buffers, buffer-sized chunks past it) or RCCL's multi-channel
+        rings (the north star's RCCL path is measured against
+        the custom kernels per bucket, not assumed away) -- timed ON THIS
+        FABRIC with the real row-parallel weights [(name, w [H, K_local])].
+        ``transports``: subset of ("xgmi", "rccl"); default every one this
+        group can run (RCCL needs a "nccl" group, xGMI the communicator).
+        Every rank runs the same collectives in lockstep and each timing is
+        max-reduced over the TP group, so all ranks hold the same plan
+        (``chunk_plan``, ``rccl_plan``); the report goes into the bench line."""
         if self.tp_size == 1:
             return {}
         dev = shapes[0][1].device
         cuda = dev.type == "cuda"
-        report, plan = {}, {}
-        saved = self.chunk_plan
+        if transports is None:
+            transports = tuple(t for t, ok in (("xgmi", self.custom_ar is not None and cuda),
+                                                ("rccl", self.rccl_ok() or not cuda)) if ok)
+        cands = [(tr, k) for tr in transports for k in depths]
+        report, plan, rplan = {}, {}, {}
+        saved = (self.chunk_plan, self.rccl_plan)
         for T in sorted(set(int(b) for b in buckets)):
             x = {name: torch.randn(T, int(w.shape[1]), device=dev).to(w.dtype) for name, w in shapes}
-            us = {k: [] for k in depths}
+            us = {c: [] for c in cands}
             try:
                 for _ in range(rounds):
-                    for k in depths:
-                        self.chunk_plan = {1 << 30: k}
-                        for name, w in shapes:  # warm, and every rank enters this candidate together
-                            self.linear_all_reduce(x[name], w)
-                        if cuda:
-                            torch.cuda.synchronize(dev)
-                        t0 = time.perf_counter()
-                        for _ in range(iters):
-                            for name, w in shapes:
-                                self.linear_all_reduce(x[name], w)
-                        if cuda:
-                            torch.cuda.synchronize(dev)
-                        us[k].append((time.perf_counter() - t0) * 1e6 / iters)
+                    for tr, k in cands:
+                        us[(tr, k)].append(self._time_candidate(shapes, x, k, tr == "rccl", iters))
             finally:
-                self.chunk_plan = saved
+                self.chunk_plan, self.rccl_plan = saved
             med = torch.tensor([sorted(v)[len(v) // 2] for v in us.values()], dtype=torch.float64)
             on_dev = cuda and dist.get_backend(self.tp_group) == "nccl"
             t = med.to(dev) if on_dev else med
             dist.all_reduce(t, op=dist.ReduceOp.MAX, group=self.tp_group)  # the slowest rank's view
             med = t.cpu().tolist()
-            best = min(range(len(depths)), key=lambda i: med[i])
-            plan[T] = depths[best]
-            report[T] = {f"k{k}": round(v, 1) for k, v in zip(depths, med)}
-            report[T]["pick"] = depths[best]
-        self.chunk_plan = plan
+            best = min(range(len(cands)), key=lambda i: (med[i], i))
+            tr, k = cands[best]
+            plan[T], rplan[T] = k, tr == "rccl"
+            report[T] = {(f"k{k_}" if tr_ == "xgmi" else f"{tr_}_k{k_}"): round(v, 1)
+                         for (tr_, k_), v in zip(cands, med)}
+            report[T]["pick"] = k
+            report[T]["transport"] = tr
+        self.chunk_plan, self.rccl_plan = plan, rplan
         return report
 
     @property
     def is_tp(self) -> bool:
         return self.tp_size > 1
 
-    def _xgmi(self, t: torch.Tensor) -> bool:
+    def _xgmi(self, t: torch.Tensor, rccl: bool = False) -> bool:
         car = self.custom_ar
-        return car is not None and t.is_cuda and (car.mode_for(t) != 0 or (self.xgmi_only and car.eligible(t)))
+        return (not rccl and car is not None and t.is_cuda
+                and (car.mode_for(t) != 0 or (self.xgmi_only and car.eligible(t))))
 
-    def all_reduce(self, t: torch.Tensor) -> torch.Tensor:
+    def all_reduce(self, t: torch.Tensor, rccl: Optional[bool] = None) -> torch.Tensor:
+        """Sum ``t`` over the TP group in place.  ``rccl``: the transport the
+        tuned plan picked for this step (default: by ``t``'s row count)."""
         if self.tp_size > 1:
-            if self._xgmi(t):
+            if rccl is None:
+                rccl = bool(self.rccl_plan) and t.dim() > 0 and self.rccl_for(t.shape[0])
+            if self._xgmi(t, rccl):
                 return self.custom_ar(t)
-            if self.xgmi_only and t.is_cuda:
+            if self.xgmi_only and t.is_cuda and not rccl:
                 raise ValueError(f"xgmi_only: a {t.dtype} all-reduce of shape {tuple(t.shape)} has no xGMI path")
             dist.all_reduce(t, group=self.tp_group)
         return t
 
-    def _all_reduce_async(self, t: torch.Tensor):
+    def _all_reduce_async(self, t: torch.Tensor, rccl: bool = False):
         """Start an all-reduce of ``t`` that overlaps later work on the compute
         stream; returns a handle whose ``wait()`` orders the compute stream
         after it."""
         car = self.custom_ar
-        if self._xgmi(t):
+        if self._xgmi(t, rccl):
             cur = torch.cuda.current_stream(t.device)
             if self.comm_stream is None:
                 self.comm_stream = torch.cuda.Stream(t.device)
@@ -147,15 +187,16 @@ class ParallelContext:
             return lin(x, w)
         M, N = x.shape[0], w.shape[0]
         k = self.chunks_for(M)
+        rccl = bool(self.rccl_plan) and self.rccl_for(M)
         if k <= 1 or M * N * x.element_size() < self.overlap_min_bytes * k:
-            return self.all_reduce(lin(x, w))
+            return self.all_reduce(lin(x, w), rccl=rccl)
         works, parts = [], []
         if M <= 256:
             step = -(-N // k)
             step = -(-step // 8) * 8
             for a in range(0, N, step):
                 y = lin(x, w[a:a + step]).contiguous()
-                works.append(self._all_reduce_async(y))
+                works.append(self._all_reduce_async(y, rccl))
                 parts.append(y)
             for h in works:
                 h.wait()
@@ -165,7 +206,7 @@ class ParallelContext:
         for a in range(0, M, step):
             y = out[a:a + step]
             torch.matmul(x[a:a + step], w.t(), out=y)  # prefill-sized: library GEMM straight into the slice
-            works.append(self._all_reduce_async(y))
+            works.append(self._all_reduce_async(y, rccl))
         for h in works:
             h.wait()
         return out

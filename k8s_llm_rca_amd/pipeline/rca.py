@@ -308,7 +308,7 @@ class IncidentStream:
         self._cv = threading.Condition()
         self._next = 0
         self._stop = False
-        self.done: List[tuple] = []   # (t_done, latency_s, ok) in completion order
+        self.done: List[tuple] = []   # (t_done, latency_s, ok, stage3, fault) in completion order
         self.n_ok = 0
         self.n_err = 0
         self.n_abandoned = 0
@@ -381,9 +381,11 @@ class IncidentStream:
                 self._next += 1
             inc = self.incidents[i % len(self.incidents)]
             t = time.perf_counter()
-            ok, err = True, None
+            ok, err, stage3 = True, None, False
             try:
                 r = p.analyze(inc.message, inc if self.hints else None)
+                # reached stage 3: some metapath's query left a statepath to analyze
+                stage3 = any(a.get("statepath") for a in r.get("analysis", []))
                 if p.last_failed_runs:
                     ok, err = False, f"{p.last_failed_runs} LLM run(s) failed: {r.get('error_message', '')[:60]!r}"
             except Exception as e:  # noqa: BLE001 - counted, never fatal to the stream
@@ -395,7 +397,7 @@ class IncidentStream:
                 if self._stop and not ok:  # cut short by the shutdown (service closed), not a failure
                     self.n_abandoned += 1
                     return
-                self.done.append((t1, t1 - t, ok))
+                self.done.append((t1, t1 - t, ok, stage3, getattr(inc, "fault", "")))
                 if ok:
                     self.n_ok += 1
                     self.ok_by_pipeline[j] += 1
@@ -433,4 +435,19 @@ class IncidentStream:
     def window(self, t0: float, t1: float) -> List[float]:
         """Latencies of the successful analyses completed in ``[t0, t1)``."""
         with self._cv:
-            return [lat for t, lat, ok in self.done if ok and t0 <= t < t1]
+            return [lat for t, lat, ok, *_ in self.done if ok and t0 <= t < t1]
+
+    def stage3(self, t0: float, t1: float) -> Dict[str, Any]:
+        """Of the successful analyses completed in ``[t0, t1)``: the fraction
+        that reached stage 3 (analyze_root_cause ran on at least one statepath),
+        and ``{fault: [reached, total]}``."""
+        by: Dict[str, List[int]] = {}
+        with self._cv:
+            rows = [(s3, f) for t, _, ok, s3, f in self.done if ok and t0 <= t < t1]
+        for s3, f in rows:
+            c = by.setdefault(f or "?", [0, 0])
+            c[0] += int(s3)
+            c[1] += 1
+        n = len(rows)
+        return {"fraction": round(sum(int(s3) for s3, _ in rows) / n, 4) if n else 0.0,
+                "by_fault": dict(sorted(by.items()))}

@@ -26,6 +26,7 @@ def knob():
     old = {}
 
     def set_(name, value):
+        K._runtime_settable(name)  # a knob copied into a module constant at import cannot be set here
         if name not in old:
             old[name] = getattr(K.KNOBS, name)
         setattr(K.KNOBS, name, value)

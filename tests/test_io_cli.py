@@ -111,6 +111,9 @@ def test_bench_self_spawns_ranks_cpu(tmp_path):
     d = _json.loads(lines[0])
     assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2" and d["steps"] == 2
     assert d["analyses_timed"] == 4 and d["errors"] == 0 and not d["truncated_by_time_budget"]
+    # the line says which timed analyses reached stage 3
+    s3 = d["stage3_reached"]
+    assert 0.0 <= s3["fraction"] <= 1.0 and sum(v[1] for v in s3["by_fault"].values()) == d["analyses_timed"] // 2
     assert abs(d["config"]["graph_nodes"] - 300) <= 0.2 * 300
     # the reference's thread regime: every pipeline's threads carry the replayed
     # incidents plus at least one engine-run incident when the timer starts

@@ -86,3 +86,22 @@ def test_poison_scratch_fills_nan():
         assert torch.isnan(t).all()
         assert scratch(4, torch.int32, "cpu").dtype == torch.int32  # integer buffers are not poisoned
     assert scratch((2, 3), torch.bfloat16, "cpu").shape == (2, 3)
+
+
+def test_import_time_knobs_refuse_runtime_changes():
+    """knobs copied into a module constant at import (layer_exec._norm_fuse,
+    linear.SKINNY_MAX_M, ...) would change KNOBS with no effect: override / set_knob
+    refuse them and name the constant."""
+    assert "norm_fuse" in K.AT_IMPORT and "skinny_max_m" in K.AT_IMPORT
+    with pytest.raises(ValueError, match="layer_exec._norm_fuse"):
+        with K.override(norm_fuse=False):
+            pass
+    with pytest.raises(ValueError, match="SKINNY_MAX_M"):
+        K.set_knob("skinny_max_m", "8")
+    assert K.KNOBS.norm_fuse is True and K.KNOBS.skinny_max_m == 16
+    # every at-import knob really is copied at import: its name appears in the module it names
+    for name, where in K.AT_IMPORT.items():
+        parts = where.split(" ")[0].split(".")
+        paths = [os.path.join(PKG, *parts[:i]) + ".py" for i in range(len(parts), 0, -1)]
+        path = next(p for p in paths if os.path.exists(p))
+        assert f"KNOBS.{name}" in open(path).read(), (name, path)

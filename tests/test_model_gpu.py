@@ -257,3 +257,61 @@ def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
         outs.append(err)
     if graphs:
         assert eng.stats["graph_steps"] == 10
+
+
+@pytest.mark.parametrize("deferred", [True, False])
+@pytest.mark.parametrize("nl", [1, 2, 3])
+def test_layer_executor_norm_fuse_bit_identical(nl, deferred):
+    """steps of <= 4 rows with the fused RMSNorm prologues ON
+    (``st.norm_fuse == 3``: the input norm in the skinny RoPE qkv GEMM, the
+    post-attention norm in the SwiGLU stream gate_up GEMM) give the same
+    (prev, residual) and logits, bit for bit, as the executor with the fusion
+    off and as the Python layer loop -- for 1 / 2 / 3 layers (the residual
+    ping-pong between ``residual`` and ``res2`` ends on either buffer) and with
+    the o / down projections either split-K with their partials deferred into
+    the next norm, or not split."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    import torch.nn.functional as F
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.ops import layer_exec as LX
+    from k8s_llm_rca_amd.ops import linear as LIN
+    from tests.test_tp_gpu import _prefill_inputs
+    keys = [(1536, 512), (2048, 512), (512, 1024)]
+    saved = {k: LIN._dispatch.get(k) for k in keys}
+    fuse0 = LX._norm_fuse
+    try:
+        LIN._dispatch[(1536, 512)] = [(16, "skinny", -1, 1)]      # qkv: skinny + RoPE / KV-write epilogue
+        LIN._dispatch[(2048, 512)] = [(16, "stream", 4, 1)]       # gate_up: stream kernel's SwiGLU form
+        LIN._dispatch[(512, 1024)] = ([(16, "stream", 4, 2)] if deferred   # o / down: split-K, partials deferred
+                                      else [(16, "skinny", -1, 1)])
+        m = LlamaModel(get_config("tiny-llama", n_layers=nl, init_std=0.08), "cuda:0", torch.bfloat16, None, seed=4)
+        for T in (1, 2, 3, 4):
+            outs = {}
+            for mode in ("fused", "unfused", "python"):
+                LX._norm_fuse = mode == "fused"
+                LX.set_enabled(mode != "python")
+                inp, kc, vc = _prefill_inputs(m, T, seed=T)
+                logits = m.forward(inp, kc, vc).float().cpu()
+                rec = {"logits": logits, "kc": kc.float().cpu()}
+                if mode != "python":
+                    assert m._exec is not None
+                    assert m._exec.st.norm_fuse == (3 if mode == "fused" else 0), (mode, T)
+                    inp, kc, vc = _prefill_inputs(m, T, seed=T)
+                    res = F.embedding(inp.input_ids.long(), m.embed)
+                    prev, r = m._exec.run(inp, res, kc, vc)
+                    rec["prev"], rec["res"] = prev.float().cpu(), r.float().cpu()
+                outs[mode] = rec
+            a, b, c = outs["fused"], outs["unfused"], outs["python"]
+            assert torch.equal(a["prev"], b["prev"]) and torch.equal(a["res"], b["res"]), (nl, T, deferred)
+            assert torch.equal(a["logits"], b["logits"]) and torch.equal(a["logits"], c["logits"]), (nl, T, deferred)
+            assert torch.equal(a["kc"], b["kc"]) and torch.equal(a["kc"], c["kc"])
+    finally:
+        LX._norm_fuse = fuse0
+        LX.set_enabled(True)
+        for k, v in saved.items():
+            if v is None:
+                LIN._dispatch.pop(k, None)
+            else:
+                LIN._dispatch[k] = v

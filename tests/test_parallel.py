@@ -226,8 +226,60 @@ def test_tune_overlap_same_plan_on_every_rank():
         r = torch.load(out, weights_only=True)
     assert r["picks"][0] == r["picks"][1]
     assert set(r["plan"]) == {300, 600} and r["k450"] == r["plan"][600]
-    assert r["keys"] == ["k1", "k2", "k4", "pick"]
+    # on a gloo group the one transport is torch.distributed's own collective
+    assert r["keys"] == ["pick", "rccl_k1", "rccl_k2", "rccl_k4", "transport"]
     assert r["err"] < 1e-4
+
+
+def _run_tune_transport(rank, world, port, out_path):
+    """RCCL vs xGMI per bucket with fake, rank-dependent timings: each rank
+    alone would pick differently; the max-reduce must give one plan."""
+    import torch.distributed as dist
+    from k8s_llm_rca_amd.parallel.groups import ParallelContext
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    pc = ParallelContext(tp_size=world, tp_rank=rank, tp_group=dist.group.WORLD, overlap_min_bytes=64)
+    # (bucket, transport, depth) -> us on this rank.  Bucket 1024: rank 0 alone prefers xGMI k2 (90),
+    # rank 1 alone RCCL k1 (80); the per-candidate max is xgmi_k2 = 130 < rccl_k1 = 150 -> xGMI k2.
+    # Bucket 8192: RCCL k4 is the slowest-rank winner on both.
+    fake = {(1024, "xgmi", 2): (90, 130), (1024, "rccl", 1): (150, 80), (8192, "rccl", 4): (200, 210),
+            (8192, "xgmi", 4): (230, 190)}
+    seen = []
+
+    def timer(shapes, x, k, rccl, iters):
+        T = next(iter(x.values())).shape[0]
+        tr = "rccl" if rccl else "xgmi"
+        seen.append((T, tr, k, pc.rccl_for(T), pc.chunks_for(T)))
+        return float(fake.get((T, tr, k), (500, 500))[rank])
+
+    pc._time_candidate = timer
+    shapes = [("o", torch.randn(96, 48)), ("down", torch.randn(96, 80))]
+    rep = pc.tune_overlap(shapes, [1024, 8192], iters=1, rounds=1, transports=("xgmi", "rccl"))
+    res = {"plan": pc.chunk_plan, "rplan": pc.rccl_plan, "rep": rep,
+           "route": [pc.rccl_for(M) for M in (512, 1024, 2000, 8192, 20000)], "n": len(seen)}
+    objs = [None] * world
+    dist.all_gather_object(objs, res)
+    if rank == 0:
+        torch.save(objs, out_path)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_tune_overlap_rccl_vs_xgmi_same_plan_on_every_rank():
+    """the init-time tuning times RCCL against the xGMI kernels
+    per prefill-size bucket; the per-candidate max over ranks decides, so
+    every rank holds the same (depth, transport) plan, and steps route by it."""
+    with tempfile.TemporaryDirectory() as d:
+        out = os.path.join(d, "r.pt")
+        mp.spawn(_run_tune_transport, args=(2, _free_port(), out), nprocs=2, join=True)
+        a, b = torch.load(out, weights_only=True)
+    assert a["plan"] == b["plan"] == {1024: 2, 8192: 4}
+    assert a["rplan"] == b["rplan"] == {1024: False, 8192: True}
+    assert a["rep"][1024]["transport"] == "xgmi" and a["rep"][8192]["transport"] == "rccl"
+    assert a["rep"][1024]["k2"] == 130 and a["rep"][1024]["rccl_k1"] == 150   # the slowest rank's view
+    # rows up to 1024 -> xGMI, 1025..8192 -> RCCL, past the last bucket -> the default (xGMI)
+    assert a["route"] == [False, False, True, True, False]
+    assert a["n"] == 2 * 6   # 2 buckets x (2 transports x 3 depths)
 
 
 def _run_moe(rank, world, port, out_path):

@@ -388,7 +388,8 @@ def _prefill_inputs(m, T, seed=5):
     from k8s_llm_rca_amd.ops import attention as A
     BS = 64
     nb = -(-T // BS)
-    ids = torch.randint(0, 100000, (T,), generator=torch.Generator().manual_seed(seed), dtype=torch.int32)
+    ids = torch.randint(0, min(100000, m.cfg.vocab_size), (T,), generator=torch.Generator().manual_seed(seed),
+                        dtype=torch.int32)
     meta = A.AttnMeta(block_tables=torch.arange(nb, dtype=torch.int32).view(1, -1).cuda(),
                       ctx_lens=torch.tensor([T], dtype=torch.int32).cuda(),
                       q_start=torch.tensor([0, T], dtype=torch.int32).cuda(), num_seqs=1, decode=False,
@@ -402,7 +403,46 @@ def _prefill_inputs(m, T, seed=5):
     return inp, kc, vc
 
 
-def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb, layers=(2, 32)):
+def _fp32_reference_logits(m, T, seed=5):
+    """Plain-PyTorch fp32 forward of ``_prefill_inputs``'s sequence on the
+    TP=1 model's weights (each layer's weights upcast on the fly): the anchor
+    both the bf16 TP=1 and TP=2 engines are measured against (VERDICT r5 #5)."""
+    import torch.nn.functional as F
+    cfg = m.cfg
+    eps, D, nq, nkv = cfg.rms_eps, m.D, m.nq, m.nkv
+    ids = torch.randint(0, min(100000, cfg.vocab_size), (T,), generator=torch.Generator().manual_seed(seed),
+                        dtype=torch.int32).cuda()
+    half = D // 2
+    cs = m.cos_sin[:T].float()
+    cos, sin = cs[:, None, :half], cs[:, None, half:]
+
+    def norm(x, w):
+        return x * torch.rsqrt(x.pow(2).mean(-1, keepdim=True) + eps) * w.float()
+
+    def rope(x):  # [T, h, D], rotation pairs (i, i + D/2)
+        a, b = x[..., :half], x[..., half:]
+        return torch.cat([a * cos - b * sin, b * cos + a * sin], dim=-1)
+
+    h = m.embed[ids.long()].float()
+    for L in m.layers:
+        y = norm(h, L["in_norm"])
+        qkv = y @ L["wqkv"].float().t()
+        q = rope(qkv[:, :nq * D].view(T, nq, D))
+        k = rope(qkv[:, nq * D:(nq + nkv) * D].view(T, nkv, D))
+        v = qkv[:, (nq + nkv) * D:(nq + 2 * nkv) * D].view(T, nkv, D)
+        k, v = (t.repeat_interleave(nq // nkv, dim=1) for t in (k, v))
+        a = F.scaled_dot_product_attention(q.transpose(0, 1)[None], k.transpose(0, 1)[None], v.transpose(0, 1)[None],
+                                           is_causal=True, scale=m.scale)[0].transpose(0, 1).reshape(T, nq * D)
+        h = h + a @ L["wo"].float().t()
+        y = norm(h, L["post_norm"])
+        gu = y @ L["w_gu"].float().t()
+        I = gu.shape[1] // 2
+        h = h + (F.silu(gu[:, :I]) * gu[:, I:]) @ L["w_down"].float().t()
+    y = norm(h[T - 1:], m.final_norm)
+    return (y @ m.lm_head.float().t()).cpu()
+
+
+def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb, layers=(1, 2, 32)):
     import torch.distributed as dist
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     torch.cuda.set_device(0)
@@ -426,6 +466,8 @@ def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb, layers=(2, 32)):
             inp, kc, vc = _prefill_inputs(m, T)
             out[f"{nl}/{T}"] = {"logits": m.forward(inp, kc, vc).float().cpu(),
                                 "exec": m._exec is not None and m._exec.fits(T)}
+            if world == 1:
+                out[f"{nl}/{T}"]["fp32"] = _fp32_reference_logits(m, T)
         del m
         torch.cuda.empty_cache()
     if world > 1:
@@ -439,16 +481,17 @@ def _tp_logits_worker(rank, world, port, out_dir, Ts, max_mb, layers=(2, 32)):
 
 
 def test_tp2_llama3_8b_logits_match_tp1_one_gpu():
-    """Llama-3-8B at TP=2 as two processes on one MI355X (gloo
-    host group, every collective on the xGMI kernels) gives the TP=1 logits
-    within bf16 tolerance on a fixed prompt -- at T=300 through the native
-    executor's fused all-reduce + add + RMSNorm, and at T=1100 (past the 4 MiB
-    buffer) through the Python layer path's chunked all-reduce.  The TP sum
-    rounds each rank's row-parallel partial to bf16, so the two differ by
-    rounding that compounds with depth through a random-init stack (measured,
-    tools/tp_check.py, profiles/r5/tp_check.txt: 0.7 / 1.1 / 2.3 / 5.8 % at
-    1 / 2 / 8 / 32 layers, the same on both paths); a wrong shard or
-    collective is O(1) after one layer."""
+    """Llama-3-8B at TP=2 as two processes on one MI355X
+    (gloo host group, every collective on the xGMI kernels) at T=300 through
+    the native executor's fused all-reduce + add + RMSNorm, and at T=1100
+    (past the 4 MiB buffer) through the Python layer path's chunked
+    all-reduce -- both measured against an fp32 PyTorch forward of the same
+    weights (:func:`_fp32_reference_logits`) at 1, 2 and 32 layers.  The TP=2
+    engine must be as close to fp32 as the TP=1 engine is:
+    err(TP2) <= 1.25 err(TP1) + 1e-3.  (Round 5 bounded TP2 vs TP1 directly,
+    loosened to 10 % at 32 layers; bf16 drift through a random-init stack is
+    real -- profiles/r5/tp_check.txt -- but a bound on the difference cannot
+    tell it from a few % of a wrong shard or a stale chunk, the anchor can.)"""
     if not torch.cuda.is_available():
         pytest.skip("needs a GPU")
     Ts = (300, 1100)
@@ -459,15 +502,24 @@ def test_tp2_llama3_8b_logits_match_tp1_one_gpu():
         b = torch.load(os.path.join(d, "tp1.pt"), weights_only=True)
     assert a["status"] == 0
     assert a["2/300"]["exec"] and not a["2/1100"]["exec"]
-    for nl, bound in ((2, 0.02), (32, 0.1)):
+    rec = {}
+    for nl in (1, 2, 32):
         for T in Ts:
             x, y = a[f"{nl}/{T}"]["logits"][:, :128256], b[f"{nl}/{T}"]["logits"][:, :128256]
+            ref = b[f"{nl}/{T}"]["fp32"][:, :128256]
             assert torch.isfinite(x).all()
-            rel = ((x - y).norm() / y.norm()).item()
-            assert rel < bound, (nl, T, rel)
-            # the top tokens agree (bf16 reduction order differs between TP=1 and TP=2)
-            top = set(y.topk(5, -1).indices.view(-1).tolist())
-            assert int(x.argmax(-1)) in top, (nl, T)
+            e2 = ((x - ref).norm() / ref.norm()).item()
+            e1 = ((y - ref).norm() / ref.norm()).item()
+            rec[f"{nl}/{T}"] = {"tp2_vs_fp32": e2, "tp1_vs_fp32": e1, "tp2_vs_tp1": ((x - y).norm() / y.norm()).item()}
+            assert e2 <= 1.25 * e1 + 1e-3, (nl, T, e2, e1)
+            # the top token of each engine is among the fp32 forward's top 5
+            top = set(ref.topk(5, -1).indices.view(-1).tolist())
+            assert int(x.argmax(-1)) in top and int(y.argmax(-1)) in top, (nl, T)
+    out = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    if os.path.isdir(out):
+        import json
+        with open(os.path.join(out, "tp_fp32_anchor.json"), "w") as f:
+            json.dump(rec, f, indent=1)
 
 
 def _tune_worker(rank, world, port, out_dir):

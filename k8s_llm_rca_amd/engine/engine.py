@@ -163,6 +163,11 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         # knob step_timing: per-path host-issue vs GPU time of the forward
         self._step_timing = KNOBS.step_timing
         self._pending_ev: list = []
+        # knob step_trace=path: per-forward GPU start / end + host enqueue vs last token wait (JSONL)
+        self._trace = KNOBS.step_trace
+        self._trace_base = None
+        self._trace_buf: list = []
+        self._last_wait_end = None
         # debug (knob nonfinite_check): per-layer non-finite flags, read with each sampling
         self._nf = None
         if KNOBS.nonfinite_check and self.device.type == "cuda" and hasattr(self.model, "nf_flags"):
@@ -308,6 +313,12 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         if self._thread is not None:
             self._thread.join()
             self._thread = None
+        if self._trace is not None:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize(self.device)
+                if self._pending_ev:
+                    self._collect_timing()
+            self.flush_trace()
 
     def _loop(self) -> None:
         prof_path = KNOBS.profile_engine

@@ -197,6 +197,7 @@ class GraphRunnerMixin:
             n += n_sel
         dev_flat = torch.empty(n, dtype=torch.int32, device=self.device)
         dev_flat.copy_(host[:n], non_blocking=True)
+        self._trace_mark()
         ev = st["host_ev"][hi] = st["host_ev"][hi] or torch.cuda.Event(blocking=KNOBS.blocking_sync)
         ev.record()
         # the upload scattered into the graph's static inputs in one launch (csrc/kernels/norm_act.hip),

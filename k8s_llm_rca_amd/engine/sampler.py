@@ -266,6 +266,7 @@ class SamplerMixin:
         t1 = time.perf_counter()
         if fl.event is not None:
             fl.event.synchronize()
+        self._last_wait_end = time.perf_counter()
         if fl.status is not None and int(fl.status[0]) != 0:
             from ..parallel.xgmi import CommFault
             raise CommFault("xGMI collective timed out: a TP peer never arrived (allreduce STATUS set)")

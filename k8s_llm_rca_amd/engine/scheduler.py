@@ -194,7 +194,7 @@ class SchedulerMixin:
         step (still in flight: their tokens are on the device only) join this
         step as decode rows fed straight from the device tokens, and the host
         processes those tokens while this step's forward runs on the GPU."""
-        t_host0 = time.perf_counter()
+        t_host0 = self._t_step0 = time.perf_counter()
         if self._cancels or self.cfg.max_run_s is not None:
             ps0 = self._pending_sample
             self._apply_cancels(set(s.id for s in ps0[1]) if ps0 is not None else set())

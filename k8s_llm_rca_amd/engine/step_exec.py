@@ -111,9 +111,12 @@ class StepExecMixin:
         device tensor ``tok[src[i]]`` when ``src[i] >= 0`` (tokens sampled by
         the in-flight step, not yet on the host)."""
         t0 = time.perf_counter()
-        timed = self._step_timing and self.device.type == "cuda"
+        timed = (self._step_timing or self._trace is not None) and self.device.type == "cuda"
         if timed:
             ev = (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            if self._trace is not None and self._trace_base is None:
+                self._trace_base = (torch.cuda.Event(enable_timing=True), t0)
+                self._trace_base[0].record()
             ev[0].record()
         if spec is not None and self._chan is not None:
             _spec_tok(spec)  # TP: sample(k) -- a message + an all-gather -- goes before forward(k+1) on every rank
@@ -128,24 +131,48 @@ class StepExecMixin:
             if not chunks:
                 self.stats["decode_steps"] += 1
             kind = "eager"
-        dt = time.perf_counter() - t0
+        t1 = time.perf_counter()
+        dt = t1 - t0
         self.stats["forward_s"] += dt
         if timed:
             ev[1].record()
-            self._pending_ev.append((kind, dt, ev))
+            rec = None
+            if self._trace is not None:
+                ek, self._trace_evk = getattr(self, "_trace_evk", None), None
+                rec = {"step": self.stats["steps"], "kind": kind, "nd": len(decode), "_ek": ek,
+                       "np": sum(q for _, q in chunks), "t_enq0": t0, "t_enq1": t1, "t_wait": self._last_wait_end,
+                       "t_step": getattr(self, "_t_step0", None)}
+            self._pending_ev.append((kind, dt, ev, rec))
         return out
 
     def _collect_timing(self) -> None:
         """Fold completed step events into stats (with overlapped steps the
         newest forward may still be running: its events stay pending)."""
         keep = []
-        for kind, dt, (e0, e1) in self._pending_ev:
+        for kind, dt, (e0, e1), rec in self._pending_ev:
             if not e1.query():
-                keep.append((kind, dt, (e0, e1)))
+                keep.append((kind, dt, (e0, e1), rec))
                 continue
             self.stats[kind + "_issue_s"] += dt
             self.stats[kind + "_gpu_s"] += e0.elapsed_time(e1) / 1e3
+            if rec is not None:
+                base, tb = self._trace_base
+                rec["g0"] = round(base.elapsed_time(e0), 4)   # ms on the GPU clock since the first traced forward
+                rec["g1"] = round(base.elapsed_time(e1), 4)
+                ek = rec.pop("_ek")
+                rec["gk"] = round(base.elapsed_time(ek), 4) if ek is not None else None  # upload landed
+                for k in ("t_enq0", "t_enq1", "t_wait", "t_step"):
+                    rec[k] = None if rec[k] is None else round((rec[k] - tb) * 1e3, 4)  # ms, host clock
+                self._trace_buf.append(json.dumps(rec))
         self._pending_ev = keep
+        if len(self._trace_buf) >= 256:
+            self.flush_trace()
+
+    def flush_trace(self) -> None:
+        if self._trace is not None and self._trace_buf:
+            with open(self._trace, "a") as f:
+                f.write("\n".join(self._trace_buf) + "\n")
+            self._trace_buf = []
 
     def _to_dev(self, arrays: List[np.ndarray]) -> List[torch.Tensor]:
         """One H2D copy for all int32 metadata arrays."""
@@ -291,7 +318,17 @@ class StepExecMixin:
             spec = (src, spec[1])
         else:
             dev = self._to_dev([flat])[0]
+        self._trace_mark()
         return self._exec_step(header, flat, dev, spec)
+
+    def _trace_mark(self) -> None:
+        """knob step_trace: a timing event right after the step's upload is
+        enqueued (its GPU time minus the forward's start = the GPU waiting for
+        the host's packing + upload)."""
+        if self._trace is not None and self.device.type == "cuda":
+            e = torch.cuda.Event(enable_timing=True)
+            e.record()
+            self._trace_evk = e
 
     @staticmethod
     def _apply_spec(ids: torch.Tensor, src: torch.Tensor, tok: torch.Tensor) -> None:

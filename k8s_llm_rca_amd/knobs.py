@@ -126,6 +126,8 @@ class Knobs:
     shape_trace: Optional[str] = _f(None, "append every step's attention shapes to this JSONL file",
                                     legacy="K8S_RCA_SHAPE_TRACE")
     step_timing: bool = _f(False, "per-path host-issue vs GPU time of every forward", legacy="K8S_RCA_STEP_TIMING")
+    step_trace: Optional[str] = _f(None, "JSONL of every forward: GPU start / end (timing events) and the host's "
+                                         "enqueue time against its last token wait (step-boundary idle analysis)")
     switch_interval: Optional[float] = _f(None, "sys.setswitchinterval for the serving process (s)",
                                           legacy="K8S_RCA_SWITCH_INTERVAL")
     profile_engine: Optional[str] = _f(None, "cProfile of the engine thread dumped to this path",

@@ -95,6 +95,9 @@ class Knobs:
     # ---------------------------------------------------------------- native layer executor / TP
     layer_exec: bool = _f(True, "whole dense layer stack issued by one C call (ops/layer_exec.py)",
                    at_import="ops.layer_exec._enabled (ops.layer_exec.set_enabled)")
+    nano_batch: bool = _f(False, "mixed steps as two layer stacks on two streams: decode rows (high-priority "
+                                 "side stream) beside prefill rows (compute stream)",
+                          at_import="ops.layer_exec._nano")
     norm_fuse: bool = _f(True, "steps of <= 4 rows: the RMSNorms ride in the qkv / gate_up GEMMs' prologues "
                                "(csrc/kernels/norm_prologue.h)",
                    at_import="ops.layer_exec._norm_fuse")

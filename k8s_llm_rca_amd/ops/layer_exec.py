@@ -72,6 +72,13 @@ NORM_FUSE_MAX_T = 4
 # all-reduce on a side stream, and the prefill attention on a side stream beside
 # the decode attention: both measured as losses -- profiles/r3/ab/tp_overlap_*,
 # profiles/r3/overlap/ -- and were retired from the executor in round 4.)
+# Mixed steps as two nano-batch layer stacks on two streams (decode rows beside
+# prefill rows, ops/layer_exec.py LlamaExecutor._run_nano); off by default: see
+# README "Round 6" for the measurement
+_nano = KNOBS.nano_batch
+NANO_MIN_DECODE = 32
+NANO_MIN_PREFILL = 512
+_nano_serial = False  # test hook: the two stacks one after the other on the compute stream
 _checked = False
 
 
@@ -128,6 +135,10 @@ class LlamaExecutor:
         st.ar_mode = 1
         st.ar_fuse = 0
         st.ar_push = 0
+        self._side = None       # nano-batch side stream (created on first use)
+        self._st_side = None
+        self._side_part = None  # its split-K scratch
+        self.nano_steps = 0
 
     @staticmethod
     def eligible(model) -> bool:
@@ -157,19 +168,59 @@ class LlamaExecutor:
 
     def run(self, inp, residual: torch.Tensor, k_cache: torch.Tensor, v_cache: torch.Tensor) -> List[torch.Tensor]:
         """All layers; returns ``(prev, residual)`` for the final norm."""
-        m, st = self.m, self.st
         self._bind_kv(k_cache, v_cache)
-        T, H = residual.shape
+        T = residual.shape[0]
+        if self._nano_ok(inp, T):
+            return self._run_nano(inp, residual, serial=_nano_serial)
+        prev = scratch(tuple(residual.shape), residual.dtype, residual.device)
+        return self._issue(self.st, inp, residual, prev, 0, T, inp.n_decode, stream_ptr(residual))
+
+    # ------------------------------------------------------------ one layer stack
+    def _issue(self, st: LlamaStep, inp, residual: torch.Tensor, prev: torch.Tensor, row0: int, T: int, nd: int,
+               stream: int, side: bool = False, dry: bool = False):
+        """Fill ``st`` for rows [row0, row0 + T) of the step (``nd`` decode rows
+        first) and issue the layer stack on ``stream``.  ``residual`` / ``prev``
+        are those rows' [T, H] buffers.  ``side``: the nano-batch side stack
+        (its own split-K scratch; it must not need hipBLASLt or the grouped
+        kernel, whose workspaces are single).  ``dry``: only the GEMM choices
+        (returns the selection list, issues nothing)."""
+        m = self.m
+        H = residual.shape[1]
         dev, dt = residual.device, residual.dtype
         ld_qkv = (m.nq + 2 * m.nkv) * m.D
+        H_, I_ = m.cfg.hidden, m.inter
+        shapes = ((ld_qkv, H_), (H_, m.nq * m.D), (2 * I_, H_), (H_, I_))
+        sels = []
+        need_mid = need_grp = 0
+        for i, (N, K) in enumerate(shapes):
+            fused = LIN.swiglu_choice(T, N, K) if i == 2 else None  # the SwiGLU-epilogue gate_up (writes act)
+            # otherwise the choice LIN.linear makes (models/llama.py's path)
+            kind, cfg, splits = fused or LIN.select_gemm(T, N, K)
+            if _tp_push_force and self._car is not None and i in (1, 3):
+                fs = 1 if i == 1 else 2
+                if LIN.stream_shape_ok(T, N, K, 13, fs):
+                    kind, cfg, splits = LIN.KIND_STREAM, 13, fs
+            fuse = 2 if fused else int(_fuse_splitk)
+            if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):
+                fuse = 3  # RoPE + KV write in the qkv GEMM's epilogue
+            elif i == 0 and N == (m.nq + 2 * m.nkv) * m.D and LIN.rope_choice(T, N, K):
+                kind, cfg, splits, fuse = LIN.KIND_BIG, LIN.BIG_PIPE, 1, 4  # gemm_big's RoPE + KV-write epilogue
+            sels.append((kind, cfg, splits, fuse))
+            if kind in (LIN.KIND_MID, LIN.KIND_STREAM, LIN.KIND_BIG) and splits > 1:
+                need_mid = max(need_mid, splits * T * N)
+            elif kind == LIN.KIND_GRP:
+                need_grp = max(need_grp, splits * T * N if splits > 1 else 1)
+        if dry:
+            return sels
+        for i, (kind, cfg, splits, fuse) in enumerate(sels):
+            st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits, st.sel[i].fuse = kind, cfg, splits, fuse
         y = scratch((T, H), dt, dev)
         qkv = scratch((T, ld_qkv), dt, dev)
         attn = scratch((T, m.nq * m.D), dt, dev)
         obuf = scratch((T, H), dt, dev)
         gu = scratch((T, 2 * m.inter), dt, dev)
         act = scratch((T, m.inter), dt, dev)
-        prev = scratch((T, H), dt, dev)
-        st.T, st.nd = T, inp.n_decode
+        st.T, st.nd = T, nd
         st.nf_flags = ptr(m.nf_flags)
         if self._car is not None:
             from ..parallel.xgmi import ONE_SHOT_MAX
@@ -181,8 +232,9 @@ class LlamaExecutor:
             st.ar_push = int(bool(st.ar_fuse) and (_tp_push or push) and self._car.push_ok(H, T, st.ar_mode))
         st.residual, st.y, st.qkv, st.attn = residual.data_ptr(), y.data_ptr(), qkv.data_ptr(), attn.data_ptr()
         st.obuf, st.gu, st.act, st.prev = obuf.data_ptr(), gu.data_ptr(), act.data_ptr(), prev.data_ptr()
-        st.pos, st.slots = inp.positions.data_ptr(), ptr(inp.slots)
-        md = inp.meta_decode if inp.n_decode > 0 else None
+        st.pos = inp.positions.data_ptr() + 4 * row0          # int32 rows
+        st.slots = ptr(inp.slots) + 4 * row0 if inp.slots is not None else None
+        md = inp.meta_decode if nd > 0 else None
         if md is not None:
             st.d_bt, st.d_ctx, st.d_qs = md.block_tables.data_ptr(), md.ctx_lens.data_ptr(), md.q_start.data_ptr()
             st.d_part_o, st.d_part_ml = ptr(md.part_o), ptr(md.part_ml)
@@ -192,7 +244,7 @@ class LlamaExecutor:
             st.d_grid = md.grid_waves or min(A.DECODE_WAVE_SLOTS, md.n_items * m.nkv)
         else:
             st.d_bt = None
-        mp = inp.meta_prefill if inp.n_decode < T else None
+        mp = inp.meta_prefill if nd < T else None
         if mp is not None:
             if mp.n_merge and mp.pf_o is None:
                 mp.pf_o, mp.pf_ml = A.prefill_workspace(m.nkv, dev, max(mp.m_slot0_end(), 1))
@@ -206,33 +258,15 @@ class LlamaExecutor:
                 mp.n_merge
         else:
             st.p_bt = None
-        H_, I_ = m.cfg.hidden, m.inter
-        shapes = ((ld_qkv, H_), (H_, m.nq * m.D), (2 * I_, H_), (H_, I_))
-        need_mid = need_grp = 0
-        for i, (N, K) in enumerate(shapes):
-            fused = LIN.swiglu_choice(T, N, K) if i == 2 else None  # the SwiGLU-epilogue gate_up (writes act)
-            # otherwise the choice LIN.linear makes (models/llama.py's path)
-            kind, cfg, splits = fused or LIN.select_gemm(T, N, K)
-            if _tp_push_force and self._car is not None and i in (1, 3):
-                fs = 1 if i == 1 else 2
-                if LIN.stream_shape_ok(T, N, K, 13, fs):
-                    kind, cfg, splits = LIN.KIND_STREAM, 13, fs
-            st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = kind, cfg, splits
-            st.sel[i].fuse = 2 if fused else int(_fuse_splitk)
-            if i == 0 and kind == LIN.KIND_SKINNY and A.skinny_rope_ok(T, N, K, m.nq, m.nkv):
-                st.sel[i].fuse = 3  # RoPE + KV write in the qkv GEMM's epilogue
-            elif i == 0 and N == (m.nq + 2 * m.nkv) * m.D and LIN.rope_choice(T, N, K):
-                st.sel[i].kind, st.sel[i].cfg, st.sel[i].splits = LIN.KIND_BIG, LIN.BIG_PIPE, 1
-                st.sel[i].fuse = 4  # gemm_big's RoPE + KV-write epilogue
-            if kind in (LIN.KIND_MID, LIN.KIND_STREAM, LIN.KIND_BIG) and splits > 1:
-                need_mid = max(need_mid, splits * T * N)
-            elif kind == LIN.KIND_GRP:
-                need_grp = max(need_grp, splits * T * N if splits > 1 else 1)
         LIN.reserve_lib_workspace(dev)
         ws = LIN._blaslt_ws[dev]
         st.blaslt_ws, st.blaslt_ws_bytes = ws.data_ptr(), LIN.BLASLT_WS_BYTES
-        # the same split-K buffers the Python path grows (reserved before any capture)
-        st.mid_part = LIN._scratch(dev, need_mid).data_ptr() if need_mid else None
+        # the same split-K buffers the Python path grows (reserved before any capture);
+        # the nano-batch side stack has its own (both stacks' partials are live at once)
+        if side:
+            st.mid_part = self._side_scratch(dev, need_mid).data_ptr() if need_mid else None
+        else:
+            st.mid_part = LIN._scratch(dev, need_mid).data_ptr() if need_mid else None
         if need_grp:
             from . import moe as MO
             st.grp_part = MO._split_scratch(dev, need_grp).data_ptr()
@@ -247,10 +281,68 @@ class LlamaExecutor:
         st.norm_fuse = nf
         res2 = scratch((T, H), dt, dev) if nf else None
         st.res2 = ptr(res2)
-        check(lib().k8s_llama_layers(ctypes.byref(st), stream_ptr(residual)), "llama_layers")
+        check(lib().k8s_llama_layers(ctypes.byref(st), stream), "llama_layers")
         # every fused add-norm moves the residual to the other buffer
         swaps = (st.L - 1) * (nf & 1) + st.L * ((nf >> 1) & 1)
         return prev, (res2 if swaps % 2 else residual)
+
+    # ------------------------------------------------------------ nano-batches
+    def _side_scratch(self, dev, n: int) -> torch.Tensor:
+        t = self._side_part
+        if t is None or t.numel() < n:
+            t = self._side_part = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+        return t
+
+    def _nano_ok(self, inp, T: int) -> bool:
+        """Split this mixed step into a decode-row stack and a prefill-row stack
+        on two streams (knob ``nano_batch``; TP = 1, no debug flags): the
+        memory-bound decode attention and weight-streaming decode GEMMs run
+        beside the compute-bound prefill GEMMs.  The decode stack must need
+        neither hipBLASLt nor the grouped kernel (single workspaces)."""
+        nd = inp.n_decode
+        if not (_nano and self._car is None and self.m.nf_flags is None and inp.meta_decode is not None
+                and inp.meta_prefill is not None and nd >= NANO_MIN_DECODE and T - nd >= NANO_MIN_PREFILL):
+            return False
+        res = torch.empty(0, dtype=self.m.dtype, device=self.m.device)
+        sels = self._issue(self.st, inp, res.new_empty((nd, self.m.cfg.hidden)), res, 0, nd, nd, 0, dry=True)
+        return all(k not in (LIN.KIND_LIB, LIN.KIND_GRP) for k, *_ in sels)
+
+    def _run_nano(self, inp, residual: torch.Tensor, serial: bool = False):
+        """Decode rows [0, nd) on a high-priority side stream, prefill rows
+        [nd, T) on the compute stream, each as its own layer stack (same
+        kernels as a step of only those rows); joined before the final norm.
+        The two stacks share only read-only weights and disjoint KV slots.
+        ``serial``: both stacks on the compute stream, one after the other
+        (the reference order of the bit-identity test)."""
+        T, H = residual.shape
+        nd = inp.n_decode
+        dev = residual.device
+        main = torch.cuda.current_stream(dev)
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev, priority=-1)
+            self._st_side = LlamaStep()
+            ctypes.pointer(self._st_side)[0] = self.st  # weight / KV tables, model constants
+        side = self._side
+        sd = self._st_side
+        sd.kc, sd.vc, sd.BS = self.st.kc, self.st.vc, self.st.BS
+        prev = scratch((T, H), residual.dtype, dev)
+        fork = torch.cuda.Event()
+        fork.record(main)
+        side.wait_stream(main)
+        # prefill stack first on the compute stream (it owns gemm_big's split tail)
+        _, res_p = self._issue(self.st, inp, residual[nd:], prev[nd:], nd, T - nd, 0, main.cuda_stream)
+        if serial:
+            _, res_d = self._issue(sd, inp, residual[:nd], prev[:nd], 0, nd, nd, main.cuda_stream, side=True)
+        else:
+            with torch.cuda.stream(side):
+                _, res_d = self._issue(sd, inp, residual[:nd], prev[:nd], 0, nd, nd, side.cuda_stream, side=True)
+            residual.record_stream(side)
+            prev.record_stream(side)
+            main.wait_stream(side)
+        self.nano_steps += 1
+        # the fused-norm ping-pong needs T <= 4: never at these sizes, the stacks return their own rows
+        assert res_p.data_ptr() == residual[nd:].data_ptr() and res_d.data_ptr() == residual.data_ptr()
+        return prev, residual
 
 
 def _silu_fused_in_table(model) -> bool:

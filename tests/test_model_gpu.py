@@ -315,3 +315,91 @@ def test_layer_executor_norm_fuse_bit_identical(nl, deferred):
                 LIN._dispatch.pop(k, None)
             else:
                 LIN._dispatch[k] = v
+
+
+def _mixed_step_8b(m, nd=40, npf=640, cached=128, seed=0):
+    """A mixed step on Llama-3-8B shapes: ``nd`` decode rows (300-800 cached keys
+    each, scattered pages of random K/V) + one ``npf``-token prefill chunk after
+    ``cached`` keys.  Returns (StepInputs, k_cache, v_cache)."""
+    import numpy as np
+    from k8s_llm_rca_amd.models.llama import StepInputs
+    from k8s_llm_rca_amd.ops import attention as A
+    BS, dev = 64, "cuda"
+    g = np.random.default_rng(seed)
+    ctx = [int(c) for c in g.integers(300, 800, nd)]   # decode row i: key ctx-1 is its new token
+    nbs = [-(-c // BS) for c in ctx] + [-(-(cached + npf) // BS)]
+    perm = g.permutation(sum(nbs))
+    bts, u = [], 0
+    for n in nbs:
+        bts.append(perm[u:u + n].tolist())
+        u += n
+    L = m.cfg.n_layers
+    kc = (torch.randn(L, sum(nbs), m.nkv, BS, m.D, generator=torch.Generator().manual_seed(seed)) * 0.5).bfloat16().to(dev)
+    vc = torch.randn(L, sum(nbs), m.nkv, m.D, BS, generator=torch.Generator().manual_seed(seed + 1)).bfloat16().to(dev)
+    mb = max(nbs[:nd])
+    bt_d = torch.zeros(nd, mb, dtype=torch.int32)
+    for i in range(nd):
+        bt_d[i, :nbs[i]] = torch.tensor(bts[i], dtype=torch.int32)
+    md = A.AttnMeta(block_tables=bt_d.to(dev), ctx_lens=torch.tensor(ctx, dtype=torch.int32, device=dev),
+                    q_start=torch.arange(nd + 1, dtype=torch.int32, device=dev), num_seqs=nd, decode=True,
+                    ctx_lens_host=ctx, q_start_host=list(range(nd + 1)))
+    A.attach_decode_plan(md, ctx, m.nq, m.nkv, BS, dev)
+    tot = cached + npf
+    mp_ = A.AttnMeta(block_tables=torch.tensor([bts[nd]], dtype=torch.int32, device=dev),
+                     ctx_lens=torch.tensor([tot], dtype=torch.int32, device=dev),
+                     q_start=torch.tensor([0, npf], dtype=torch.int32, device=dev), num_seqs=1, decode=False,
+                     ctx_lens_host=[tot], q_start_host=[0, npf])
+    A.attach_plan(mp_, A.plan_prefill([0, npf], m.nq // m.nkv, BS, [tot], nkv=m.nkv), dev)
+    pos = ctx_pos = [c - 1 for c in ctx] + list(range(cached, tot))
+    slots = [bts[i][p // BS] * BS + p % BS for i, p in enumerate(ctx_pos[:nd])] + \
+        [bts[nd][p // BS] * BS + p % BS for p in range(cached, tot)]
+    T = nd + npf
+    ids = torch.tensor(g.integers(0, 100000, T), dtype=torch.int32, device=dev)
+    inp = StepInputs(ids, torch.tensor(pos, dtype=torch.int32, device=dev),
+                     torch.tensor(slots, dtype=torch.int32, device=dev), nd, md, mp_,
+                     torch.tensor(list(range(nd)) + [T - 1], dtype=torch.int64, device=dev))
+    return inp, kc, vc
+
+
+def test_nano_batch_two_streams_bit_identical_to_serial():
+    """a mixed step as two nano-batch layer stacks (decode rows on
+    a high-priority side stream beside the prefill rows on the compute stream,
+    ops/layer_exec.py ``_run_nano``) gives bit-identically the logits and KV of
+    the same two stacks run one after the other, and agrees with the single
+    combined stack to bf16 tolerance (the stacks pick their GEMM kernels for
+    their own M)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.models.config import get_config
+    from k8s_llm_rca_amd.models.llama import LlamaModel
+    from k8s_llm_rca_amd.ops import layer_exec as LX
+    from k8s_llm_rca_amd.ops import linear as LIN
+    saved = (dict(LIN._dispatch), dict(LIN._big_ranges), LX._nano, LX._nano_serial)
+    try:
+        dev = torch.device("cuda:0")
+        LIN.reserve_lib_workspace(dev)
+        assert LIN.load_dispatch(LIN.dispatch_path("llama3-8b"))
+        LIN.load_big(LIN.big_path("llama3-8b"))
+        LIN.reserve_dispatch_scratch(dev)
+        m = LlamaModel(get_config("llama3-8b", n_layers=2), "cuda:0", torch.bfloat16, None, seed=2)
+        outs = {}
+        for mode in ("single", "serial", "streams"):
+            LX._nano, LX._nano_serial = mode != "single", mode == "serial"
+            inp, kc, vc = _mixed_step_8b(m)
+            n0 = m._exec.nano_steps if m._exec is not None else 0
+            logits = m.forward(inp, kc, vc).float()
+            torch.cuda.synchronize()
+            assert m._exec.nano_steps == n0 + (mode != "single"), mode
+            outs[mode] = (logits.cpu(), kc.float().cpu(), vc.float().cpu())
+        a, b, c = outs["streams"], outs["serial"], outs["single"]
+        assert all(torch.equal(x, y) for x, y in zip(a, b))
+        assert torch.isfinite(a[0]).all()
+        rel = ((a[0] - c[0]).norm() / c[0].norm()).item()
+        assert rel < 0.02, rel
+        assert (a[0].argmax(-1) == c[0].argmax(-1)).float().mean().item() >= 0.9
+    finally:
+        LIN._dispatch.clear()
+        LIN._dispatch.update(saved[0])
+        LIN._big_ranges.clear()
+        LIN._big_ranges.update(saved[1])
+        LX._nano, LX._nano_serial = saved[2], saved[3]

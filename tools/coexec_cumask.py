@@ -136,8 +136,27 @@ def main():
             for i in range(a.reps):
                 LIN.gemm_big(x, ws[i % 2], y, silu=True)
 
+        # the GEMM split into a part sized to run on the 8 CUs/XCD the attention leaves idle
+        # (m = 3) while it streams, and the rest on the whole chip after it
+        n1 = 34 * 128  # act columns of part 1 (~30 % of 14336)
+        w1 = [((torch.rand(2 * n1, K, device=dev) * 2 - 1) * 0.02).bfloat16() for _ in range(2)]
+        w2 = [((torch.rand(N2 - 2 * n1, K, device=dev) * 2 - 1) * 0.02).bfloat16() for _ in range(2)]
+        y1 = torch.empty(M, n1, device=dev).bfloat16()
+        y2 = torch.empty(M, N2 // 2 - n1, device=dev).bfloat16()
+
+        def gemm1(x=x, y1=y1):
+            for i in range(a.reps):
+                LIN.gemm_big(x, w1[i % 2], y1, silu=True)
+
+        def gemm2(x=x, y2=y2):
+            for i in range(a.reps):
+                LIN.gemm_big(x, w2[i % 2], y2, silu=True)
+
+        hi = torch.cuda.Stream(priority=-1)
         arms = {"attn_full": on(full, lambda: attn(full_grid)), "gemm_full": on(full, gemm),
-                "both_unmasked": both(full, lambda: attn(full_grid), torch.cuda.Stream(), gemm)}
+                "both_unmasked": both(full, lambda: attn(full_grid), torch.cuda.Stream(), gemm),
+                # the attention on a high-priority stream: its waves are dispatched first as GEMM tiles retire
+                "both_attn_high_prio": both(hi, lambda: attn(full_grid), torch.cuda.Stream(), gemm)}
         for m in [int(v) for v in a.splits.split(",")]:
             sa = masked_stream(L, mask_words(n_cu, lambda i, m=m: (i // 8) % 4 < m), dev)
             sg = masked_stream(L, mask_words(n_cu, lambda i, m=m: (i // 8) % 4 >= m), dev)
@@ -148,6 +167,21 @@ def main():
             arms[f"gemm_m{m}"] = on(sg, gemm)
             arms[f"both_m{m}"] = both(sa, lambda grid=grid: attn(grid), sg, gemm)
             arms[f"both_m{m}_gall"] = both(sa, lambda grid=grid: attn(grid), full, gemm)
+            if m == 3:
+                def split_run(sa=sa, sg=sg, grid=grid):
+                    cur = torch.cuda.current_stream()
+                    ev = torch.cuda.Event()
+                    ev.record(cur)
+                    sa.wait_event(ev)
+                    sg.wait_event(ev)
+                    with torch.cuda.stream(sa):
+                        attn(grid)
+                    with torch.cuda.stream(sg):
+                        gemm1()
+                    cur.wait_stream(sa)
+                    cur.wait_stream(sg)
+                    gemm2()
+                arms["split_m3_then_full"] = split_run
         for fn in arms.values():
             fn()
         torch.cuda.synchronize()
@@ -162,9 +196,15 @@ def main():
                "attn_full_TBps": kv_bytes / med["attn_full"] / 1e6, "gemm_full_TFs": flop / med["gemm_full"] / 1e6}
         print(f"M={M}: attention alone {med['attn_full']:.1f} us ({row['attn_full_TBps']:.2f} TB/s), "
               f"gate_up gemm_big alone {med['gemm_full']:.1f} us ({row['gemm_full_TFs']:.0f} TFLOP/s), "
-              f"serial {serial:.1f} us, both unmasked {med['both_unmasked']:.1f} us", flush=True)
+              f"serial {serial:.1f} us, both unmasked {med['both_unmasked']:.1f} us, attention on a high-priority "
+              f"stream {med['both_attn_high_prio']:.1f} us ({100 * (1 - med['both_attn_high_prio'] / serial):+.1f} %)",
+              flush=True)
         for m in [int(v) for v in a.splits.split(",")]:
             bo, bg = med[f"both_m{m}"], med[f"both_m{m}_gall"]
+            if m == 3:
+                sp = med["split_m3_then_full"]
+                print(f"  attention on 24 CUs/XCD + 30 % of the GEMM on the other 8, then the rest on all: {sp:.1f} us "
+                      f"({100 * (1 - sp / serial):+.1f} % vs serial)", flush=True)
             print(f"  attention on {8 * m} CUs/XCD: attn {med[f'attn_m{m}']:.1f} us "
                   f"({kv_bytes / med[f'attn_m{m}'] / 1e6:.2f} TB/s), gemm on the rest {med[f'gemm_m{m}']:.1f} us; "
                   f"both {bo:.1f} us ({100 * (1 - bo / serial):+.1f} % vs serial), "

@@ -38,7 +38,9 @@ def meta_for(ctx, contiguous, dev, part=None):
 def main():
     dev = torch.device("cuda")
     g = torch.Generator().manual_seed(0)
-    ctx = (torch.randint(3000, 6400, (125,), generator=g)).tolist()
+    rows = int(os.environ.get("PROBE_ROWS", "125"))
+    lo, hi = int(os.environ.get("PROBE_CTX_LO", "3000")), int(os.environ.get("PROBE_CTX_HI", "6400"))
+    ctx = (torch.randint(lo, hi, (rows,), generator=g)).tolist()
     parts = [None] + [int(v) for v in os.environ.get("PROBE_PARTS", "").split(",") if v]
     for contiguous, part in [(False, None), (True, None)] + [(False, p) for p in parts[1:]]:
         meta, nb = meta_for(ctx, contiguous, dev, part)

@@ -357,3 +357,21 @@ K8S_API int k8s_nonfinite_flag(const void* x, long n, int* flag, hipStream_t s) 
   hipLaunchKernelGGL(nonfinite_flag_kernel, dim3((unsigned)blocks), dim3(256), 0, s, (const uint16_t*)x, n, flag);
   return (int)hipGetLastError();
 }
+
+// Host-visible completion flag (knob token_flag): stream-ordered after the
+// sampled tokens' device -> host copy, every lane of one wave stores `value`
+// into its own int of `flag` (pinned host memory; plain per-lane VECTOR
+// stores, no scalar-cache write), and the engine polls flag[0] with short
+// sleeps instead of waiting in hipEventSynchronize (engine/sampler.py).  The
+// copy has completed before this kernel starts (stream order), so a host that
+// reads flag[0] >= value also reads the step's tokens.
+__global__ void __launch_bounds__(64) host_flag_kernel(int* __restrict__ flag, int value) {
+  // a system-scope release store per lane: write-through to host memory (sc0 sc1)
+  __hip_atomic_store(flag + threadIdx.x, value, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+K8S_API int k8s_host_flag(int* flag, int value, hipStream_t s) {
+  if (!flag) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(host_flag_kernel, dim3(1), dim3(64), 0, s, flag, value);
+  return (int)hipGetLastError();
+}

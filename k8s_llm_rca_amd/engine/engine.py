@@ -168,6 +168,10 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         self._trace_base = None
         self._trace_buf: list = []
         self._last_wait_end = None
+        # knob token_flag: pinned host flag raised after each step's token copy (engine/sampler.py)
+        self._tflag = None
+        self._tflag_np = None
+        self._tflag_seq = 0
         # debug (knob nonfinite_check): per-layer non-finite flags, read with each sampling
         self._nf = None
         if KNOBS.nonfinite_check and self.device.type == "cuda" and hasattr(self.model, "nf_flags"):

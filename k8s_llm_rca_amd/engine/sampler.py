@@ -28,6 +28,8 @@ from .kv_cache import chain_key
 from .structured import GrammarState
 from .types import PART_MIN, SPEC, InFlight, Request, Sequence, _LazySample, _spec_tok
 
+# knob token_flag: the host's poll period while the GPU finishes a step
+TOKEN_FLAG_SLEEP_S = 50e-6
 log = logging.getLogger("k8s_llm_rca_amd.engine.engine")
 
 
@@ -248,15 +250,39 @@ class SamplerMixin:
             nf = torch.empty(self._nf.numel(), dtype=torch.int32, pin_memory=True)
             nf.copy_(self._nf, non_blocking=True)
             self._nf.zero_()
+        seq = 0
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)
+            if KNOBS.token_flag and self.pc.tp_size == 1:
+                # stream-ordered after the copy: a one-wave kernel raises the pinned flag
+                from ..ops._lib import check, lib, stream_ptr
+                if self._tflag is None:
+                    self._tflag = torch.zeros(64, dtype=torch.int32, pin_memory=True)
+                    self._tflag_np = self._tflag.numpy()
+                self._tflag_seq += 1
+                seq = self._tflag_seq
+                check(lib().k8s_host_flag(self._tflag.data_ptr(), seq, stream_ptr(tok)), "host_flag")
             ev = torch.cuda.Event(blocking=KNOBS.blocking_sync)
             ev.record()
         else:
             host, ev = tok, None
         self.stats["sample_s"] += time.perf_counter() - t0
-        return InFlight(seqs, tok, host, ev, t0, status, nf)
+        return InFlight(seqs, tok, host, ev, t0, status, nf, seq)
+
+    def _wait_flag(self, fl: InFlight) -> None:
+        """Sleep-poll the pinned host flag until the step's tokens have landed
+        (knob token_flag): the engine thread leaves the CPU and the GIL to the
+        pipelines instead of spinning in hipEventSynchronize.  The event is
+        recorded after the flag kernel, so a completed event with the flag
+        still unseen falls back to it (never a hang)."""
+        f = self._tflag_np
+        t = time.perf_counter()
+        while int(f[0]) < fl.flag_seq:
+            time.sleep(TOKEN_FLAG_SLEEP_S)
+            if time.perf_counter() - t > 1.0 and fl.event.query():
+                fl.event.synchronize()
+                return
 
     def _process_tokens(self, fl: InFlight, placeholders: bool = False) -> List[int]:
         """Host side of a sampled step: wait for its tokens (not for later GPU
@@ -264,7 +290,9 @@ class SamplerMixin:
         ``placeholders``: the sequences carry a SPEC token that the sampled
         token replaces."""
         t1 = time.perf_counter()
-        if fl.event is not None:
+        if fl.flag_seq:
+            self._wait_flag(fl)
+        elif fl.event is not None:
             fl.event.synchronize()
         self._last_wait_end = time.perf_counter()
         if fl.status is not None and int(fl.status[0]) != 0:

@@ -40,9 +40,9 @@ class _LazySample:
 
 class InFlight:
     """A sampled step whose tokens have not been processed on the host yet."""
-    __slots__ = ("seqs", "tok", "tok_host", "event", "t0", "status", "nf")
+    __slots__ = ("seqs", "tok", "tok_host", "event", "t0", "status", "nf", "flag_seq")
 
-    def __init__(self, seqs, tok, tok_host, event, t0, status=None, nf=None):
+    def __init__(self, seqs, tok, tok_host, event, t0, status=None, nf=None, flag_seq=0):
         self.seqs = seqs
         self.tok = tok            # [B] int32 on the device (feeds the next forward)
         self.tok_host = tok_host  # [B] int32 host copy (pinned on GPU), valid once `event` completes
@@ -50,6 +50,7 @@ class InFlight:
         self.t0 = t0
         self.status = status      # TP: pinned copy of the xGMI STATUS word, taken before the sampling
         self.nf = nf              # knob nonfinite_check: pinned copy of the per-layer non-finite flags
+        self.flag_seq = flag_seq  # knob token_flag: the host flag reaches this value once tok_host is valid
 
 
 def _knob(name: str, default):

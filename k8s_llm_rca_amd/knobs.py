@@ -135,6 +135,10 @@ class Knobs:
                                           legacy="K8S_RCA_SWITCH_INTERVAL")
     profile_engine: Optional[str] = _f(None, "cProfile of the engine thread dumped to this path",
                                        legacy="K8S_RCA_PROFILE_ENGINE")
+    token_flag: bool = _f(True, "TP = 1: the engine waits for a step's sampled tokens by polling a pinned-host flag "
+                                "a one-wave kernel sets after their copy (50 us sleeps), not spinning in "
+                                "hipEventSynchronize: engine thread 66 -> 10 CPU-s per contract window, throughput "
+                                "unchanged (profiles/r6/token_flag/)")
     blocking_sync: bool = _f(False, "host waits on the engine's token / staging / graph-mirror events block in the "
                                     "driver (hipEventBlockingSync) instead of spinning")
     nonfinite_check: bool = _f(False, "device-side non-finite flag on every layer's normed input (no host sync)")

@@ -74,6 +74,7 @@ _SIGS = {
     "k8s_graph_expand2": [P, P, P, P, P, P, P, P, I, I, I, I, P, P, P, P, P, P],
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],
     "k8s_window_mark": [I, P],
+    "k8s_host_flag": [P, I, P],
     "k8s_set_knob": [I, I],
     "k8s_nonfinite_flag": [P, ctypes.c_long, P, P],
     "k8s_get_knob": [I],

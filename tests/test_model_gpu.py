@@ -403,3 +403,29 @@ def test_nano_batch_two_streams_bit_identical_to_serial():
         LIN._big_ranges.clear()
         LIN._big_ranges.update(saved[1])
         LX._nano, LX._nano_serial = saved[2], saved[3]
+
+
+def test_token_flag_wait_same_tokens():
+    """Knob token_flag: the engine waits for each step's tokens by
+    polling a pinned-host flag that a one-wave kernel raises after their copy,
+    instead of hipEventSynchronize; the generations are the same as with the
+    event wait, and the flag ran (its sequence advanced)."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd import knobs as K
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    outs = []
+    for on in (False, True):
+        with K.override(token_flag=on):
+            eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=256, temperature=0.0,
+                                         graph_batch_sizes=(1, 2, 4, 8)))
+            res = {}
+            for i in range(5):
+                sid = eng.new_sequence()
+                p = eng.tok.system_prefix("s") + eng.tok.message("user", "flag %d " % i * (10 + 7 * i)) + \
+                    eng.tok.header("assistant")
+                eng.submit(sid, p, None, 16, temperature=0.0, on_done=lambda g, st, i=i: res.__setitem__(i, g))
+            eng.run_until_idle()
+            assert (eng._tflag_seq > 0) == on
+            outs.append(res)
+    assert outs[0] == outs[1] and all(len(v) == 16 for v in outs[0].values())

@@ -28,8 +28,11 @@ from .kv_cache import chain_key
 from .structured import GrammarState
 from .types import PART_MIN, SPEC, InFlight, Request, Sequence, _LazySample, _spec_tok
 
-# knob token_flag: the host's poll period while the GPU finishes a step
+# knob token_flag: the host's poll period while the GPU finishes a step, and the
+# smallest sampled batch that polls (a few-row step is latency-bound: a 50 us poll
+# period would be ~2 % of a concurrency-1 decode token, so it keeps the event wait)
 TOKEN_FLAG_SLEEP_S = 50e-6
+TOKEN_FLAG_MIN_ROWS = 16
 log = logging.getLogger("k8s_llm_rca_amd.engine.engine")
 
 
@@ -254,7 +257,7 @@ class SamplerMixin:
         if tok.is_cuda:
             host = torch.empty(B, dtype=torch.int32, pin_memory=True)
             host.copy_(tok, non_blocking=True)
-            if KNOBS.token_flag and self.pc.tp_size == 1:
+            if KNOBS.token_flag and self.pc.tp_size == 1 and B >= TOKEN_FLAG_MIN_ROWS:
                 # stream-ordered after the copy: a one-wave kernel raises the pinned flag
                 from ..ops._lib import check, lib, stream_ptr
                 if self._tflag is None:

@@ -414,7 +414,10 @@ def test_token_flag_wait_same_tokens():
         pytest.skip("no GPU")
     from k8s_llm_rca_amd import knobs as K
     from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.engine import sampler as SM
     outs = []
+    min_rows = SM.TOKEN_FLAG_MIN_ROWS
+    SM.TOKEN_FLAG_MIN_ROWS = 1  # every step polls (the default keeps the event wait below 16 rows)
     for on in (False, True):
         with K.override(token_flag=on):
             eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", num_blocks=256, temperature=0.0,
@@ -428,4 +431,5 @@ def test_token_flag_wait_same_tokens():
             eng.run_until_idle()
             assert (eng._tflag_seq > 0) == on
             outs.append(res)
+    SM.TOKEN_FLAG_MIN_ROWS = min_rows
     assert outs[0] == outs[1] and all(len(v) == 16 for v in outs[0].values())

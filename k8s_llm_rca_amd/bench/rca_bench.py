@@ -285,6 +285,7 @@ def run(args) -> Optional[Dict[str, Any]]:
                                  dtype=torch.bfloat16 if cuda else torch.float32,
                                  kv_max_gb=args.kv_gb, max_batch_tokens=args.max_batch_tokens,
                                  max_context=args.max_context,
+                                 **({"kv_host_gb": args.kv_host_gb} if args.kv_host_gb is not None else {}),
                                  use_graphs=cuda and not args.no_graphs, prefix_sharing=not args.no_prefix_sharing,
                                  seed=args.seed + (0 if tp_mode else rank),
                                  num_blocks=None if cuda else 512), pc)
@@ -532,6 +533,9 @@ def run(args) -> Optional[Dict[str, Any]]:
                    "blaslt_buckets": int(getattr(eng, "lib_algos", 0) or 0),
                    # gemm_big launches that ran without the split tail (a stream other than the engine's)
                    "big_tail_foreign": _tail_foreign(eng),
+                   # KV host tier (--kv-host-gb): idle threads swapped out / back in the window
+                   **({"swap_outs": d.get("swap_outs", 0), "swap_ins": d.get("swap_ins", 0),
+                       "kv_host": eng.kv_host.report()} if getattr(eng, "kv_host", None) is not None else {}),
                    # K8SRCA_STEP_TIMING=1: host issue time vs GPU time of the forwards
                    **({k: round(d[k], 3) for k in ("eager_issue_s", "eager_gpu_s", "graph_issue_s", "graph_gpu_s")}
                       if d["eager_gpu_s"] or d["graph_gpu_s"] else {})},
@@ -612,6 +616,9 @@ def parser() -> argparse.ArgumentParser:
                    help="keep the graphs on the host (default on GPU: HBM mirror + batched HIP graph kernels)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--kv-gb", type=float, default=None, help="KV pool cap (default: 85%% of free HBM)")
+    p.add_argument("--kv-host-gb", type=float, default=None,
+                   help="KV host tier: GB of page-locked host memory idle threads are swapped to instead of "
+                        "dropped (engine/kv_offload.py; TP = 1)")
     p.add_argument("--max-context", type=int, default=None,
                    help="serving window (tokens) a thread is cut at (default: the model's own window); "
                         "reported in config.truncation")

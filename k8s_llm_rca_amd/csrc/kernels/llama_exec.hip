@@ -21,6 +21,8 @@
 #include <cstddef>
 #include <cstdlib>
 
+#include <cstdio>
+
 #include "common.h"
 
 // the kernels' C entry points (other translation units of this library)
@@ -218,10 +220,15 @@ bool push_kind(const K8sGemmSel& g) { return g.kind == 4 && (g.cfg >= 13 || g.sp
 
 }  // namespace
 
-#define K8S_TRY(call)          \
-  do {                         \
-    const int rc_ = (call);    \
-    if (rc_) return rc_;       \
+// a failing op names itself (the step's rc alone does not say which of ~10 per layer it was)
+#define K8S_TRY(call)                                                                                     \
+  do {                                                                                                    \
+    const int rc_ = (call);                                                                               \
+    if (rc_) {                                                                                            \
+      fprintf(stderr, "k8s_llama_layers: llama_exec.hip:%d failed with %d (T=%d nd=%d sel kinds %d %d %d %d)\n", \
+              __LINE__, rc_, s.T, s.nd, s.sel[0].kind, s.sel[1].kind, s.sel[2].kind, s.sel[3].kind);      \
+      return rc_;                                                                                         \
+    }                                                                                                     \
   } while (0)
 
 // Layers [0, L): on return `y` holds nothing useful and `prev` + `residual`

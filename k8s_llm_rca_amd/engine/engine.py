@@ -120,6 +120,19 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
                 budget = min(budget, cfg.kv_max_gb * (1 << 30))
             nb = max(16, int(budget // per))
         self.kv = KVPool(self.mc.n_layers, nkv, D, nb, BS, self.device, cfg.dtype)
+        # KV host tier: idle threads are swapped to page-locked host memory instead
+        # of dropped (engine/kv_offload.py).  One engine per device: at TP > 1 the
+        # ranks' pools would have to swap in lockstep, which the channel does not carry
+        self.kv_host = None
+        if cfg.kv_host_gb and cfg.kv_host_gb > 0:
+            if self.pc.tp_size > 1:
+                log.warning("kv_host_gb ignored at TP = %d (host tier is per-device, TP = 1 only)", self.pc.tp_size)
+            else:
+                from .kv_offload import KVHostTier
+                per = KVPool.bytes_per_block(self.mc.n_layers, nkv, D, BS, self.kv.k.element_size())
+                self.kv_host = KVHostTier(self.kv, max(1, int(cfg.kv_host_gb * (1 << 30) // per)))
+        self.kv_watermark = (cfg.kv_host_watermark if cfg.kv_host_watermark is not None
+                             else min(nb // 4, (cfg.max_batch_tokens + self.max_context) // BS + 2))
         self.max_blocks_per_seq = (self.max_context + BS - 1) // BS + 1
         self.seqs: Dict[int, Sequence] = {}
         self._next_sid = 0
@@ -189,7 +202,7 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
                       "end_grammar": 0, "end_eos": 0, "end_no_allowed": 0, "end_cap": 0,
                       "timeouts": 0,
                       "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
-                      "tiny_chunk_tokens": 0}
+                      "tiny_chunk_tokens": 0, "swap_outs": 0, "swap_ins": 0}
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
         self._fault: Optional[str] = None  # a dead communicator: every later request fails at admission
@@ -317,6 +330,8 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
         if self._thread is not None:
             self._thread.join()
             self._thread = None
+        if self.kv_host is not None:
+            self.kv_host.drain()
         if self._trace is not None:
             if self.device.type == "cuda":
                 torch.cuda.synchronize(self.device)
@@ -364,10 +379,7 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
             r = s.req
             if r is not None:
                 s.req = None
-                s.n_cached = 0
-                self.kv.release(s.blocks)
-                s.blocks = []
-                s.bh = []
+                self._drop_kv(s)
                 if r.on_done:
                     r.on_done(None, {"error": err})
 

@@ -45,9 +45,7 @@ class SchedulerMixin:
                     continue
                 s = self.seqs.pop(sid, None)
                 if s is not None:
-                    self.kv.release(s.blocks)
-                    s.blocks = []
-                    s.bh = []
+                    self._drop_kv(s, gone=True)
             self._releases = keep + self._releases
 
     def _apply_cancels(self, in_flight: set) -> None:
@@ -102,13 +100,16 @@ class SchedulerMixin:
             BS = self.kv.block_size
             del s.bh[lcp // BS:]
             keep = (lcp + BS - 1) // BS
-            if lcp % BS and keep <= len(s.blocks) and not self.kv.make_private(s.blocks[keep - 1]):
-                # the history diverges inside a page other threads share: recompute it privately
-                keep -= 1
-                s.n_cached = keep * BS
-            if len(s.blocks) > keep:
-                self.kv.release(s.blocks[keep:])
-                s.blocks = s.blocks[:keep]
+            if s.host is not None:  # swapped to the host tier: bring the kept pages back
+                self._swap_in(s, keep)
+            else:
+                if lcp % BS and keep <= len(s.blocks) and not self.kv.make_private(s.blocks[keep - 1]):
+                    # the history diverges inside a page other threads share: recompute it privately
+                    keep -= 1
+                    s.n_cached = keep * BS
+                if len(s.blocks) > keep:
+                    self.kv.release(s.blocks[keep:])
+                    s.blocks = s.blocks[:keep]
             gs = GrammarState(self.grt, grammar, self.eos_ids, max_tokens=max_new, use_hints=self.cfg.use_hints)
             r = Request(s, gs, max_new, temp, seed, on_done, len(toks), top_k, top_p)
             s.req = r
@@ -155,6 +156,8 @@ class SchedulerMixin:
         need = (upto + self.kv.block_size - 1) // self.kv.block_size - len(s.blocks)
         if need <= 0:
             return True
+        if need > self.kv.free_blocks and self.kv_host is not None:
+            self._swap_make_room(need, protect)
         if need > self.kv.free_blocks:
             self._evict(need - self.kv.free_blocks, protect)
         if need > self.kv.free_blocks:
@@ -163,7 +166,9 @@ class SchedulerMixin:
         return True
 
     def _evict(self, n_blocks: int, protect: set) -> None:
-        idle = sorted((s for s in self._snapshot() if s.req is None and s.blocks and s.id not in protect),
+        """Drop LRU idle threads' pages (their next run re-prefills)."""
+        idle = sorted((s for s in self._snapshot()
+                       if s.req is None and s.blocks and s.id not in protect and not self._loading(s)),
                       key=lambda s: s.last_used)
         freed = 0
         for s in idle:
@@ -174,6 +179,95 @@ class SchedulerMixin:
             self.stats["evictions"] += 1
             if freed >= n_blocks:
                 return
+
+    # ------------------------------------------------------ KV host tier
+    def _loading(self, s: Sequence) -> bool:
+        """True while a swap-in of ``s``'s pages is still on the copy stream."""
+        ev = s.loading
+        if ev is None:
+            return False
+        if ev.query():
+            s.loading = None
+            return False
+        return True
+
+    def _drop_kv(self, s: Sequence, gone: bool = False) -> None:
+        """Give up every page of ``s``, in HBM and on the host (``gone``: the
+        sequence itself is released, not just its cache)."""
+        if self._loading(s):
+            self.kv_host.defer_release(s.blocks, s.loading)  # the copy still writes them
+            s.loading = None
+        else:
+            self.kv.release(s.blocks)
+        s.blocks = []
+        if s.host is not None:
+            (self.kv_host.free if gone else self.kv_host.drop)(s.host)
+            s.host = None
+        s.bh = []
+        s.n_cached = 0
+
+    def _swap_out_idle(self, n_blocks: int, protect: set) -> int:
+        """Swap LRU idle threads to the host tier until ``n_blocks`` pages are
+        on their way back to the pool; returns the pages swapped."""
+        t = self.kv_host
+        idle = sorted((s for s in self._snapshot()
+                       if s.req is None and s.blocks and s.id not in protect and not self._loading(s)),
+                      key=lambda s: s.last_used)
+        got = 0
+        for s in idle:
+            if got >= n_blocks:
+                break
+            nb = len(s.blocks)
+            if t.free_slots < nb:  # the host is full: give up its least recently used copies
+                for v in sorted((v for v in self._snapshot() if v.host is not None and v.req is None
+                                 and v.id not in protect), key=lambda v: v.last_used):
+                    if t.free_slots >= nb or v.last_used > s.last_used:
+                        break
+                    self._drop_kv(v)
+            if t.free_slots < nb:
+                break  # what is left falls to the drop path (_evict)
+            s.host = t.swap_out(s.blocks)
+            s.blocks = []
+            got += nb
+            self.stats["swap_outs"] += 1
+        return got
+
+    def _swap_make_room(self, need: int, protect: set) -> None:
+        """``need`` free pages now: swap idle threads out and wait for enough
+        of the copies to land (the watermark makes this rare)."""
+        t = self.kv_host
+        t.poll()
+        short = need - self.kv.free_blocks - t.pending_blocks
+        if short > 0:
+            self._swap_out_idle(short, protect)
+        if need > self.kv.free_blocks:
+            t.wait_out(need - self.kv.free_blocks)
+
+    def _swap_tick(self) -> None:
+        """Keep free + in-flight pages at the watermark by swapping ahead of need."""
+        t = self.kv_host
+        t.poll()
+        deficit = self.kv_watermark - self.kv.free_blocks - t.pending_blocks
+        if deficit > 0:
+            self._swap_out_idle(deficit, set())
+
+    def _swap_in(self, s: Sequence, keep: int) -> None:
+        """Admission of a swapped thread: pages [0, keep) come back from the
+        host (the run is scheduled once the copy is done), the rest are freed."""
+        t = self.kv_host
+        slots, s.host = s.host, None
+        keep = min(keep, len(slots))
+        t.free(slots[keep:])
+        s.n_cached = min(s.n_cached, keep * self.kv.block_size)
+        if keep and self._ensure_blocks(s, keep * self.kv.block_size, {s.id}):
+            s.loading = t.swap_in(slots[:keep], s.blocks)
+            self.stats["swap_ins"] += 1
+            return
+        t.drop(slots[:keep])
+        self.kv.release(s.blocks)
+        s.blocks = []
+        s.bh = []
+        s.n_cached = 0
 
     def _defer_prefill(self, cands: List["Sequence"]) -> bool:
         """Hold this step's prefill back (``EngineConfig.prefill_min_tokens``):
@@ -202,6 +296,8 @@ class SchedulerMixin:
         self.stats["admit_s"] += time.perf_counter() - t_host0
         if self._releases:
             self._apply_releases()
+        if self.kv_host is not None:
+            self._swap_tick()
         # The previous forward's sampling is launched only now, AFTER this
         # step is scheduled, so sample(k) and forward(k+1) reach the GPU back
         # to back while it is still busy with forward(k): the host's
@@ -211,12 +307,17 @@ class SchedulerMixin:
         if ps is not None:
             for s in ps[1]:
                 s.tokens.append(SPEC)
-        active = [s for s in self._snapshot() if s.req is not None and s.pending > 0]
+        snap = self._snapshot()
+        active = [s for s in snap if s.req is not None and s.pending > 0 and not self._loading(s)]
         if not active:
             if ps is not None:  # nothing else to run: just finish the pending sample
                 for s in ps[1]:
                     s.tokens.pop()
                 self._process_tokens(self._launch_sample(*ps))
+                return True
+            loading = [s for s in snap if s.req is not None and s.loading is not None]
+            if loading:  # only swap-ins are pending: wait for the oldest
+                loading[0].loading.synchronize()
                 return True
             return False
         BS = self.kv.block_size
@@ -353,6 +454,8 @@ class SchedulerMixin:
                 continue
             if v.req.t_submit <= s.req.t_submit:
                 break  # only younger requests yield to older ones
+            if self._loading(v):
+                continue  # its swap-in still writes the pages
             self.kv.release(v.blocks)  # pages other threads share stay resident
             v.blocks = []
             v.bh = []

@@ -115,6 +115,12 @@ class EngineConfig:
     temperature: float = 0.7
     use_hints: bool = True
     logits_fp32: bool = True   # lm_head writes fp32 logits for the sampler
+    # KV host tier (engine/kv_offload.py): GB of page-locked host memory that idle
+    # threads' pages are swapped to instead of being dropped (0 = off; TP = 1)
+    kv_host_gb: float = field(default_factory=lambda: _knob("kv_host_gb", 0.0))
+    # swap idle threads out ahead of need while free + in-flight pool pages are
+    # below this many (None: one max-size prefill step plus one full thread)
+    kv_host_watermark: Optional[int] = None
     model_overrides: dict = field(default_factory=dict)
 
 
@@ -142,7 +148,7 @@ class Request:
 
 
 class Sequence:
-    __slots__ = ("id", "tokens", "n_cached", "blocks", "req", "last_used", "bh")
+    __slots__ = ("id", "tokens", "n_cached", "blocks", "req", "last_used", "bh", "host", "loading")
 
     def __init__(self, sid: int):
         self.id = sid
@@ -152,6 +158,12 @@ class Sequence:
         self.bh: List[int] = []  # chain keys of the leading full blocks (prefix table)
         self.req: Optional[Request] = None
         self.last_used = 0.0
+        # KV host tier (engine/kv_offload.py): while swapped out, ``blocks`` is
+        # empty and ``host`` holds the host slots of pages 0..len(host)-1 (the
+        # first n_cached tokens); ``loading`` is the completion event of a
+        # swap-in still on the copy stream (the sequence is not scheduled before)
+        self.host: Optional[List[int]] = None
+        self.loading = None
 
     @property
     def pending(self) -> int:

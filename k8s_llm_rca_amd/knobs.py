@@ -124,6 +124,7 @@ class Knobs:
     prefill_min: Optional[int] = _f(None, "EngineConfig.prefill_min_tokens override")
     prefill_defer_rows: Optional[int] = _f(None, "EngineConfig.prefill_defer_min_rows override")
     prefill_defer_s: Optional[float] = _f(None, "EngineConfig.prefill_max_defer_s override")
+    kv_host_gb: Optional[float] = _f(None, "EngineConfig.kv_host_gb override (KV host tier, GB pinned)")
     tiny_chunk_tokens: Optional[int] = _f(None, "EngineConfig.tiny_chunk_tokens override",
                                           legacy="K8S_TINY_CHUNK_TOKENS")
     shape_trace: Optional[str] = _f(None, "append every step's attention shapes to this JSONL file",

@@ -75,6 +75,10 @@ _SIGS = {
     "k8s_state_lookup": [P, P, P, P, P, P, P, I, I, I, I, P, P, P, I, P, P, P],
     "k8s_window_mark": [I, P],
     "k8s_host_flag": [P, I, P],
+    "k8s_kv_stage": [P, P, P, ctypes.c_long, I, I, P, I, I, P],
+    "k8s_host_register": [P, ctypes.c_long],
+    "k8s_host_unregister": [P],
+    "k8s_memcpy_async": [P, P, ctypes.c_long, P],
     "k8s_set_knob": [I, I],
     "k8s_nonfinite_flag": [P, ctypes.c_long, P, P],
     "k8s_get_knob": [I],

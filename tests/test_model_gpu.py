@@ -433,3 +433,66 @@ def test_token_flag_wait_same_tokens():
             outs.append(res)
     SM.TOKEN_FLAG_MIN_ROWS = min_rows
     assert outs[0] == outs[1] and all(len(v) == 16 for v in outs[0].values())
+
+
+def test_kv_stage_round_trip_kernel():
+    """k8s_kv_stage + the DMA copies of the KV host tier (engine/kv_offload.py):
+    pages swapped out and back into other pool pages are bit-identical, across
+    staging chunks and runs of consecutive host slots."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.kv_cache import KVPool
+    from k8s_llm_rca_amd.engine.kv_offload import KVHostTier
+    pool = KVPool(3, 8, 128, 40, 64, "cuda", torch.bfloat16)
+    g = torch.Generator(device="cuda").manual_seed(3)
+    pool.k.copy_(torch.randn(pool.k.shape, generator=g, device="cuda"))
+    pool.v.copy_(torch.randn(pool.v.shape, generator=g, device="cuda"))
+    blocks = pool.alloc(12)
+    src = [blocks[i] for i in (0, 1, 2, 5, 7, 8, 11)]
+    ref_k, ref_v = pool.k[:, src].clone(), pool.v[:, src].clone()
+    per = KVPool.bytes_per_block(3, 8, 128, 64)
+    t = KVHostTier(pool, 16, staging_bytes=3 * per)  # 3 blocks per staging chunk
+    assert t.chunk == 3
+    slots = t.swap_out(src)
+    t.drain()
+    assert pool.free_blocks == 40 - 12 + len(src)
+    pool.k.zero_()
+    pool.v.zero_()
+    dst = pool.alloc(len(src))[::-1]
+    ev = t.swap_in(slots, dst)
+    ev.synchronize()
+    torch.cuda.synchronize()
+    assert torch.equal(pool.k[:, dst], ref_k) and torch.equal(pool.v[:, dst], ref_v)
+    t.close()
+
+
+def test_kv_host_tier_same_tokens():
+    """An engine whose pool is too small for its idle threads swaps them to the
+    host tier and back: the generations (greedy) are the same as with a pool
+    that never runs short, nothing is dropped or re-prefilled."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.engine.kv_cache import KVPool
+
+    def run(**kw):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", temperature=0.0,
+                                     graph_batch_sizes=(1, 2, 4, 8), **kw))
+        outs = {}
+        sids = [eng.new_sequence() for _ in range(4)]
+        for r in range(3):
+            for i, sid in enumerate(sids):
+                base = eng.seqs[sid].tokens if r else eng.tok.system_prefix("s")
+                p = base + eng.tok.message("user", ("t%d r%d " % (i, r)) * 12) + eng.tok.header("assistant")
+                eng.submit(sid, p, None, 12, temperature=0.0, on_done=lambda g, st, k=(r, i): outs.__setitem__(k, g))
+                eng.run_until_idle()
+        eng.stop()
+        return eng, outs
+
+    ref, want = run(num_blocks=256)
+    per = KVPool.bytes_per_block(ref.mc.n_layers, ref.model.nkv, ref.model.D, 64)
+    eng, got = run(num_blocks=10, kv_host_gb=64 * per / (1 << 30), kv_host_watermark=2)
+    assert got == want and all(v is not None for v in got.values())
+    assert eng.stats["evictions"] == 0 and eng.stats["swap_outs"] > 0 and eng.stats["swap_ins"] > 0
+    assert eng.stats["prefill_tokens"] == ref.stats["prefill_tokens"]
+    eng.kv_host.close()

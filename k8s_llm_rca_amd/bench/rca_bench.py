@@ -660,6 +660,10 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # the same model served with an 8k window (config.truncation.max_context): threads are cut
     # where Llama-3's are, the steady state is reachable (12 pre-aged incidents) and 64 pipelines'
     # KV fits beside the experts -- 1.74 /s at p50 30.5 s, 0 preemptions (profiles/r5/mixtral_8k/)
+    # Llama-3-70B on ONE GPU (TP = 1): 141 GB of weights leave ~413k tokens of KV, 20 pipelines' threads;
+    # with idle threads swapped to a 140 GB host tier (engine/kv_offload.py) 48 pipelines run without
+    # re-prefills: 0.668 analyses/s vs 0.486 at 20 and 0.469 at 40 without it (profiles/r6/kvhost/)
+    "llama3-70b-tp1-host": dict(model="llama3-70b", incidents=48, quantum=4, kv_host_gb=140.0),
     "mixtral-10k-8k": dict(model="mixtral-8x7b", graph_nodes=10_000, max_context=8192, incidents=64, quantum=8),
 }
 

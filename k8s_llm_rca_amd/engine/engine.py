@@ -42,6 +42,7 @@ from ..ops import attention as A
 from ..parallel.groups import ParallelContext, single
 from .graph_runner import GraphRunnerMixin
 from .kv_cache import KVPool
+from .kv_manager import KVCacheManager
 from .sampler import SamplerMixin
 from .scheduler import SchedulerMixin
 from .step_exec import StepExecMixin
@@ -63,7 +64,10 @@ def _build_model(mc: ModelConfig, device, dtype, pc, seed):
 class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
     """The engine: lifecycle, submission API and state; scheduling
     (``scheduler.py``), step packing / execution (``step_exec.py``), HIP-graph
-    decode (``graph_runner.py``) and sampling (``sampler.py``) are its mixins."""
+    decode (``graph_runner.py``) and sampling (``sampler.py``) are its mixins.
+    The KV side is an object of its own: ``self.kvm`` (``kv_manager.py``) owns
+    the page pool, the host tier and every allocation / eviction / swap /
+    preemption / prefix-sharing policy, and touches only sequences' cache fields."""
 
     def __init__(self, cfg: EngineConfig, pc: Optional[ParallelContext] = None, model=None):
         self.cfg = cfg
@@ -135,6 +139,7 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
                              else min(nb // 4, (cfg.max_batch_tokens + self.max_context) // BS + 2))
         self.max_blocks_per_seq = (self.max_context + BS - 1) // BS + 1
         self.seqs: Dict[int, Sequence] = {}
+        self.kvm = None  # KVCacheManager: set below, once the stats dict exists
         self._next_sid = 0
         self._incoming: List[tuple] = []
         self._releases: List[int] = []
@@ -203,6 +208,8 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
                       "timeouts": 0,
                       "recompute_tokens": 0, "kv_read_blocks_sampled": 0, "kv_unique_blocks_sampled": 0,
                       "tiny_chunk_tokens": 0, "swap_outs": 0, "swap_ins": 0}
+        # where every thread's KV lives and what happens when HBM runs short (kv_manager.py)
+        self.kvm = KVCacheManager(self.kv, self.kv_host, self.kv_watermark, self._snapshot, self.stats)
         self._cancels: List[int] = []
         self.error: Optional[BaseException] = None
         self._fault: Optional[str] = None  # a dead communicator: every later request fails at admission
@@ -379,7 +386,7 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
             r = s.req
             if r is not None:
                 s.req = None
-                self._drop_kv(s)
+                self.kvm.drop(s)
                 if r.on_done:
                     r.on_done(None, {"error": err})
 

@@ -23,7 +23,6 @@ from ..ops import attention as A
 from ..ops import sampling as SMP
 from ..ops._lib import scratch
 from ..utils import tracing
-from .kv_cache import chain_key
 from .structured import GrammarState
 from .types import PART_MIN, SPEC, InFlight, Request, Sequence, _LazySample, _spec_tok
 

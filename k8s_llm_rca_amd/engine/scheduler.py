@@ -1,11 +1,11 @@
 """LLM engine, part 1 of 4: scheduling (``LLMEngine`` = these mixins + the
 lifecycle in ``engine.py``).
 
-Admission of submitted runs (per-thread prefix reuse, cross-thread prefix
-attach, grammar driving / jump-forward), KV page allocation with LRU eviction
-and recompute preemption, prompt-prefill batching, and ``step()``: which
-decode rows and prefill chunks go into the next forward, overlapped with the
-host processing of the previous step.  The reference has no scheduler: its
+Admission of submitted runs (grammar driving / jump-forward; the KV side --
+prefix reuse, sharing, allocation, eviction, swap, preemption -- is the
+``KVCacheManager`` in ``kv_manager.py``, ``self.kvm``), prompt-prefill
+batching, and ``step()``: which decode rows and prefill chunks go into the
+next forward, overlapped with the host processing of the previous step.  The reference has no scheduler: its
 driver loops run one GPT-4 call at a time (``/root/reference/test_with_file.py:64,111,159``).
 """
 from __future__ import annotations
@@ -26,7 +26,6 @@ from ..ops import attention as A
 from ..ops import sampling as SMP
 from ..ops._lib import scratch
 from ..utils import tracing
-from .kv_cache import chain_key
 from .structured import GrammarState
 from .types import PART_MIN, SPEC, InFlight, Request, Sequence, _LazySample, _spec_tok
 
@@ -45,7 +44,7 @@ class SchedulerMixin:
                     continue
                 s = self.seqs.pop(sid, None)
                 if s is not None:
-                    self._drop_kv(s, gone=True)
+                    self.kvm.drop(s, gone=True)
             self._releases = keep + self._releases
 
     def _apply_cancels(self, in_flight: set) -> None:
@@ -97,19 +96,7 @@ class SchedulerMixin:
             self.stats["recompute_tokens"] += max(0, n - lcp)
             s.tokens = toks
             s.n_cached = lcp
-            BS = self.kv.block_size
-            del s.bh[lcp // BS:]
-            keep = (lcp + BS - 1) // BS
-            if s.host is not None:  # swapped to the host tier: bring the kept pages back
-                self._swap_in(s, keep)
-            else:
-                if lcp % BS and keep <= len(s.blocks) and not self.kv.make_private(s.blocks[keep - 1]):
-                    # the history diverges inside a page other threads share: recompute it privately
-                    keep -= 1
-                    s.n_cached = keep * BS
-                if len(s.blocks) > keep:
-                    self.kv.release(s.blocks[keep:])
-                    s.blocks = s.blocks[:keep]
+            self.kvm.keep_prefix(s, lcp)  # KV of the common prefix kept (or swapped back in)
             gs = GrammarState(self.grt, grammar, self.eos_ids, max_tokens=max_new, use_hints=self.cfg.use_hints)
             r = Request(s, gs, max_new, temp, seed, on_done, len(toks), top_k, top_p)
             s.req = r
@@ -152,123 +139,6 @@ class SchedulerMixin:
         if r.on_done:
             r.on_done(list(r.generated), st)
 
-    def _ensure_blocks(self, s: Sequence, upto: int, protect: set) -> bool:
-        need = (upto + self.kv.block_size - 1) // self.kv.block_size - len(s.blocks)
-        if need <= 0:
-            return True
-        if need > self.kv.free_blocks and self.kv_host is not None:
-            self._swap_make_room(need, protect)
-        if need > self.kv.free_blocks:
-            self._evict(need - self.kv.free_blocks, protect)
-        if need > self.kv.free_blocks:
-            return False
-        s.blocks.extend(self.kv.alloc(need))
-        return True
-
-    def _evict(self, n_blocks: int, protect: set) -> None:
-        """Drop LRU idle threads' pages (their next run re-prefills)."""
-        idle = sorted((s for s in self._snapshot()
-                       if s.req is None and s.blocks and s.id not in protect and not self._loading(s)),
-                      key=lambda s: s.last_used)
-        freed = 0
-        for s in idle:
-            freed += self.kv.release(s.blocks)  # pages other threads still share stay resident
-            s.blocks = []
-            s.bh = []
-            s.n_cached = 0
-            self.stats["evictions"] += 1
-            if freed >= n_blocks:
-                return
-
-    # ------------------------------------------------------ KV host tier
-    def _loading(self, s: Sequence) -> bool:
-        """True while a swap-in of ``s``'s pages is still on the copy stream."""
-        ev = s.loading
-        if ev is None:
-            return False
-        if ev.query():
-            s.loading = None
-            return False
-        return True
-
-    def _drop_kv(self, s: Sequence, gone: bool = False) -> None:
-        """Give up every page of ``s``, in HBM and on the host (``gone``: the
-        sequence itself is released, not just its cache)."""
-        if self._loading(s):
-            self.kv_host.defer_release(s.blocks, s.loading)  # the copy still writes them
-            s.loading = None
-        else:
-            self.kv.release(s.blocks)
-        s.blocks = []
-        if s.host is not None:
-            (self.kv_host.free if gone else self.kv_host.drop)(s.host)
-            s.host = None
-        s.bh = []
-        s.n_cached = 0
-
-    def _swap_out_idle(self, n_blocks: int, protect: set) -> int:
-        """Swap LRU idle threads to the host tier until ``n_blocks`` pages are
-        on their way back to the pool; returns the pages swapped."""
-        t = self.kv_host
-        idle = sorted((s for s in self._snapshot()
-                       if s.req is None and s.blocks and s.id not in protect and not self._loading(s)),
-                      key=lambda s: s.last_used)
-        got = 0
-        for s in idle:
-            if got >= n_blocks:
-                break
-            nb = len(s.blocks)
-            if t.free_slots < nb:  # the host is full: give up its least recently used copies
-                for v in sorted((v for v in self._snapshot() if v.host is not None and v.req is None
-                                 and v.id not in protect), key=lambda v: v.last_used):
-                    if t.free_slots >= nb or v.last_used > s.last_used:
-                        break
-                    self._drop_kv(v)
-            if t.free_slots < nb:
-                break  # what is left falls to the drop path (_evict)
-            s.host = t.swap_out(s.blocks)
-            s.blocks = []
-            got += nb
-            self.stats["swap_outs"] += 1
-        return got
-
-    def _swap_make_room(self, need: int, protect: set) -> None:
-        """``need`` free pages now: swap idle threads out and wait for enough
-        of the copies to land (the watermark makes this rare)."""
-        t = self.kv_host
-        t.poll()
-        short = need - self.kv.free_blocks - t.pending_blocks
-        if short > 0:
-            self._swap_out_idle(short, protect)
-        if need > self.kv.free_blocks:
-            t.wait_out(need - self.kv.free_blocks)
-
-    def _swap_tick(self) -> None:
-        """Keep free + in-flight pages at the watermark by swapping ahead of need."""
-        t = self.kv_host
-        t.poll()
-        deficit = self.kv_watermark - self.kv.free_blocks - t.pending_blocks
-        if deficit > 0:
-            self._swap_out_idle(deficit, set())
-
-    def _swap_in(self, s: Sequence, keep: int) -> None:
-        """Admission of a swapped thread: pages [0, keep) come back from the
-        host (the run is scheduled once the copy is done), the rest are freed."""
-        t = self.kv_host
-        slots, s.host = s.host, None
-        keep = min(keep, len(slots))
-        t.free(slots[keep:])
-        s.n_cached = min(s.n_cached, keep * self.kv.block_size)
-        if keep and self._ensure_blocks(s, keep * self.kv.block_size, {s.id}):
-            s.loading = t.swap_in(slots[:keep], s.blocks)
-            self.stats["swap_ins"] += 1
-            return
-        t.drop(slots[:keep])
-        self.kv.release(s.blocks)
-        s.blocks = []
-        s.bh = []
-        s.n_cached = 0
-
     def _defer_prefill(self, cands: List["Sequence"]) -> bool:
         """Hold this step's prefill back (``EngineConfig.prefill_min_tokens``):
         only when every candidate is a new run's prompt (no token generated
@@ -296,8 +166,7 @@ class SchedulerMixin:
         self.stats["admit_s"] += time.perf_counter() - t_host0
         if self._releases:
             self._apply_releases()
-        if self.kv_host is not None:
-            self._swap_tick()
+        self.kvm.tick()  # KV host tier: landed swap-outs, swap ahead of need
         # The previous forward's sampling is launched only now, AFTER this
         # step is scheduled, so sample(k) and forward(k+1) reach the GPU back
         # to back while it is still busy with forward(k): the host's
@@ -308,7 +177,7 @@ class SchedulerMixin:
             for s in ps[1]:
                 s.tokens.append(SPEC)
         snap = self._snapshot()
-        active = [s for s in snap if s.req is not None and s.pending > 0 and not self._loading(s)]
+        active = [s for s in snap if s.req is not None and s.pending > 0 and not self.kvm.loading(s)]
         if not active:
             if ps is not None:  # nothing else to run: just finish the pending sample
                 for s in ps[1]:
@@ -328,8 +197,8 @@ class SchedulerMixin:
         placed: set = set()
         for s in active:
             if s.pending == 1 and len(decode) < self.cfg.max_decode_seqs:
-                if self._ensure_blocks(s, s.n_cached + 1, protect) or self._preempt_for(s, s.n_cached + 1, placed,
-                                                                                        protect, active):
+                if (self.kvm.ensure_blocks(s, s.n_cached + 1, protect)
+                        or self.kvm.preempt_for(s, s.n_cached + 1, placed, protect, active)):
                     decode.append(s)
                     placed.add(s.id)
         budget -= len(decode)
@@ -350,10 +219,10 @@ class SchedulerMixin:
                 self._fail_req(s.req, "context longer than the whole KV pool")
                 continue
             if self.cfg.prefix_sharing and s.n_cached % BS == 0 and len(s.blocks) == s.n_cached // BS:
-                self._attach_prefix(s)
+                self.kvm.attach_prefix(s)
                 q = min(s.pending, budget)
-            if not (self._ensure_blocks(s, s.n_cached + q, protect)
-                    or self._preempt_for(s, s.n_cached + q, placed, protect, active)):
+            if not (self.kvm.ensure_blocks(s, s.n_cached + q, protect)
+                    or self.kvm.preempt_for(s, s.n_cached + q, placed, protect, active)):
                 continue
             chunks.append((s, q))
             placed.add(s.id)
@@ -409,7 +278,7 @@ class SchedulerMixin:
             s.last_used = time.perf_counter()
         if self.cfg.prefix_sharing:
             for s, _ in chunks:  # publish the pages this prefill completed (their KV write is enqueued)
-                self._register_blocks(s)
+                self.kvm.register_blocks(s)
         self.stats["steps"] += 1
         n_rows = len(drows) + sum(q for _, q in big)
         if n_rows <= 256:  # decode-size step: the projections stream every weight once (M <= 256 kernels)
@@ -431,7 +300,7 @@ class SchedulerMixin:
                 p = spec_pos.get(s.id)
                 if p is not None and (len(s.tokens) <= p or s.tokens[p] != t):
                     s.n_cached = p  # the speculative KV at p is not this sequence's token (it finished)
-                    del s.bh[p // self.kv.block_size:]
+                    self.kvm.truncate_chain(s, p)
         # rows still waiting for a sample (a finished or newly-forced sequence is not)
         keep = [(i, s) for i, (ri, s) in enumerate(sample_rows)
                 if s.req is not None and s.n_cached == len(s.tokens)]
@@ -443,59 +312,3 @@ class SchedulerMixin:
             else:
                 self._process_tokens(self._launch_sample(*pend))
         return True
-
-    def _preempt_for(self, s: Sequence, upto: int, placed: set, protect: set, active: List[Sequence]) -> bool:
-        """Free KV for ``s`` by preempting younger active requests (youngest
-        first; not ones already placed in this step): a victim keeps its
-        request and tokens, drops its pages and is re-prefilled when pages
-        are free again (recompute preemption).  False if ``s`` still does not fit."""
-        for v in reversed(active):
-            if v is s or v.req is None or v.id in placed or not v.blocks:
-                continue
-            if v.req.t_submit <= s.req.t_submit:
-                break  # only younger requests yield to older ones
-            if self._loading(v):
-                continue  # its swap-in still writes the pages
-            self.kv.release(v.blocks)  # pages other threads share stay resident
-            v.blocks = []
-            v.bh = []
-            v.n_cached = 0
-            self.stats["preemptions"] += 1
-            if self._ensure_blocks(s, upto, protect):
-                return True
-        return False
-
-    def _attach_prefix(self, s: Sequence) -> None:
-        """Map the next full blocks of ``s``'s prompt onto published pages
-        (at least one token is left to prefill: it produces the logits)."""
-        BS = self.kv.block_size
-        toks = s.tokens
-        parent = s.bh[-1] if s.bh else 0
-        if len(s.bh) != len(s.blocks):  # chain keys of this thread's own leading pages first
-            for j in range(len(s.bh), len(s.blocks)):
-                parent = chain_key(parent, toks[j * BS:(j + 1) * BS])
-                s.bh.append(parent)
-        n = s.n_cached
-        hit = 0
-        while n + BS < len(toks):
-            k = chain_key(parent, toks[n:n + BS])
-            b = self.kv.lookup(k)
-            if b is None:
-                break
-            s.blocks.append(b)
-            s.bh.append(k)
-            parent = k
-            n += BS
-            hit += 1
-        if hit:
-            s.n_cached = n
-            self.stats["prefix_hit_tokens"] += hit * BS
-
-    def _register_blocks(self, s: Sequence) -> None:
-        BS = self.kv.block_size
-        toks = s.tokens
-        parent = s.bh[-1] if s.bh else 0
-        for j in range(len(s.bh), s.n_cached // BS):
-            parent = chain_key(parent, toks[j * BS:(j + 1) * BS])
-            s.bh.append(parent)
-            self.kv.register(s.blocks[j], parent)

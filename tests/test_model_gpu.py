@@ -241,7 +241,7 @@ def test_tiny_chunk_decode_rows_match_prefill_logits(graphs):
     for n0, q in ((40, 6), (63, 5), (64, 8), (254, 6), (1000, 7)):
         s = eng.seqs[eng.new_sequence()]
         s.tokens = torch.randint(5, 1000, (n0 + q,), generator=g).tolist()
-        assert eng._ensure_blocks(s, n0 + q, set())
+        assert eng.kvm.ensure_blocks(s, n0 + q, set())
         eng._forward([], [(s, n0)], [n0 - 1])
         s.n_cached = n0
         big = eng._forward([], [(s, q)], list(range(q))).float()

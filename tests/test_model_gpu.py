@@ -496,3 +496,39 @@ def test_kv_host_tier_same_tokens():
     assert eng.stats["evictions"] == 0 and eng.stats["swap_outs"] > 0 and eng.stats["swap_ins"] > 0
     assert eng.stats["prefill_tokens"] == ref.stats["prefill_tokens"]
     eng.kv_host.close()
+
+
+def test_kv_host_tier_concurrent_runs_same_tokens():
+    """Every thread's next run submitted at once while the pool holds only a few
+    threads: swap-ins run on the copy stream while other rows decode, and a run
+    is scheduled only once its pages have landed -- the same greedy tokens as a
+    pool that never runs short."""
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from k8s_llm_rca_amd.engine.engine import EngineConfig, LLMEngine
+    from k8s_llm_rca_amd.engine.kv_cache import KVPool
+
+    def run(**kw):
+        eng = LLMEngine(EngineConfig(model="tiny-llama", device="cuda", temperature=0.0,
+                                     graph_batch_sizes=(1, 2, 4, 8), **kw))
+        outs = {}
+        sids = [eng.new_sequence() for _ in range(6)]
+        for r in range(3):
+            for half in (sids[:3], sids[3:]):  # three threads run together, the other three idle
+                for sid in half:
+                    i = sids.index(sid)
+                    base = eng.seqs[sid].tokens if r else eng.tok.system_prefix("s")
+                    p = base + eng.tok.message("user", ("c%d r%d " % (i, r)) * (8 + 3 * i)) + \
+                        eng.tok.header("assistant")
+                    eng.submit(sid, p, None, 10, temperature=0.0,
+                               on_done=lambda g, st, k=(r, i): outs.__setitem__(k, g))
+                eng.run_until_idle()
+        eng.stop()
+        return eng, outs
+
+    ref, want = run(num_blocks=512)
+    per = KVPool.bytes_per_block(ref.mc.n_layers, ref.model.nkv, ref.model.D, 64)
+    eng, got = run(num_blocks=20, kv_host_gb=128 * per / (1 << 30), kv_host_watermark=2)
+    assert got == want and all(v is not None for v in got.values())
+    assert eng.stats["swap_ins"] > 0 and eng.stats["evictions"] == 0
+    eng.kv_host.close()

@@ -38,6 +38,7 @@ import ctypes
 import logging
 import sys
 import time
+import weakref
 from typing import List, Optional, Tuple
 
 import torch
@@ -62,6 +63,11 @@ def _runs(ids: List[int]) -> List[Tuple[int, int, int]]:
     return out
 
 
+def _unregister(host: torch.Tensor) -> None:
+    from ..ops._lib import lib
+    lib().k8s_host_unregister(host.data_ptr())
+
+
 class KVHostTier:
     def __init__(self, pool: KVPool, host_blocks: int, staging_bytes: int = 512 << 20):
         if host_blocks < 1:
@@ -84,6 +90,9 @@ class KVHostTier:
             check(lib().k8s_host_register(self.host.data_ptr(), self.host.numel() * self.host.element_size()),
                   "k8s_host_register")
             self._registered = True
+            # unlocked when the tier is collected (never at interpreter exit: the OS reclaims it)
+            self._fin = weakref.finalize(self, _unregister, self.host)
+            self._fin.atexit = False
         self.t_pin = time.perf_counter() - t0
         self._free: List[int] = list(range(host_blocks - 1, -1, -1))
         self.chunk = max(1, min(MAX_IDS, staging_bytes // self.block_bytes))
@@ -155,12 +164,11 @@ class KVHostTier:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ready)
-        with torch.cuda.stream(self.stream):
-            for c0 in range(0, len(blocks), self.chunk):
-                cb, cs = blocks[c0:c0 + self.chunk], slots[c0:c0 + self.chunk]
-                self._stage(cb, pack=True)
-                for i, s0, n in _runs(cs):
-                    self._copy(self.host[s0].data_ptr(), self.stage[i].data_ptr(), n)
+        for c0 in range(0, len(blocks), self.chunk):  # gather + DMA, in order on the copy stream
+            cb, cs = blocks[c0:c0 + self.chunk], slots[c0:c0 + self.chunk]
+            self._stage(cb, pack=True)
+            for i, s0, n in _runs(cs):
+                self._copy(self.host[s0].data_ptr(), self.stage[i].data_ptr(), n)
         done = torch.cuda.Event()
         done.record(self.stream)
         self._out.append((done, list(blocks)))
@@ -187,12 +195,11 @@ class KVHostTier:
         ready = torch.cuda.Event()
         ready.record(torch.cuda.current_stream(self.device))
         self.stream.wait_event(ready)
-        with torch.cuda.stream(self.stream):
-            for c0 in range(0, len(blocks), self.chunk):
-                cb, cs = blocks[c0:c0 + self.chunk], slots[c0:c0 + self.chunk]
-                for i, s0, n in _runs(cs):
-                    self._copy(self.stage[i].data_ptr(), self.host[s0].data_ptr(), n)
-                self._stage(cb, pack=False)
+        for c0 in range(0, len(blocks), self.chunk):  # DMA + scatter, in order on the copy stream
+            cb, cs = blocks[c0:c0 + self.chunk], slots[c0:c0 + self.chunk]
+            for i, s0, n in _runs(cs):
+                self._copy(self.stage[i].data_ptr(), self.host[s0].data_ptr(), n)
+            self._stage(cb, pack=False)
         done = torch.cuda.Event()
         done.record(self.stream)
         self.free(slots)  # a later swap-out into them is ordered behind this copy (same stream)
@@ -247,8 +254,7 @@ class KVHostTier:
         """Finish every transfer and unlock the host buffer."""
         if self._registered:
             self.drain()
-            from ..ops._lib import lib
-            lib().k8s_host_unregister(self.host.data_ptr())
+            self._fin()
             self._registered = False
 
     def report(self) -> dict:

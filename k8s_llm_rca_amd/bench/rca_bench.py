@@ -664,6 +664,13 @@ PRESETS: Dict[str, Dict[str, Any]] = {
     # with idle threads swapped to a 140 GB host tier (engine/kv_offload.py) 48 pipelines run without
     # re-prefills: 0.668 analyses/s vs 0.486 at 20 and 0.469 at 40 without it (profiles/r6/kvhost/)
     "llama3-70b-tp1-host": dict(model="llama3-70b", incidents=48, quantum=4, kv_host_gb=140.0),
+    # the same two Mixtral configs at twice the concurrency, idle threads on the KV host tier
+    # (profiles/r6/kvhost/): 32k window 1.33 -> 1.62 /s at 96 (p50 28.9 -> 47.7 s); 8k window
+    # 1.74 -> 2.39 /s at 128 (p50 30.5 -> 58.9 s) -- throughput per GPU for latency
+    "mixtral-10k-host": dict(model="mixtral-8x7b", graph_nodes=10_000, thread_age=4, incidents=96, quantum=12,
+                             kv_host_gb=120.0),
+    "mixtral-10k-8k-host": dict(model="mixtral-8x7b", graph_nodes=10_000, max_context=8192, incidents=128,
+                                quantum=16, kv_host_gb=100.0),
     "mixtral-10k-8k": dict(model="mixtral-8x7b", graph_nodes=10_000, max_context=8192, incidents=64, quantum=8),
 }
 

@@ -173,8 +173,12 @@ class LLMEngine(SchedulerMixin, StepExecMixin, GraphRunnerMixin, SamplerMixin):
                              and self.model.vocab_local % 8 == 0)
         # TP: every rank needs the sampled tokens on its device to overlap steps
         self._async = cfg.async_steps and (self.pc.tp_size == 1 or self._dist_sample or self._sim)
-        self._mask_sent = 0      # rank 0: mask-table rows already broadcast to the workers
-        self._wmask = None       # TP ranks: device copy of the mask table (rows received so far)
+        # TP: the vocab-parallel sampler (its own object, tp_sampler.py)
+        self.tps = None
+        if self._dist_sample:
+            from .tp_sampler import VocabParallelSampler
+            self.tps = VocabParallelSampler(self.pc, self.device, self.vocab, self.model.vocab_local, self.grt,
+                                            self._chan, self._to_dev)
         # knob shape_trace=path: append every step's attention shapes as JSON
         # lines (replayed by tools/bench_kernels.py --what replay)
         self._shape_trace = KNOBS.shape_trace

@@ -370,7 +370,7 @@ class StepExecMixin:
                               "this worker stops executing steps", self.pc.tp_rank)
                     continue
                 hdr, flat, rows_a = arrs
-                self._last_tok = self._sample_rows(logits, hdr, flat, rows_a)
+                self._last_tok = self.tps.sample_rows(logits, hdr, flat, rows_a)
                 if car is not None and ready:
                     if status is None:
                         status = torch.zeros(1, dtype=torch.int32, pin_memory=True)

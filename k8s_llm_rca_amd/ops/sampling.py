@@ -79,7 +79,7 @@ def combine_candidates(cands: torch.Tensor, top_k: torch.Tensor, top_p: torch.Te
     scores (identical on every rank).  Exact for rows with ``0 < top_k <=
     CAND_K``: the whole top-k set, hence the nucleus and its mass, is in the
     union.  The engine sends every other filtered row through a logits
-    all-gather instead (``LLMEngine._sample_gathered``)."""
+    all-gather instead (``VocabParallelSampler._sample_gathered``, engine/tp_sampler.py)."""
     tp, B, C, _ = cands.shape
     allc = cands.permute(1, 0, 2, 3).reshape(B, tp * C, 3)
     v, ids, sc = allc[..., 0], allc[..., 1].round().long(), allc[..., 2]
@@ -114,7 +114,7 @@ def combine_candidates(cands: torch.Tensor, top_k: torch.Tensor, top_p: torch.Te
 
 def combine_shards(pairs: torch.Tensor, cands: Optional[torch.Tensor], cand_rows: Optional[torch.Tensor],
                    top_k: Optional[torch.Tensor], top_p: Optional[torch.Tensor]) -> torch.Tensor:
-    """The TP sampler's combine (``LLMEngine._sample_shard``): [tp, B, 2]
+    """The TP sampler's combine (``VocabParallelSampler._sample_shard``): [tp, B, 2]
     winners -> [B] tokens, and for the ``cand_rows`` (bool [B]: top-k rows with
     ``k <= CAND_K``) the exact top-k / top-p pick from the [tp, B, C, 3]
     candidates.  A row that any shard flagged ``NON_FINITE`` keeps the flag:

@@ -193,7 +193,7 @@ class XgmiAllReduce:
         """[world, *x.shape] = every rank's ``x`` (any dtype: the bytes are
         moved as bf16 pairs through :meth:`all_to_all` with the row replicated
         for every destination).  Device-side, no host sync: the TP sampler's
-        winners / candidates travel this way (``LLMEngine._sample_shard``).
+        winners / candidates travel this way (``VocabParallelSampler._sample_shard``).
         Larger than the buffer: consecutive buffer-sized pieces."""
         flat = x.contiguous().view(-1).view(torch.uint8)
         nb = flat.numel()

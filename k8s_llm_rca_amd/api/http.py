@@ -261,6 +261,13 @@ def prometheus_text(service: AssistantService, engine=None) -> str:
                     if isinstance(v, (int, float)):
                         yield CounterMetricFamily(f"k8srca_engine_{k}", f"engine counter {k}", value=float(v))
                 yield GaugeMetricFamily("k8srca_kv_free_blocks", "free KV blocks", value=engine.kv.free_blocks)
+                host = getattr(engine, "kv_host", None)
+                if host is not None:  # the KV host tier (engine/kv_offload.py)
+                    yield GaugeMetricFamily("k8srca_kv_host_free_blocks", "free KV host-tier blocks",
+                                            value=host.free_slots)
+                    yield GaugeMetricFamily("k8srca_kv_host_pending_blocks",
+                                            "HBM pages whose swap-out copy is still in flight",
+                                            value=host.pending_blocks)
 
     reg = CollectorRegistry()
     reg.register(_Collector())

@@ -91,3 +91,15 @@ def test_release_frees_host_slots():
     for sid in list(eng.seqs):
         eng.release_sequence(sid)
     assert eng.kv_host.free_slots == 64 and eng.kv.free_blocks == 12
+
+
+def test_prometheus_reports_host_tier():
+    from k8s_llm_rca_amd.api.http import prometheus_text
+    from k8s_llm_rca_amd.api.service import AssistantService
+    from k8s_llm_rca_amd.engine.backend import EngineBackend
+    ref = _engine(num_blocks=256)
+    per = KVPool.bytes_per_block(ref.mc.n_layers, ref.model.nkv, ref.model.D, 32, elem=4)
+    eng = _engine(num_blocks=12, kv_host_gb=16 * per / (1 << 30), kv_host_watermark=2)
+    _rounds(eng, rounds=1)
+    txt = prometheus_text(AssistantService(EngineBackend(eng)), eng)
+    assert "k8srca_kv_host_free_blocks" in txt and "k8srca_engine_swap_outs" in txt

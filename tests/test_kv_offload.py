@@ -103,3 +103,40 @@ def test_prometheus_reports_host_tier():
     _rounds(eng, rounds=1)
     txt = prometheus_text(AssistantService(EngineBackend(eng)), eng)
     assert "k8srca_kv_host_free_blocks" in txt and "k8srca_engine_swap_outs" in txt
+
+
+class _Ev:
+    """A copy-completion event stand-in (CPU): done once ``done`` is set."""
+    def __init__(self):
+        self.done = False
+
+    def query(self):
+        return self.done
+
+    def synchronize(self):
+        self.done = True
+
+
+def test_pages_under_a_swap_in_are_released_only_after_it_lands():
+    """A thread dropped while its swap-in copy is still on the copy stream (a
+    cancelled run, a released thread) gives its pages back only once the copy
+    has landed, and it is never chosen for eviction or preemption meanwhile."""
+    from k8s_llm_rca_amd.engine.types import Sequence
+    ref = _engine(num_blocks=256)
+    per = KVPool.bytes_per_block(ref.mc.n_layers, ref.model.nkv, ref.model.D, 32, elem=4)
+    eng = _engine(num_blocks=12, kv_host_gb=8 * per / (1 << 30), kv_host_watermark=0)
+    kvm = eng.kvm
+    s = Sequence(eng.new_sequence())
+    eng.seqs[s.id] = s
+    s.blocks = eng.kv.alloc(3)
+    ev = _Ev()
+    s.loading = ev
+    assert kvm.loading(s)
+    kvm.evict(12, set())            # an idle thread under a swap-in is not evicted
+    assert len(s.blocks) == 3
+    free0 = eng.kv.free_blocks
+    kvm.drop(s)                     # e.g. its run was cancelled mid-copy
+    assert s.blocks == [] and s.loading is None and eng.kv.free_blocks == free0
+    assert eng.kv_host.poll() == 0 and eng.kv.free_blocks == free0   # still being written
+    ev.done = True
+    assert eng.kv_host.poll() == 3 and eng.kv.free_blocks == free0 + 3

@@ -22,6 +22,7 @@ every run (``/root/reference/common/openai_generic_assistant.py:45-51``).
 """
 from __future__ import annotations
 
+from collections import Counter
 from typing import Callable, Dict, List, Optional
 
 from .kv_cache import KVPool, chain_key
@@ -35,7 +36,7 @@ class KVCacheManager:
         self.host = host                # KVHostTier or None
         self.watermark = watermark      # swap ahead while free + in-flight pages are below this
         self.snapshot = snapshot        # the engine's sequences (thread-safe copy)
-        self.stats = stats if stats is not None else {}
+        self.stats = stats if stats is not None else Counter()  # standalone: counters start at 0
         self.BS = pool.block_size
 
     # ------------------------------------------------------------ admission

@@ -472,7 +472,40 @@ __global__ void __launch_bounds__(64, 2) attn_decode_items_kernel(AttnArgs a) {
 // the (m, l) loads, instead of after the max / weights exchange; the exchange
 // and the summation are the LDS form's own (bit-identical).  Longer rows take
 // the LDS form below.
-constexpr int kRedPre = 16;
+// Rows of up to 16 partitions (the many-row steps) take the 16-load form; up to
+// 32 (one or a few rows over long contexts: 27 at one row x 5k keys, which had
+// fallen to the LDS form's serial loads) the 32-load form -- the same arithmetic.
+constexpr int kRedPre = 32;
+template <int NPRE>
+__device__ __forceinline__ void reduce_pre(const AttnArgs& a, size_t base, int np, int qh, int seq, int d, float* sf,
+                                           float* sl, float* scratch) {
+  // the partial-O column of every partition in flight first (clamped: unconditional),
+  // then the LDS form's own max / weights exchange, so the arithmetic is the same
+  float po[NPRE];
+#pragma unroll
+  for (int p = 0; p < NPRE; ++p) po[p] = a.part_o[(base + min(p, np - 1)) * D + d];
+  float M = d < np ? a.part_ml[(base + d) * 2] : -INFINITY;
+  M = block_max(M, scratch);
+  float f = 0.f, lf = 0.f;
+  if (d < np) {
+    const float m = a.part_ml[(base + d) * 2];
+    f = (m == -INFINITY) ? 0.f : exp2f(m - M);
+    lf = a.part_ml[(base + d) * 2 + 1] * f;
+  }
+  sf[d] = f;
+  sl[d] = lf;
+  __syncthreads();
+  float L = 0.f, acc = 0.f;
+#pragma unroll
+  for (int j = 0; j < NPRE; ++j)
+    if (j < np) {
+      L += sl[j];
+      acc = fmaf(po[j], sf[j], acc);  // explicit: an unrolled, predicated a * b + c may not contract
+    }
+  const int qrow = a.q_start[seq];
+  a.out[(size_t)qrow * a.out_stride + qh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+}
+
 template <bool PRE>
 __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   __shared__ float sf[128], sl[128], scratch[16];
@@ -482,32 +515,12 @@ __global__ void __launch_bounds__(128) attn_reduce_kernel(AttnArgs a) {
   const int np = min(a.n_parts, (ctx + part_size - 1) / part_size);
   if (np <= 1 && a.items) return;  // work-list mode: whole rows were written by the decode kernel
   const size_t base = ((size_t)seq * a.nq + qh) * a.n_parts;
-  if (PRE && np >= 1 && np <= kRedPre) {  // (np == 0, an empty row: the LDS form writes its zero)
-    // the partial-O column of every partition in flight first (clamped: unconditional),
-    // then the LDS form's own max / weights exchange, so the arithmetic is the same
-    float po[kRedPre];
-#pragma unroll
-    for (int p = 0; p < kRedPre; ++p) po[p] = a.part_o[(base + min(p, np - 1)) * D + d];
-    float M = d < np ? a.part_ml[(base + d) * 2] : -INFINITY;
-    M = block_max(M, scratch);
-    float f = 0.f, lf = 0.f;
-    if (d < np) {
-      const float m = a.part_ml[(base + d) * 2];
-      f = (m == -INFINITY) ? 0.f : exp2f(m - M);
-      lf = a.part_ml[(base + d) * 2 + 1] * f;
-    }
-    sf[d] = f;
-    sl[d] = lf;
-    __syncthreads();
-    float L = 0.f, acc = 0.f;
-#pragma unroll
-    for (int j = 0; j < kRedPre; ++j)
-      if (j < np) {
-        L += sl[j];
-        acc = fmaf(po[j], sf[j], acc);  // explicit: an unrolled, predicated a * b + c may not contract
-      }
-    const int qrow = a.q_start[seq];
-    a.out[(size_t)qrow * a.out_stride + qh * D + d] = f2bf(L > 0.f ? acc / L : 0.f);
+  if (PRE && np >= 1 && np <= 16) {  // (np == 0, an empty row: the LDS form writes its zero)
+    reduce_pre<16>(a, base, np, qh, seq, d, sf, sl, scratch);
+    return;
+  }
+  if (PRE && np > 16 && np <= kRedPre) {
+    reduce_pre<kRedPre>(a, base, np, qh, seq, d, sf, sl, scratch);
     return;
   }
   float M = -INFINITY;
